@@ -1,0 +1,152 @@
+/*
+ * omf_codec.h — C ABI of the MI355X-native OmniFed gradient-compression codec.
+ *
+ * Drop-in boundary for the hybrid engine's global gRPC hop.  The reference is
+ * pure Python/PyTorch (no native code, no FFI): its codec entry points are the
+ * Python functions cited on each declaration below
+ * (paths relative to at-aaims/OmniFed).  The Python host layer
+ * `omnifed_amd.hybrid.compression` / `omnifed_amd.hybrid.communicator.
+ * global_grpc_compression` keeps those names and signatures and binds this ABI
+ * with ctypes (INTEGRATION.md shows the binding).
+ *
+ * Conventions
+ *  - Every pointer argument is DEVICE memory owned by the caller unless noted.
+ *    The library allocates only in omf_plan_create (its own workspace); the
+ *    hot-path calls never allocate, copy host memory or synchronise.
+ *  - `stream` is a hipStream_t (NULL = the legacy default stream).  Calls are
+ *    asynchronous on that stream; results are ready when the stream is.
+ *  - Return value: 0 (OMF_OK) or a negative OMF_E* code; the message for the
+ *    calling thread is in omf_last_error().  No C++ exception crosses the ABI.
+ *  - Reentrant: no global mutable state.  A plan's workspace is used by one
+ *    call at a time (one plan per stream/thread in flight).
+ *
+ * Data layout ("update arena"): the named tensors of one client, flattened in
+ * named_parameters() order into one fp32 buffer, tensor t occupying elements
+ * [offsets[t], offsets[t] + sizes[t]).  offsets[t] must be a multiple of 4
+ * (16-byte aligned starts; gaps between tensors are padding that is never
+ * read as data).  Payload arenas (int8 / int32 QSGD levels, fp32 decoded
+ * values) use the SAME element offsets.  Base pointers: fp32 and int32 buffers
+ * 16-byte aligned, int8 buffers 4-byte aligned.
+ */
+#ifndef OMF_CODEC_H
+#define OMF_CODEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OMF_OK 0
+#define OMF_EINVAL (-1)   /* bad argument (maps to Python ValueError) */
+#define OMF_EHIP (-2)     /* HIP runtime error */
+#define OMF_ETIMEOUT (-3) /* an in-kernel wait hit its bound (reported by omf_plan_check) */
+#define OMF_ENOMEM (-4)
+
+typedef struct omf_plan omf_plan;
+
+/* ABI version (major*100 + minor). */
+int omf_abi_version(void);
+
+/* Last error message of the calling thread ("" if none). */
+const char* omf_last_error(void);
+
+/*
+ * Plan over a fixed list of named tensors (one client's update dict).
+ * sizes/offsets are HOST arrays of ntensors elements; chunk_elems is the work
+ * unit of one workgroup (0 = default 16384; must be a multiple of 16384).
+ * Tensors of <= 16384 elements are processed by one workgroup each.
+ * Replaces the per-call Python loop of encode_updates_dict /
+ * decode_updates_dict (src/omnifed/hybrid/communicator/global_grpc_compression.py:207-223).
+ */
+int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntensors,
+                    int64_t chunk_elems, int device, omf_plan** out);
+int omf_plan_destroy(omf_plan* plan);
+/* Number of workgroups one encode launch uses (diagnostics / roofline bookkeeping). */
+int64_t omf_plan_encode_items(const omf_plan* plan);
+/* Synchronise `stream` and report an in-kernel wait timeout (OMF_ETIMEOUT) if one occurred. */
+int omf_plan_check(omf_plan* plan, void* stream);
+
+/*
+ * QSGD encode, all tensors of the plan in ONE launch.
+ * Replaces QSGDQuantCompression.quantize_vector / compress
+ * (src/omnifed/hybrid/compression/qsgd.py:36-82) as called per tensor by
+ * _encode_qsgd_layer (global_grpc_compression.py:101-123), with the client
+ * weighting of GrpcCommunicator.aggregate (global_grpc.py:101-123) fused in:
+ *   xs = fl32(x * alpha)                      (alpha = 1.0f: identity)
+ *   norm[t] = fp32 L2 norm of xs over tensor t  (or norm_in[t] if norm_in != NULL)
+ *   q_i = sign(xs_i/norm) * clamp(floor(|xs_i/norm|*L) + (u_i < frac), 0, L),  L = 2^bit_width
+ * bit_width in [0, 30]; payload element = int8 if L <= 127 else int32 (qsgd.py:18-21).
+ * u: NULL = on-device Philox4x32-10 uniforms from (seed, offset) — see
+ * oracle/philox.py for the exact counter layout; non-NULL = caller-supplied
+ * fp32 uniforms in the arena layout (parity mode, e.g. the MT19937 stream of
+ * torch.rand_like).  A zero norm yields an all-zero payload (the Python layer
+ * then emits the reference's dense passthrough LayerState).
+ * norm_out (ntensors fp32) receives the norm used for every tensor.
+ */
+int omf_qsgd_encode(omf_plan* plan, const float* x, float alpha, int32_t bit_width,
+                    const float* u, uint64_t seed, uint64_t offset, const float* norm_in,
+                    void* q_out, float* norm_out, void* stream);
+
+/* Only the per-tensor norms of xs = fl32(x*alpha) (parity-mode helper: lets the host
+ * know which tensors consume MT19937 draws before it builds u). */
+int omf_qsgd_norms(omf_plan* plan, const float* x, float alpha, float* norm_out, void* stream);
+
+/*
+ * QSGD decode, all tensors in one launch.
+ * Replaces QSGDQuantCompression.decompress_quantized (qsgd.py:84-96) as called by
+ * _decode_qsgd_layer (global_grpc_compression.py:163-182), and — with
+ * accumulate != 0 — the PS accumulate step acc[name] += update
+ * (src/omnifed/hybrid/communicator/global_grpc_server.py:147-153):
+ *   y_i = fl32(fl32(norm[t] * q_i) / fl32(levels));   accumulate: y_out_i = fl32(y_out_i + y_i)
+ * width: 8 (int8 payload) or 32 (int32), the LayerState.width field; levels > 0 is
+ * LayerState.level (any positive value; powers of two take an exact multiply path).
+ */
+int omf_qsgd_decode(omf_plan* plan, const void* q, int32_t width, int32_t levels, const float* norm,
+                    float* y_out, int32_t accumulate, void* stream);
+
+/*
+ * y_i = fl32(y_i / divisor) over n elements (PS averaging,
+ * CentralServerServicer._apply_model_updates, global_grpc_server.py:155-171).
+ */
+int omf_div_f32(float* y, int64_t n, float divisor, void* stream);
+
+/*
+ * Top-K sparsification with error feedback, all tensors of the plan in one call.
+ * Replaces TopKCompression.compress (src/omnifed/hybrid/compression/topk.py:33-42)
+ * with ResidualUpdates.compensate/update (src/omnifed/hybrid/compression/core.py:26-37)
+ * and topk_sparse (topk.py:10-15):
+ *   residual_mode 0: t' = x                       (no error-feedback state)
+ *   residual_mode 1: t' = residual + x, then residual := t' - desparse(selection)
+ *   residual_mode 2: t' = x,            then residual := t' - desparse(selection)
+ *                    (first call for a name: the reference has no residual yet)
+ *   k_t = max(1, int(n_t * ratio))  (omf_topk_k); the k_t largest |t'| of tensor t;
+ *   values (fp32 t') / indices (tensor-local int64) of tensor t are written at
+ *   [K_t, K_t + k_t) with K_t = sum_{u<t} k_u (packed in plan order).
+ * Order within a tensor: descending |t'|, ties by ascending index (torch.topk's
+ * order for k*64 <= n on the reference CPU path; ties there are unspecified).
+ * ws: caller workspace of omf_topk_workspace_bytes(plan, ratio) bytes.
+ */
+int64_t omf_topk_k(int64_t numel, double ratio);
+size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio);
+int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,
+                    float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * Top-K decode of ONE tensor of n elements: topk_desparse (topk.py:18-21),
+ * _decode_topk_layer (global_grpc_compression.py:140-160) and the sparse
+ * scatter-add of layerwise_decompress (core.py:62-71):
+ *   mode 0: y := 0, then y[idx_j] = val_j       (PS uplink decode)
+ *   mode 1: y[idx_j] = val_j, y holds the base  (client overlay decode)
+ *   mode 2: y[idx_j] += val_j                   (scatter-add; indices unique per call)
+ * Indices outside [0, n) are skipped.
+ */
+int omf_topk_decode(const float* values, const int64_t* indices, int64_t k, float* y,
+                    int64_t n, int32_t mode, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* OMF_CODEC_H */

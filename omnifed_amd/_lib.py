@@ -1,0 +1,84 @@
+"""ctypes binding of ``libomf_codec.so`` (declarations: ``include/omf_codec.h``).
+
+There is no CPU fallback: if the library is missing, ``lib()`` raises.  The
+library is built in-tree by ``omnifed_amd.build`` and loaded from
+``omnifed_amd/libomf_codec.so`` so that the driver can see which native code
+ran.  ctypes releases the GIL for the duration of every call.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from .build import LIB as LIB_PATH
+
+OMF_OK = 0
+OMF_EINVAL = -1
+OMF_EHIP = -2
+OMF_ETIMEOUT = -3
+OMF_ENOMEM = -4
+
+_c_i32 = ctypes.c_int32
+_c_i64 = ctypes.c_int64
+_c_u64 = ctypes.c_uint64
+_c_f32 = ctypes.c_float
+_c_f64 = ctypes.c_double
+_c_p = ctypes.c_void_p
+_c_size = ctypes.c_size_t
+
+# name -> (restype, argtypes); every symbol include/omf_codec.h declares.
+SIGNATURES = {
+    "omf_abi_version": (ctypes.c_int, []),
+    "omf_last_error": (ctypes.c_char_p, []),
+    "omf_plan_create": (ctypes.c_int, [ctypes.POINTER(_c_i64), ctypes.POINTER(_c_i64), _c_i32, _c_i64,
+                                        ctypes.c_int, ctypes.POINTER(_c_p)]),
+    "omf_plan_destroy": (ctypes.c_int, [_c_p]),
+    "omf_plan_encode_items": (_c_i64, [_c_p]),
+    "omf_plan_check": (ctypes.c_int, [_c_p, _c_p]),
+    "omf_qsgd_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p, _c_p, _c_p]),
+    "omf_qsgd_norms": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_p]),
+    "omf_qsgd_decode": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
+    "omf_div_f32": (ctypes.c_int, [_c_p, _c_i64, _c_f32, _c_p]),
+    "omf_topk_k": (_c_i64, [_c_i64, _c_f64]),
+    "omf_topk_workspace_bytes": (_c_size, [_c_p, _c_f64]),
+    "omf_topk_encode": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_f64, _c_p, _c_p, _c_p, _c_size, _c_p]),
+    "omf_topk_decode": (ctypes.c_int, [_c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i32, _c_p]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class CodecError(RuntimeError):
+    pass
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP codec library; raise if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise CodecError(
+                    f"HIP codec library not built: {LIB_PATH} is missing "
+                    "(run `python -m omnifed_amd.build`); there is no CPU fallback")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc == OMF_OK:
+        return
+    msg = lib().omf_last_error().decode(errors="replace")
+    if rc == OMF_EINVAL:
+        raise ValueError(f"{what}: {msg}")
+    raise CodecError(f"{what} failed ({rc}): {msg}")

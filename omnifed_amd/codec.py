@@ -1,0 +1,271 @@
+"""Device codec: the Python face of ``libomf_codec.so`` over torch device tensors.
+
+An *update arena* is one fp32 device buffer holding every named tensor of a
+client, tensor t at ``[offsets[t], offsets[t] + sizes[t])`` (``arena_layout``
+pads every start to a multiple of 64 elements = 256 B).  All kernels process a
+whole arena per launch; payload arenas (int8/int32 levels, decoded fp32) share
+the element offsets.  Every function validates shapes, dtypes, devices and
+alignment on the host before anything is launched: a kernel never sees a
+buffer shorter than the plan assumes.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import torch
+
+from ._lib import check, lib
+
+ALIGN_ELEMS = 64
+
+
+def arena_layout(sizes: Sequence[int], align: int = ALIGN_ELEMS) -> Tuple[List[int], int]:
+    """Offsets (multiples of ``align``) and total length of an arena holding ``sizes``."""
+    offs, cur = [], 0
+    for n in sizes:
+        offs.append(cur)
+        cur += (int(n) + align - 1) // align * align
+    return offs, max(cur, align)
+
+
+def storage_width(levels: int) -> int:
+    """qsgd.py:18-21: payload bits per element (8 while levels <= 127, else 32)."""
+    return 8 if levels <= 127 else 32
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _need(t: torch.Tensor, name: str, dtype, device, numel: int, align: int):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name}: dtype {t.dtype}, expected {dtype}")
+    if t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if t.numel() < numel:
+        raise ValueError(f"{name}: {t.numel()} elements, plan needs {numel}")
+    if t.data_ptr() % align:
+        raise ValueError(f"{name} must be {align}-byte aligned")
+
+
+class Plan:
+    """An ``omf_plan`` over fixed tensor sizes/offsets on one device (cached, reusable)."""
+
+    _cache: Dict[tuple, "Plan"] = {}
+    _cache_lock = threading.Lock()
+
+    def __init__(self, sizes: Sequence[int], offsets: Optional[Sequence[int]] = None,
+                 device: Optional[torch.device] = None, chunk: int = 0):
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.type != "cuda":
+            raise ValueError("the codec runs on a GPU device")
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        self.sizes = [int(n) for n in sizes]
+        if offsets is None:
+            offsets, _ = arena_layout(self.sizes)
+        self.offsets = [int(o) for o in offsets]
+        if len(self.sizes) != len(self.offsets) or not self.sizes:
+            raise ValueError("sizes and offsets must be non-empty and of equal length")
+        self.nt = len(self.sizes)
+        self.device = device
+        self.chunk = int(chunk)
+        self.arena_end = self.offsets[-1] + self.sizes[-1]
+        L = lib()
+        n = self.nt
+        szs = (ctypes.c_int64 * n)(*self.sizes)
+        ofs = (ctypes.c_int64 * n)(*self.offsets)
+        h = ctypes.c_void_p()
+        check(L.omf_plan_create(szs, ofs, n, self.chunk, device.index, ctypes.byref(h)), "omf_plan_create")
+        self._h = h
+        self._lock = threading.Lock()
+        self._topk_ws: Optional[torch.Tensor] = None
+
+    @classmethod
+    def get(cls, sizes, offsets=None, device=None, chunk: int = 0) -> "Plan":
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        device = torch.device(device)
+        if device.index is None:
+            device = torch.device("cuda", torch.cuda.current_device())
+        if offsets is None:
+            offsets, _ = arena_layout(sizes)
+        key = (tuple(int(s) for s in sizes), tuple(int(o) for o in offsets), str(device), int(chunk))
+        with cls._cache_lock:
+            p = cls._cache.get(key)
+            if p is None:
+                p = cls(sizes, offsets, device, chunk)
+                cls._cache[key] = p
+            return p
+
+    @property
+    def handle(self):
+        return self._h
+
+    @property
+    def encode_items(self) -> int:
+        return int(lib().omf_plan_encode_items(self._h))
+
+    def check(self, stream: Optional[int] = None) -> None:
+        check(lib().omf_plan_check(self._h, ctypes.c_void_p(stream if stream is not None else _stream(self.device))),
+              "omf_plan_check")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                lib().omf_plan_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    # ------------------------------------------------------------ QSGD
+    def qsgd_encode(self, x: torch.Tensor, bit_width: int, q_out: Optional[torch.Tensor] = None,
+                    norm_out: Optional[torch.Tensor] = None, alpha: float = 1.0,
+                    u: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
+                    norm_in: Optional[torch.Tensor] = None, stream: Optional[int] = None):
+        """Encode the whole arena ``x``; returns ``(q, norms)`` (device tensors)."""
+        s = int(bit_width)
+        if not 0 <= s <= 30:
+            raise ValueError("bit_width must be in [0, 30]")
+        width = storage_width(2 ** s)
+        qdt = torch.int8 if width == 8 else torch.int32
+        dev = self.device
+        _need(x, "x", torch.float32, dev, self.arena_end, 16)
+        if q_out is None:
+            q_out = torch.empty(self.arena_end, dtype=qdt, device=dev)
+        _need(q_out, "q_out", qdt, dev, self.arena_end, 4 if width == 8 else 16)
+        if norm_out is None:
+            norm_out = torch.empty(self.nt, dtype=torch.float32, device=dev)
+        _need(norm_out, "norm_out", torch.float32, dev, self.nt, 4)
+        if u is not None:
+            _need(u, "u", torch.float32, dev, self.arena_end, 16)
+        if norm_in is not None:
+            _need(norm_in, "norm_in", torch.float32, dev, self.nt, 4)
+        st = stream if stream is not None else _stream(dev)
+        with self._lock:
+            check(lib().omf_qsgd_encode(self._h, _ptr(x), float(alpha), s, _ptr(u),
+                                        int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset) & 0xFFFFFFFFFFFFFFFF,
+                                        _ptr(norm_in), _ptr(q_out), _ptr(norm_out), ctypes.c_void_p(st)),
+                  "omf_qsgd_encode")
+        return q_out, norm_out
+
+    def qsgd_norms(self, x: torch.Tensor, alpha: float = 1.0, norm_out: Optional[torch.Tensor] = None,
+                   stream: Optional[int] = None) -> torch.Tensor:
+        dev = self.device
+        _need(x, "x", torch.float32, dev, self.arena_end, 16)
+        if norm_out is None:
+            norm_out = torch.empty(self.nt, dtype=torch.float32, device=dev)
+        _need(norm_out, "norm_out", torch.float32, dev, self.nt, 4)
+        st = stream if stream is not None else _stream(dev)
+        with self._lock:
+            check(lib().omf_qsgd_norms(self._h, _ptr(x), float(alpha), _ptr(norm_out), ctypes.c_void_p(st)),
+                  "omf_qsgd_norms")
+        return norm_out
+
+    def qsgd_decode(self, q: torch.Tensor, width: int, levels: int, norm: torch.Tensor,
+                    y_out: Optional[torch.Tensor] = None, accumulate: bool = False,
+                    stream: Optional[int] = None) -> torch.Tensor:
+        width, levels = int(width), int(levels)
+        if width not in (8, 32):
+            raise ValueError(f"unsupported width={width}")
+        if levels <= 0:
+            raise ValueError(f"invalid level={levels}")
+        dev = self.device
+        qdt = torch.int8 if width == 8 else torch.int32
+        _need(q, "q", qdt, dev, self.arena_end, 4 if width == 8 else 16)
+        _need(norm, "norm", torch.float32, dev, self.nt, 4)
+        if y_out is None:
+            if accumulate:
+                raise ValueError("accumulate=True needs y_out")
+            y_out = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
+        _need(y_out, "y_out", torch.float32, dev, self.arena_end, 16)
+        st = stream if stream is not None else _stream(dev)
+        check(lib().omf_qsgd_decode(self._h, _ptr(q), width, levels, _ptr(norm), _ptr(y_out),
+                                    1 if accumulate else 0, ctypes.c_void_p(st)), "omf_qsgd_decode")
+        return y_out
+
+    # ------------------------------------------------------------ Top-K
+    def topk_ks(self, ratio: float) -> List[int]:
+        L = lib()
+        return [int(L.omf_topk_k(n, float(ratio))) for n in self.sizes]
+
+    def topk_encode(self, x: torch.Tensor, ratio: float, residual: Optional[torch.Tensor] = None,
+                    residual_mode: int = 0, values: Optional[torch.Tensor] = None,
+                    indices: Optional[torch.Tensor] = None, stream: Optional[int] = None):
+        """Returns ``(values, indices, ks)``; tensor t's selection at ``[sum(ks[:t]), +ks[t])``."""
+        dev = self.device
+        ks = self.topk_ks(ratio)
+        for n, k in zip(self.sizes, ks):
+            if k > n:
+                raise ValueError("selected index k out of range: compress_ratio too large")
+        K = sum(ks)
+        _need(x, "x", torch.float32, dev, self.arena_end, 16)
+        if residual_mode not in (0, 1, 2):
+            raise ValueError("residual_mode must be 0, 1 or 2")
+        if residual_mode:
+            if residual is None:
+                raise ValueError("residual_mode != 0 needs a residual buffer")
+            _need(residual, "residual", torch.float32, dev, self.arena_end, 16)
+        if values is None:
+            values = torch.empty(K, dtype=torch.float32, device=dev)
+        if indices is None:
+            indices = torch.empty(K, dtype=torch.int64, device=dev)
+        _need(values, "values", torch.float32, dev, K, 4)
+        _need(indices, "indices", torch.int64, dev, K, 8)
+        L = lib()
+        need = int(L.omf_topk_workspace_bytes(self._h, float(ratio)))
+        st = stream if stream is not None else _stream(dev)
+        with self._lock:
+            if self._topk_ws is None or self._topk_ws.numel() < need:
+                self._topk_ws = torch.empty(need, dtype=torch.uint8, device=dev)
+            check(L.omf_topk_encode(self._h, _ptr(x), _ptr(residual) if residual_mode else None, int(residual_mode),
+                                    float(ratio), _ptr(values), _ptr(indices), _ptr(self._topk_ws),
+                                    ctypes.c_size_t(self._topk_ws.numel()), ctypes.c_void_p(st)),
+                  "omf_topk_encode")
+        return values, indices, ks
+
+
+def div_(y: torch.Tensor, divisor: float, stream: Optional[int] = None) -> torch.Tensor:
+    """In-place ``y /= divisor`` (fp32 IEEE division) on the GPU."""
+    if y.dtype != torch.float32 or not y.is_cuda or not y.is_contiguous() or y.data_ptr() % 16:
+        raise ValueError("div_: y must be a contiguous, 16-byte aligned fp32 CUDA tensor")
+    st = stream if stream is not None else _stream(y.device)
+    check(lib().omf_div_f32(_ptr(y), y.numel(), float(divisor), ctypes.c_void_p(st)), "omf_div_f32")
+    return y
+
+
+def topk_decode(values: torch.Tensor, indices: torch.Tensor, n: int, y: Optional[torch.Tensor] = None,
+                mode: int = 0, stream: Optional[int] = None) -> torch.Tensor:
+    """Scatter decode of one tensor: mode 0 zeros+set, 1 overlay on ``y``, 2 scatter-add into ``y``."""
+    dev = values.device
+    if not dev.type == "cuda":
+        raise ValueError("topk_decode runs on a GPU device")
+    if values.dtype != torch.float32 or indices.dtype != torch.int64:
+        raise ValueError("values must be fp32 and indices int64")
+    values = values.contiguous()
+    indices = indices.to(dev).contiguous()
+    if values.numel() != indices.numel():
+        raise ValueError("values and indices differ in length")
+    if y is None:
+        if mode != 0:
+            raise ValueError("mode 1/2 need y")
+        y = torch.empty(int(n), dtype=torch.float32, device=dev)
+    _need(y, "y", torch.float32, dev, int(n), 4)
+    st = stream if stream is not None else _stream(dev)
+    check(lib().omf_topk_decode(_ptr(values), _ptr(indices), values.numel(), _ptr(y), int(n), int(mode),
+                                ctypes.c_void_p(st)), "omf_topk_decode")
+    return y
