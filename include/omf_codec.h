@@ -65,8 +65,23 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
 int omf_plan_destroy(omf_plan* plan);
 /* Number of workgroups one encode launch uses (diagnostics / roofline bookkeeping). */
 int64_t omf_plan_encode_items(const omf_plan* plan);
-/* Synchronise `stream` and report an in-kernel wait timeout (OMF_ETIMEOUT) if one occurred. */
+/* Synchronise `stream` and report an in-kernel wait timeout (OMF_ETIMEOUT) if one occurred;
+ * returns 1 (results still exact) when the resident encoder had to recompute a norm. */
 int omf_plan_check(omf_plan* plan, void* stream);
+/* Encoder strategy: 0 = register-resident items for tensors of at most
+ * omf_plan_resident_capacity() items (x read once; the workgroup holds its 16 Ki elements
+ * while the tensor norm is published) and two-pass items for larger tensors;
+ * 1 (default) = two-pass for every tensor (x re-read after the norm; measured faster on
+ * MI355X, where waiting workgroups idle their slots — DESIGN.md §4).  Identical payloads given the
+ * norm; the norms fold partials over different item sizes, so they agree to rounding. */
+int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy);
+/* Largest tensor (in 16 Ki-element items) that takes the register-resident path: half the
+ * encoder's co-resident workgroups (occupancy x CUs). */
+int64_t omf_plan_resident_capacity(const omf_plan* plan);
+/* Tuning / test hook: cap > 0 replaces the capacity (rebuilds the item sequence; not for
+ * the hot path); wait_us > 0 bounds each norm wait (default 20 ms) after which a workgroup
+ * recomputes the norm itself (exact, reported by omf_plan_check). */
+int omf_plan_set_resident_capacity(omf_plan* plan, int64_t cap, int64_t wait_us);
 
 /*
  * QSGD encode, all tensors of the plan in ONE launch.

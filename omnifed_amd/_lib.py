@@ -37,6 +37,9 @@ SIGNATURES = {
     "omf_plan_destroy": (ctypes.c_int, [_c_p]),
     "omf_plan_encode_items": (_c_i64, [_c_p]),
     "omf_plan_check": (ctypes.c_int, [_c_p, _c_p]),
+    "omf_plan_set_encode_strategy": (ctypes.c_int, [_c_p, _c_i32]),
+    "omf_plan_resident_capacity": (_c_i64, [_c_p]),
+    "omf_plan_set_resident_capacity": (ctypes.c_int, [_c_p, _c_i64, _c_i64]),
     "omf_qsgd_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p, _c_p, _c_p]),
     "omf_qsgd_norms": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_p]),
     "omf_qsgd_decode": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
@@ -62,11 +65,12 @@ def lib() -> ctypes.CDLL:
         return _lib
     with _lock:
         if _lib is None:
-            if not os.path.exists(LIB_PATH):
+            path = os.environ.get("OMF_CODEC_LIB_EXPERIMENT") or LIB_PATH  # variant builds (scripts/exp)
+            if not os.path.exists(path):
                 raise CodecError(
                     f"HIP codec library not built: {LIB_PATH} is missing "
                     "(run `python -m omnifed_amd.build`); there is no CPU fallback")
-            L = ctypes.CDLL(LIB_PATH)
+            L = ctypes.CDLL(path)
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(L, name)
                 fn.restype = res

@@ -119,9 +119,27 @@ class Plan:
     def encode_items(self) -> int:
         return int(lib().omf_plan_encode_items(self._h))
 
-    def check(self, stream: Optional[int] = None) -> None:
-        check(lib().omf_plan_check(self._h, ctypes.c_void_p(stream if stream is not None else _stream(self.device))),
-              "omf_plan_check")
+    def check(self, stream: Optional[int] = None) -> bool:
+        """Synchronise; raise on an in-kernel timeout.  Returns False if the resident encoder
+        had to recompute a norm (results exact, but the grid was not co-resident)."""
+        rc = lib().omf_plan_check(self._h, ctypes.c_void_p(stream if stream is not None else _stream(self.device)))
+        if rc == 1:
+            return False
+        check(rc, "omf_plan_check")
+        return True
+
+    @property
+    def resident_capacity(self) -> int:
+        return int(lib().omf_plan_resident_capacity(self._h))
+
+    def set_resident_capacity(self, cap: int = 0, wait_us: int = 0) -> None:
+        """Tuning / test hook: see omf_plan_set_resident_capacity."""
+        check(lib().omf_plan_set_resident_capacity(self._h, int(cap), int(wait_us)), "omf_plan_set_resident_capacity")
+
+    def set_encode_strategy(self, strategy: str) -> None:
+        """'resident' (x read once where it fits, default) or 'ordered' (two-pass everywhere)."""
+        code = {"resident": 0, "ordered": 1}[strategy]
+        check(lib().omf_plan_set_encode_strategy(self._h, code), "omf_plan_set_encode_strategy")
 
     def __del__(self):
         h = getattr(self, "_h", None)

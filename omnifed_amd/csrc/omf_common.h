@@ -70,21 +70,60 @@ __device__ __forceinline__ uint32_t add_agent(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ void drain_vmem() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Philox4x32-10 (Salmon et al., SC'11).  Counter layout: oracle/philox.py.
+// Each round's two 32x32->64 products are single 64-bit multiplies (v_mad_u64_u32).
+#ifndef OMF_PHILOX_ROUNDS
+#define OMF_PHILOX_ROUNDS 10
+#endif
 __device__ __forceinline__ uint4 philox4x32_10(uint4 c, uint32_t k0, uint32_t k1) {
 #pragma unroll
-  for (int r = 0; r < 10; ++r) {
+  for (int r = 0; r < OMF_PHILOX_ROUNDS; ++r) {
     if (r) {
       k0 += 0x9E3779B9u;
       k1 += 0xBB67AE85u;
     }
-    const uint32_t hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
-    const uint32_t hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
-    c = make_uint4(hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0);
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c.x;
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c.z;
+    c = make_uint4((uint32_t)(p1 >> 32) ^ c.y ^ k0, (uint32_t)p1, (uint32_t)(p0 >> 32) ^ c.w ^ k1, (uint32_t)p0);
   }
   return c;
 }
 
 // 24-bit uniform in [0,1): the torch CPU generator's rule.
 __device__ __forceinline__ float u24(uint32_t w) { return (float)(w & 0xFFFFFFu) * 5.9604644775390625e-08f; }
+
+// Four 24-bit uniforms from three consecutive 32-bit words (96 bits, little-endian fields).
+__device__ __forceinline__ float4 u24x4(uint32_t w0, uint32_t w1, uint32_t w2) {
+  return make_float4(u24(w0), u24(__builtin_amdgcn_alignbit(w1, w0, 24)), u24(__builtin_amdgcn_alignbit(w2, w1, 16)),
+                     (float)(w2 >> 8) * 5.9604644775390625e-08f);
+}
+
+// Correctly rounded x / d from r = RN(1/d): Markstein's theorem (one Newton step brings
+// q within 1 ulp, the second fma-corrected step rounds correctly).  Valid for d in
+// [2^-100, 2^100] and |x| >= 2^-96 or x == 0; callers take x / d elsewhere
+// (scripts/exp/div_check.c: 0 mismatches in 1e9 random and near-halfway cases).
+__device__ __forceinline__ float div_markstein(float x, float d, float r) {
+  float q = __fmul_rn(x, r);
+  float e = fmaf(-q, d, x);
+  q = fmaf(e, r, q);
+  e = fmaf(-q, d, x);
+  return fmaf(e, r, q);
+}
+
+__device__ __forceinline__ bool div_needs_exact(float x) {
+  const float a = fabsf(x);
+  return a != 0.0f && !(a >= 0x1p-96f);  // tiny non-zero (or NaN): exact division
+}
+
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_nt(float* p, float4 v) {
+  f32x4_t t = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(t, reinterpret_cast<f32x4_t*>(p));
+}
+__device__ __forceinline__ void store_nt(uint32_t* p, uint32_t v) { __builtin_nontemporal_store(v, p); }
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void store_nt(int32_t* p, int4 v) {
+  i32x4_t t = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(t, reinterpret_cast<i32x4_t*>(p));
+}
 
 }  // namespace omf

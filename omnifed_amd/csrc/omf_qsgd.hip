@@ -4,20 +4,23 @@
 //   src/omnifed/hybrid/compression/qsgd.py:36-96 (reference, Python/torch CPU).
 //
 // Kernel map:
-//   qsgd_encode_ordered  one launch for every tensor of a client.  Work items
-//                        (64 KiB of fp32 each) are taken in ticket order:
-//                        NORM(t) chunks publish fp64 partial sums of squares,
-//                        the last arriver folds them in fixed order into
-//                        norm[t] and publishes a {tag, norm} granule; QUANT(t)
-//                        chunks wait on that granule and re-read x (served by
-//                        the 256 MiB Infinity Cache: NORM(t+1) is the only
-//                        traffic in between); tensors of <= 16 Ki elements are
-//                        one FUSED item (norm + quantise from registers).
+//   qsgd_encode_ordered  one launch for every tensor of a client.  Work items are
+//                        taken in ticket order (an atomic counter, so a workgroup
+//                        only ever waits on items that are already running):
+//                        RESIDENT(t)  16 Ki elements held in registers: publish the
+//                                     fp64 partial sum of squares, wait for the
+//                                     tensor norm, quantise from registers — x is
+//                                     read once (tensors of <= cap/2 items);
+//                        NORM(t)      chunk partial only (large tensors, pass 1);
+//                        QUANT(t)     wait for the norm, re-read, quantise (pass 2).
+//                        The last arriver of a tensor folds its partials in fixed
+//                        order (deterministic norm) and publishes a {tag, norm}
+//                        granule that the waiters poll.
 //   qsgd_quant_flat      norm supplied by the caller: one pass, no hand-off.
 //   qsgd_decode_flat     y = (norm * q) / L, optionally accumulated (PS).
 //
-// HBM-bound; no MFMA (no contraction).  Coalesced 16 B/lane fp32 loads and stores,
-// 4 B/lane int8 payload stores (one 256 B line per wave instruction).
+// HBM-bound; no MFMA (no contraction).  Coalesced 16 B/lane fp32 loads, non-temporal
+// 16 B/lane fp32 and 4 B/lane int8 payload stores.
 #include <algorithm>
 #include <cstring>
 #include <vector>
@@ -29,11 +32,11 @@ using namespace omf;
 
 namespace {
 
-constexpr int kV = 16;                          // float4 per thread per sub-chunk
+constexpr int kV = 16;                                // float4 per thread per sub-chunk
 constexpr int64_t kSub = (int64_t)kV * kThreads * 4;  // 16384 elements = 64 KiB fp32
-constexpr uint64_t kTimeoutTicks = 200000000ull;      // 2 s of the 100 MHz realtime clock
+constexpr uint64_t kWaitTicks = 2000000ull;           // 20 ms of the 100 MHz realtime clock
 
-enum : int32_t { kNorm = 0, kQuant = 1, kFused = 2 };
+enum : int32_t { kNorm = 0, kQuant = 1, kResident = 2 };
 
 struct Item {
   int64_t begin, end;  // arena element range of this work item
@@ -42,6 +45,7 @@ struct Item {
 
 struct TensorInfo {
   int64_t begin, n;
+  int64_t chunk;          // elements per item of this tensor
   int32_t nchunks, pbase;
 };
 
@@ -61,6 +65,7 @@ struct EncArgs {
   float alpha;
   float levels;  // 2^s as float (exact)
   uint32_t seed_lo, seed_hi, offset;
+  uint64_t wait_ticks;  // bounded norm wait (100 MHz ticks)
 };
 
 struct DecArgs {
@@ -74,32 +79,50 @@ struct DecArgs {
 
 // ---------------------------------------------------------------- element math
 
-// One QSGD level, qsgd.py:50-63.  xs / norm is IEEE division (hipcc default:
-// correctly rounded); the remaining steps are exact in fp32.  Out-of-range or NaN
-// magnitudes follow the reference's x86 float->int64 conversion (INT64_MIN, then
-// clamp to 0): the payload element is 0.
-__device__ __forceinline__ int32_t qsgd_level(float xs, float norm, float L, float u) {
-  const float vn = xs / norm;
+// One QSGD level from vn = xs / norm, qsgd.py:50-63: every step after the division is
+// exact in fp32.  Out-of-range or NaN magnitudes follow the reference's x86
+// float->int64 conversion (INT64_MIN, then clamp to 0): the payload element is 0.
+__device__ __forceinline__ int32_t qsgd_level(float vn, float L, float u) {
   const float a = fabsf(vn);
   const float sc = __fmul_rn(a, L);
-  int32_t mag = 0;
-  if (sc < 9.2233720e18f) {  // false for NaN / inf / >= 2^63
-    const float fl = floorf(sc);
-    const float p = __fsub_rn(sc, fl);
-    float m = fl + ((u < p) ? 1.0f : 0.0f);  // exact: p > 0 implies fl < 2^23
-    m = fminf(m, L);
-    mag = (int32_t)m;
-  }
+  const float fl = floorf(sc);
+  const float p = __fsub_rn(sc, fl);
+  float m = fl + ((u < p) ? 1.0f : 0.0f);  // exact: p > 0 implies fl < 2^23
+  m = fminf(m, L);
+  const int32_t mag = (sc < 9.2233720e18f) ? (int32_t)m : 0;  // false for NaN / inf / >= 2^63
   const int32_t sg = (vn > 0.0f) - (vn < 0.0f);
   return sg * mag;
 }
 
-template <int V>
+// Per-tensor divisor state: IEEE xs / norm, fast (Markstein) when norm is in range.
+struct Divisor {
+  float d, r;
+  bool fast;
+  __device__ __forceinline__ explicit Divisor(float norm) : d(norm), r(1.0f / norm) {
+    const float a = fabsf(norm);
+    fast = a >= 0x1p-100f && a <= 0x1p100f;
+  }
+  __device__ __forceinline__ float4 div4(float4 x) const {
+    if (!fast) return make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
+    float4 q = make_float4(div_markstein(x.x, d, r), div_markstein(x.y, d, r), div_markstein(x.z, d, r),
+                           div_markstein(x.w, d, r));
+    const bool need = div_needs_exact(x.x) | div_needs_exact(x.y) | div_needs_exact(x.z) | div_needs_exact(x.w);
+    if (__any(need)) {  // wave-uniform branch: tiny inputs take the exact division
+      if (div_needs_exact(x.x)) q.x = x.x / d;
+      if (div_needs_exact(x.y)) q.y = x.y / d;
+      if (div_needs_exact(x.z)) q.z = x.z / d;
+      if (div_needs_exact(x.w)) q.w = x.w / d;
+    }
+    return q;
+  }
+};
+
+template <int V, bool FULL>
 __device__ __forceinline__ void load_f4(const float* __restrict__ p, int64_t b, int64_t end, float4 (&v)[V]) {
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
-    if (e + 4 <= end) {
+    if (FULL || e + 4 <= end) {
       v[k] = *reinterpret_cast<const float4*>(p + e);
     } else {
       float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -135,139 +158,233 @@ __device__ __forceinline__ float sumsq_f4(const float4 (&v)[V], float acc) {
   return acc;
 }
 
+// Uniforms of rows k = 4g .. 4g+3 of this thread in a sub-chunk starting at b:
+// 3 Philox calls per 16 elements (oracle/philox.py: group G, 96-bit slots).
+__device__ __forceinline__ void philox_rows(const EncArgs& a, int64_t b, int64_t tbegin, int32_t tensor, int g,
+                                            float4 (&uu)[4]) {
+  const uint64_t G = ((uint64_t)((b - tbegin) >> 12) + (uint64_t)g) * (uint64_t)kThreads + threadIdx.x;
+  uint32_t w[12];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const uint64_t ctr = 3 * G + c;
+    const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)tensor, a.offset),
+                                  a.seed_lo, a.seed_hi);
+    w[4 * c] = r.x; w[4 * c + 1] = r.y; w[4 * c + 2] = r.z; w[4 * c + 3] = r.w;
+  }
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) uu[sl] = u24x4(w[3 * sl], w[3 * sl + 1], w[3 * sl + 2]);
+}
+
 // Quantise V float4 of one sub-chunk starting at b (tensor t begins at tbegin) and store.
-template <int WIDTH, bool HAS_U, int V>
+// FULL: the sub-chunk is complete (no bounds checks).
+template <int WIDTH, bool HAS_U, bool FULL, int V>
 __device__ __forceinline__ void quant_store(const float4 (&v)[V], const EncArgs& a, int64_t b, int64_t end,
                                             int64_t tbegin, int32_t tensor, float norm) {
-  float4 uu[V];
-  if (HAS_U) {
-    load_f4<V>(a.u, b, end, uu);
-  } else {
-#pragma unroll
-    for (int k = 0; k < V; ++k) {
-      const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
-      const uint64_t j = (uint64_t)(e - tbegin) >> 2;
-      const uint4 r = philox4x32_10(make_uint4((uint32_t)j, (uint32_t)(j >> 32), (uint32_t)tensor, a.offset),
-                                    a.seed_lo, a.seed_hi);
-      uu[k] = make_float4(u24(r.x), u24(r.y), u24(r.z), u24(r.w));
-    }
-  }
+  static_assert(V % 4 == 0, "rows come in groups of 4 (RNG slots)");
   const bool zero = !(norm != 0.0f);  // norm == 0: all-zero payload (reference: dense passthrough)
+  const Divisor dv(norm);
 #pragma unroll
-  for (int k = 0; k < V; ++k) {
-    const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
-    if (e >= end) continue;
-    int32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-    if (!zero) {
-      q0 = qsgd_level(v[k].x, norm, a.levels, uu[k].x);
-      q1 = qsgd_level(v[k].y, norm, a.levels, uu[k].y);
-      q2 = qsgd_level(v[k].z, norm, a.levels, uu[k].z);
-      q3 = qsgd_level(v[k].w, norm, a.levels, uu[k].w);
-    }
-    if (WIDTH == 1) {
-      int8_t* q8 = reinterpret_cast<int8_t*>(a.q);
-      if (e + 4 <= end) {
-        const uint32_t packed = (uint32_t)(uint8_t)q0 | ((uint32_t)(uint8_t)q1 << 8) |
-                                ((uint32_t)(uint8_t)q2 << 16) | ((uint32_t)(uint8_t)q3 << 24);
-        *reinterpret_cast<uint32_t*>(q8 + e) = packed;
-      } else {
-        q8[e] = (int8_t)q0;
-        if (e + 1 < end) q8[e + 1] = (int8_t)q1;
-        if (e + 2 < end) q8[e + 2] = (int8_t)q2;
+  for (int g = 0; g < V / 4; ++g) {
+    float4 uu[4];
+    if (HAS_U) {
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) {
+        const int64_t e = b + 4 * ((int64_t)(4 * g + sl) * kThreads + threadIdx.x);
+        if (FULL || e + 4 <= end) {
+          uu[sl] = *reinterpret_cast<const float4*>(a.u + e);
+        } else {
+          uu[sl] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (e < end) uu[sl].x = a.u[e];
+          if (e + 1 < end) uu[sl].y = a.u[e + 1];
+          if (e + 2 < end) uu[sl].z = a.u[e + 2];
+        }
       }
     } else {
-      int32_t* q32 = reinterpret_cast<int32_t*>(a.q);
-      if (e + 4 <= end) {
-        *reinterpret_cast<int4*>(q32 + e) = make_int4(q0, q1, q2, q3);
+#ifdef OMF_EXP_NORNG  // experiment builds only: price the RNG
+      for (int sl = 0; sl < 4; ++sl) uu[sl] = make_float4(0.5f, 0.25f, 0.75f, 0.125f);
+#else
+      philox_rows(a, b, tbegin, tensor, g, uu);
+#endif
+    }
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      const int k = 4 * g + sl;
+      const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+      if (!FULL && e >= end) continue;
+      int32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
+      if (!zero) {
+#ifdef OMF_EXP_NODIV  // experiment builds only: price the exact division
+        const float4 vn = make_float4(v[k].x * dv.r, v[k].y * dv.r, v[k].z * dv.r, v[k].w * dv.r);
+#else
+        const float4 vn = dv.div4(v[k]);
+#endif
+        q0 = qsgd_level(vn.x, a.levels, uu[sl].x);
+        q1 = qsgd_level(vn.y, a.levels, uu[sl].y);
+        q2 = qsgd_level(vn.z, a.levels, uu[sl].z);
+        q3 = qsgd_level(vn.w, a.levels, uu[sl].w);
+      }
+      if (WIDTH == 1) {
+        int8_t* q8 = reinterpret_cast<int8_t*>(a.q);
+        if (FULL || e + 4 <= end) {
+          const uint32_t packed = (uint32_t)(uint8_t)q0 | ((uint32_t)(uint8_t)q1 << 8) |
+                                  ((uint32_t)(uint8_t)q2 << 16) | ((uint32_t)(uint8_t)q3 << 24);
+          store_nt(reinterpret_cast<uint32_t*>(q8 + e), packed);
+        } else {
+          q8[e] = (int8_t)q0;
+          if (e + 1 < end) q8[e + 1] = (int8_t)q1;
+          if (e + 2 < end) q8[e + 2] = (int8_t)q2;
+        }
       } else {
-        q32[e] = q0;
-        if (e + 1 < end) q32[e + 1] = q1;
-        if (e + 2 < end) q32[e + 2] = q2;
+        int32_t* q32 = reinterpret_cast<int32_t*>(a.q);
+        if (FULL || e + 4 <= end) {
+          store_nt(q32 + e, make_int4(q0, q1, q2, q3));
+        } else {
+          q32[e] = q0;
+          if (e + 1 < end) q32[e + 1] = q1;
+          if (e + 2 < end) q32[e + 2] = q2;
+        }
       }
     }
   }
 }
 
-__device__ __forceinline__ float wait_norm(const EncArgs& a, int32_t t) {
-  const uint64_t t0 = wall_clock64();
-  for (;;) {
-    const uint64_t g = ld_agent(&a.gran[t]);
-    if ((g >> 32) == 1u) return __uint_as_float((uint32_t)g);
-    if (wall_clock64() - t0 > kTimeoutTicks) {
-      __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      return __uint_as_float(0x7fc00000u);
-    }
-    __builtin_amdgcn_s_sleep(2);
+// Load + scale + quantise + store one sub-chunk [b, e).
+template <int WIDTH, bool HAS_U>
+__device__ __forceinline__ void quant_sub(const EncArgs& a, int64_t b, int64_t e, int64_t tbegin, int32_t tensor,
+                                          float norm) {
+  float4 v[kV];
+  if (e - b == kSub) {
+    load_f4<kV, true>(a.x, b, e, v);
+    scale_f4<kV>(v, a.alpha);
+    quant_store<WIDTH, HAS_U, true, kV>(v, a, b, e, tbegin, tensor, norm);
+  } else {
+    load_f4<kV, false>(a.x, b, e, v);
+    scale_f4<kV>(v, a.alpha);
+    quant_store<WIDTH, HAS_U, false, kV>(v, a, b, e, tbegin, tensor, norm);
   }
+}
+
+// ---------------------------------------------------------------- norm hand-off
+
+// Sum of squares of one item's range, exactly as a NORM item computes it: sub-chunks in
+// order, each thread accumulating its own rows in fp32.
+__device__ __forceinline__ float chunk_sumsq(const EncArgs& a, int64_t b, int64_t e) {
+  float acc = 0.0f;
+  for (int64_t sb = b; sb < e; sb += kSub) {
+    const int64_t se = min(sb + kSub, e);
+    float4 v[kV];
+    if (se - sb == kSub) load_f4<kV, true>(a.x, sb, se, v);
+    else load_f4<kV, false>(a.x, sb, se, v);
+    scale_f4<kV>(v, a.alpha);
+    acc = sumsq_f4<kV>(v, acc);
+  }
+  return acc;
+}
+
+struct HandoffShared {
+  double red[kWaves];
+  uint32_t last, ok;
+  float norm;
+};
+
+// Publish one item's partial; the last arriver of the tensor folds all partials in a fixed
+// order (deterministic norm) and publishes the {tag = 1, norm} granule.  Protocol
+// (cdna_hip_programming.md §6 G16): partial stored sc1 and drained before the
+// agent-scope counter add; the last arriver reads the partials with sc1 loads.
+__device__ __forceinline__ void publish_partial(const EncArgs& a, const TensorInfo& ti, int32_t t, int32_t idx,
+                                                float acc, HandoffShared& sh) {
+  const double s = block_sum_f64((double)acc, sh.red);
+  if (threadIdx.x == 0) {
+    st_agent(&a.partials[ti.pbase + idx], (uint64_t)__double_as_longlong(s));
+    drain_vmem();
+    const uint32_t old = add_agent(&a.counters[t], 1u);
+    sh.last = (old == (uint32_t)(ti.nchunks - 1)) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (sh.last) {
+    double p = 0.0;
+    for (int j = threadIdx.x; j < ti.nchunks; j += kThreads)
+      p += __longlong_as_double((long long)ld_agent(&a.partials[ti.pbase + j]));
+    const double tot = block_sum_f64(p, sh.red);
+    if (threadIdx.x == 0) {
+      const float norm = sqrtf((float)tot);
+      a.norm_out[t] = norm;
+      st_agent(&a.gran[t], (1ull << 32) | (uint64_t)__float_as_uint(norm));
+    }
+  }
+}
+
+// Poll the tensor's granule (one lane, relaxed sc1 loads, bounded).  On timeout (the
+// tensor's items were not all co-resident) recompute every partial exactly as its owner
+// does and fold them in the last arriver's order: identical bits, err bit 2 set.
+__device__ __forceinline__ float norm_wait_or_recompute(const EncArgs& a, const TensorInfo& ti, int32_t t,
+                                                        HandoffShared& sh) {
+  if (threadIdx.x == 0) {
+    const uint64_t t0 = wall_clock64();
+    uint32_t ok = 0;
+    float nv = 0.0f;
+    for (;;) {
+      const uint64_t g = ld_agent(&a.gran[t]);
+      if ((g >> 32) == 1u) {
+        nv = __uint_as_float((uint32_t)g);
+        ok = 1;
+        break;
+      }
+      if (wall_clock64() - t0 > a.wait_ticks) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+    sh.norm = nv;
+    sh.ok = ok;
+  }
+  __syncthreads();
+  const float nv = sh.norm;
+  const uint32_t ok = sh.ok;
+  __syncthreads();
+  if (ok) return nv;
+  double p = 0.0;
+  for (int j = 0; j < ti.nchunks; ++j) {
+    const int64_t b = ti.begin + (int64_t)j * ti.chunk, e = min(b + ti.chunk, ti.begin + ti.n);
+    const double sj = block_sum_f64((double)chunk_sumsq(a, b, e), sh.red);
+    if ((j % kThreads) == (int)threadIdx.x) p += sj;
+  }
+  const double tot = block_sum_f64(p, sh.red);
+  if (threadIdx.x == 0) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return sqrtf((float)tot);
 }
 
 // ---------------------------------------------------------------- kernels
 
 template <int WIDTH, bool HAS_U, bool NORM_ONLY>
 __global__ __launch_bounds__(kThreads) void qsgd_encode_ordered(EncArgs a) {
-  __shared__ double s_red[kWaves];
+  __shared__ HandoffShared sh;
   __shared__ uint32_t s_ticket;
-  __shared__ uint32_t s_last;
-  __shared__ float s_norm;
-  const int tid = threadIdx.x;
-  if (tid == 0) s_ticket = add_agent(a.ticket, 1u);
+  if (threadIdx.x == 0) s_ticket = add_agent(a.ticket, 1u);
   __syncthreads();
   const Item it = a.items[s_ticket];
   const TensorInfo ti = a.tinfo[it.tensor];
 
-  if (it.kind == kQuant) {
+  if (it.kind == kResident) {  // one sub-chunk, x read once
+    const bool full = (it.end - it.begin) == kSub;
+    float4 v[kV];
+    if (full) load_f4<kV, true>(a.x, it.begin, it.end, v);
+    else load_f4<kV, false>(a.x, it.begin, it.end, v);
+    scale_f4<kV>(v, a.alpha);
+    publish_partial(a, ti, it.tensor, it.chunk, sumsq_f4<kV>(v, 0.0f), sh);
     if (NORM_ONLY) return;
-    if (tid == 0) s_norm = wait_norm(a, it.tensor);
-    __syncthreads();
-    const float norm = s_norm;
-    for (int64_t b = it.begin; b < it.end; b += kSub) {
-      const int64_t e = min(b + kSub, it.end);
-      float4 v[kV];
-      load_f4<kV>(a.x, b, e, v);
-      scale_f4<kV>(v, a.alpha);
-      quant_store<WIDTH, HAS_U, kV>(v, a, b, e, ti.begin, it.tensor, norm);
-    }
+    const float norm = norm_wait_or_recompute(a, ti, it.tensor, sh);
+    if (full) quant_store<WIDTH, HAS_U, true, kV>(v, a, it.begin, it.end, ti.begin, it.tensor, norm);
+    else quant_store<WIDTH, HAS_U, false, kV>(v, a, it.begin, it.end, ti.begin, it.tensor, norm);
     return;
   }
-
   if (it.kind == kNorm) {
-    float acc = 0.0f;
-    for (int64_t b = it.begin; b < it.end; b += kSub) {
-      const int64_t e = min(b + kSub, it.end);
-      float4 v[kV];
-      load_f4<kV>(a.x, b, e, v);
-      scale_f4<kV>(v, a.alpha);
-      acc = sumsq_f4<kV>(v, acc);
-    }
-    const double s = block_sum_f64((double)acc, s_red);
-    if (tid == 0) {
-      st_agent(&a.partials[ti.pbase + it.chunk], (uint64_t)__double_as_longlong(s));
-      drain_vmem();  // partial globally visible before the arrival count
-      const uint32_t old = add_agent(&a.counters[it.tensor], 1u);
-      s_last = (old == (uint32_t)(ti.nchunks - 1)) ? 1u : 0u;
-    }
-    __syncthreads();
-    if (!s_last) return;
-    // Last arriver: fold the partials in a fixed order (deterministic norm).
-    double p = 0.0;
-    for (int j = tid; j < ti.nchunks; j += kThreads) p += __longlong_as_double((long long)ld_agent(&a.partials[ti.pbase + j]));
-    const double tot = block_sum_f64(p, s_red);
-    if (tid == 0) {
-      const float norm = sqrtf((float)tot);
-      a.norm_out[it.tensor] = norm;
-      st_agent(&a.gran[it.tensor], (1ull << 32) | (uint64_t)__float_as_uint(norm));
-    }
+    publish_partial(a, ti, it.tensor, it.chunk, chunk_sumsq(a, it.begin, it.end), sh);
     return;
   }
-
-  // kFused: whole tensor (<= kSub elements) in registers.
-  float4 v[kV];
-  load_f4<kV>(a.x, it.begin, it.end, v);
-  scale_f4<kV>(v, a.alpha);
-  const double s = block_sum_f64((double)sumsq_f4<kV>(v, 0.0f), s_red);
-  const float norm = sqrtf((float)s);
-  if (tid == 0) a.norm_out[it.tensor] = norm;
-  if (!NORM_ONLY) quant_store<WIDTH, HAS_U, kV>(v, a, it.begin, it.end, ti.begin, it.tensor, norm);
+  // kQuant: second pass of a large tensor.
+  if (NORM_ONLY) return;
+  const float norm = norm_wait_or_recompute(a, ti, it.tensor, sh);
+  for (int64_t b = it.begin; b < it.end; b += kSub)
+    quant_sub<WIDTH, HAS_U>(a, b, min(b + kSub, it.end), ti.begin, it.tensor, norm);
 }
 
 template <int WIDTH, bool HAS_U>
@@ -276,12 +393,75 @@ __global__ __launch_bounds__(kThreads) void qsgd_quant_flat(EncArgs a) {
   const TensorInfo ti = a.tinfo[it.tensor];
   const float norm = a.norm_in[it.tensor];
   if (it.chunk == 0 && threadIdx.x == 0) a.norm_out[it.tensor] = norm;
-  for (int64_t b = it.begin; b < it.end; b += kSub) {
-    const int64_t e = min(b + kSub, it.end);
-    float4 v[kV];
-    load_f4<kV>(a.x, b, e, v);
-    scale_f4<kV>(v, a.alpha);
-    quant_store<WIDTH, HAS_U, kV>(v, a, b, e, ti.begin, it.tensor, norm);
+  for (int64_t b = it.begin; b < it.end; b += kSub)
+    quant_sub<WIDTH, HAS_U>(a, b, min(b + kSub, it.end), ti.begin, it.tensor, norm);
+}
+
+// Decode one sub-chunk [b, end): y = fl32(fl32(norm * q) / L) (optionally acc += y).
+template <int WIDTH, bool ACC, bool POW2, bool FULL>
+__device__ __forceinline__ void decode_sub(const DecArgs& a, int64_t b, int64_t end, float norm) {
+  int32_t raw[kV][WIDTH == 1 ? 1 : 4];
+#pragma unroll
+  for (int k = 0; k < kV; ++k) {
+    const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+    if (WIDTH == 1) {
+      const int8_t* q8 = reinterpret_cast<const int8_t*>(a.q);
+      if (FULL || e + 4 <= end) {
+        raw[k][0] = *reinterpret_cast<const int32_t*>(q8 + e);
+      } else {
+        uint32_t t = 0;
+        if (e < end) t |= (uint32_t)(uint8_t)q8[e];
+        if (e + 1 < end) t |= (uint32_t)(uint8_t)q8[e + 1] << 8;
+        if (e + 2 < end) t |= (uint32_t)(uint8_t)q8[e + 2] << 16;
+        raw[k][0] = (int32_t)t;
+      }
+    } else {
+      const int32_t* q32 = reinterpret_cast<const int32_t*>(a.q);
+      if (FULL || e + 4 <= end) {
+        const int4 t = *reinterpret_cast<const int4*>(q32 + e);
+        raw[k][0] = t.x; raw[k][1] = t.y; raw[k][2] = t.z; raw[k][3] = t.w;
+      } else {
+        raw[k][0] = (e < end) ? q32[e] : 0;
+        raw[k][1] = (e + 1 < end) ? q32[e + 1] : 0;
+        raw[k][2] = (e + 2 < end) ? q32[e + 2] : 0;
+        raw[k][3] = 0;
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kV; ++k) {
+    const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+    if (!FULL && e >= end) continue;
+    int32_t qi[4];
+    if (WIDTH == 1) {
+      qi[0] = (int32_t)(int8_t)(raw[k][0] & 0xff);
+      qi[1] = (int32_t)(int8_t)((raw[k][0] >> 8) & 0xff);
+      qi[2] = (int32_t)(int8_t)((raw[k][0] >> 16) & 0xff);
+      qi[3] = (int32_t)(int8_t)((raw[k][0] >> 24) & 0xff);
+    } else {
+      qi[0] = raw[k][0]; qi[1] = raw[k][1]; qi[2] = raw[k][2]; qi[3] = raw[k][3];
+    }
+    // (norm * q) / 2^s == (norm * q) * 2^-s exactly (power-of-two scaling, both correctly rounded).
+    float yv[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float nq = __fmul_rn(norm, (float)qi[c]);
+      yv[c] = POW2 ? __fmul_rn(nq, a.inv_levels) : nq / a.levels;
+    }
+    float* y = a.y + e;
+    if (FULL || e + 4 <= end) {
+      float4 o = make_float4(yv[0], yv[1], yv[2], yv[3]);
+      if (ACC) {
+        const float4 prev = *reinterpret_cast<const float4*>(y);
+        o.x = __fadd_rn(prev.x, o.x); o.y = __fadd_rn(prev.y, o.y);
+        o.z = __fadd_rn(prev.z, o.z); o.w = __fadd_rn(prev.w, o.w);
+      }
+      store_nt(y, o);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 3; ++c)
+        if (e + c < end) y[c] = ACC ? __fadd_rn(y[c], yv[c]) : yv[c];
+    }
   }
 }
 
@@ -291,69 +471,8 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_flat(DecArgs a) {
   const float norm = a.norm[it.tensor];
   for (int64_t b = it.begin; b < it.end; b += kSub) {
     const int64_t end = min(b + kSub, it.end);
-    int32_t raw[kV][WIDTH == 1 ? 1 : 4];
-#pragma unroll
-    for (int k = 0; k < kV; ++k) {
-      const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
-      if (WIDTH == 1) {
-        const int8_t* q8 = reinterpret_cast<const int8_t*>(a.q);
-        if (e + 4 <= end) {
-          raw[k][0] = *reinterpret_cast<const int32_t*>(q8 + e);
-        } else {
-          uint32_t t = 0;
-          if (e < end) t |= (uint32_t)(uint8_t)q8[e];
-          if (e + 1 < end) t |= (uint32_t)(uint8_t)q8[e + 1] << 8;
-          if (e + 2 < end) t |= (uint32_t)(uint8_t)q8[e + 2] << 16;
-          raw[k][0] = (int32_t)t;
-        }
-      } else {
-        const int32_t* q32 = reinterpret_cast<const int32_t*>(a.q);
-        if (e + 4 <= end) {
-          const int4 t = *reinterpret_cast<const int4*>(q32 + e);
-          raw[k][0] = t.x; raw[k][1] = t.y; raw[k][2] = t.z; raw[k][3] = t.w;
-        } else {
-          raw[k][0] = (e < end) ? q32[e] : 0;
-          raw[k][1] = (e + 1 < end) ? q32[e + 1] : 0;
-          raw[k][2] = (e + 2 < end) ? q32[e + 2] : 0;
-          raw[k][3] = 0;
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kV; ++k) {
-      const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
-      if (e >= end) continue;
-      int32_t qi[4];
-      if (WIDTH == 1) {
-        qi[0] = (int32_t)(int8_t)(raw[k][0] & 0xff);
-        qi[1] = (int32_t)(int8_t)((raw[k][0] >> 8) & 0xff);
-        qi[2] = (int32_t)(int8_t)((raw[k][0] >> 16) & 0xff);
-        qi[3] = (int32_t)(int8_t)((raw[k][0] >> 24) & 0xff);
-      } else {
-        qi[0] = raw[k][0]; qi[1] = raw[k][1]; qi[2] = raw[k][2]; qi[3] = raw[k][3];
-      }
-      // (norm * q) / 2^s == (norm * q) * 2^-s exactly (power-of-two scaling, both correctly rounded).
-      float yv[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const float nq = __fmul_rn(norm, (float)qi[c]);
-        yv[c] = POW2 ? __fmul_rn(nq, a.inv_levels) : nq / a.levels;
-      }
-      float* y = a.y + e;
-      if (e + 4 <= end) {
-        float4 o = make_float4(yv[0], yv[1], yv[2], yv[3]);
-        if (ACC) {
-          const float4 prev = *reinterpret_cast<const float4*>(y);
-          o.x = __fadd_rn(prev.x, o.x); o.y = __fadd_rn(prev.y, o.y);
-          o.z = __fadd_rn(prev.z, o.z); o.w = __fadd_rn(prev.w, o.w);
-        }
-        *reinterpret_cast<float4*>(y) = o;
-      } else {
-#pragma unroll
-        for (int c = 0; c < 3; ++c)
-          if (e + c < end) y[c] = ACC ? __fadd_rn(y[c], yv[c]) : yv[c];
-      }
-    }
+    if (end - b == kSub) decode_sub<WIDTH, ACC, POW2, true>(a, b, end, norm);
+    else decode_sub<WIDTH, ACC, POW2, false>(a, b, end, norm);
   }
 }
 
@@ -379,16 +498,20 @@ struct omf_plan {
   int32_t nt = 0;
   int64_t chunk = kSub;
   std::vector<int64_t> sizes, offsets;
-  int64_t n_enc = 0, n_flat = 0, n_partials = 0;
-  void* d_block = nullptr;  // one allocation: items, tensor info, partials, sync words
-  Item* d_enc = nullptr;
+  int64_t arena_end = 0;
+  int64_t cap = 0;               // tensors of <= cap items take the register-resident path
+  int32_t strategy = 1;          // 0 register-resident + two-pass, 1 two-pass only (default: faster on MI355X)
+  uint64_t wait_ticks = kWaitTicks;
+  int64_t n_enc[2] = {0, 0};
+  Item* d_enc[2] = {nullptr, nullptr};
+  TensorInfo* d_tinfo[2] = {nullptr, nullptr};
+  int64_t n_flat = 0, n_partials = 0;
   Item* d_flat = nullptr;
-  TensorInfo* d_tinfo = nullptr;
   uint64_t* d_partials = nullptr;
   int64_t* d_sizes = nullptr;   // per-tensor element counts (Top-K)
   int64_t* d_begins = nullptr;  // per-tensor arena offsets (Top-K)
-  int64_t arena_end = 0;
-  uint8_t* d_sync = nullptr;  // [ticket u32, err u32, pad 8][counters u32 x nt, pad16][granules u64 x nt, pad16]
+  void* d_block = nullptr;      // one allocation for everything above
+  uint8_t* d_sync = nullptr;    // [ticket u32, err u32, pad 8][counters u32 x nt, pad16][granules u64 x nt, pad16]
   size_t sync_bytes = 0, off_counters = 16, off_gran = 0;
 };
 
@@ -410,6 +533,103 @@ static size_t round16(size_t b) { return (b + 15) & ~(size_t)15; }
 
 static bool aligned(const void* p, size_t a) { return ((uintptr_t)p % a) == 0; }
 
+// Ticket-order item sequence.  Register-resident tensors (<= cap items of kSub) are
+// emitted in place; a larger tensor emits its NORM items in place and its QUANT items
+// after the next tensor's items (one tensor of slack for the norm hand-off).
+static void build_sequence(const omf_plan& p, bool resident_ok, std::vector<Item>& seq,
+                           std::vector<TensorInfo>& tinfo, int64_t& npart) {
+  seq.clear();
+  tinfo.assign(p.nt, TensorInfo{});
+  npart = 0;
+  std::vector<Item> deferred;
+  for (int32_t t = 0; t < p.nt; ++t) {
+    const int64_t n = p.sizes[t], b = p.offsets[t];
+    const int64_t ns = (n + kSub - 1) / kSub;
+    std::vector<Item> q_t;
+    if (ns == 1 || (resident_ok && ns <= p.cap)) {
+      tinfo[t] = TensorInfo{b, n, kSub, (int32_t)ns, (int32_t)npart};
+      for (int64_t c = 0; c < ns; ++c) {
+        const int64_t cb = b + c * kSub;
+        seq.push_back(Item{cb, std::min(b + n, cb + kSub), t, kResident, (int32_t)c, 0});
+      }
+      npart += ns;
+    } else {
+      const int64_t nc = (n + p.chunk - 1) / p.chunk;
+      tinfo[t] = TensorInfo{b, n, p.chunk, (int32_t)nc, (int32_t)npart};
+      for (int64_t c = 0; c < nc; ++c) {
+        const int64_t cb = b + c * p.chunk, ce = std::min(b + n, cb + p.chunk);
+        seq.push_back(Item{cb, ce, t, kNorm, (int32_t)c, 0});
+        q_t.push_back(Item{cb, ce, t, kQuant, (int32_t)c, 0});
+      }
+      npart += nc;
+    }
+    seq.insert(seq.end(), deferred.begin(), deferred.end());
+    deferred.swap(q_t);
+  }
+  seq.insert(seq.end(), deferred.begin(), deferred.end());
+}
+
+// (Re)build both sequences and upload every table into one device allocation.
+static int upload_plan(omf_plan* p) {
+  std::vector<Item> seq[2], flat;
+  std::vector<TensorInfo> tinfo[2];
+  int64_t np[2];
+  build_sequence(*p, true, seq[0], tinfo[0], np[0]);
+  build_sequence(*p, false, seq[1], tinfo[1], np[1]);
+  for (int32_t t = 0; t < p->nt; ++t) {
+    const int64_t n = p->sizes[t], b = p->offsets[t];
+    for (int64_t c = 0; c * p->chunk < n; ++c) {
+      const int64_t cb = b + c * p->chunk;
+      flat.push_back(Item{cb, std::min(b + n, cb + p->chunk), t, kQuant, (int32_t)c, 0});
+    }
+  }
+  if ((int64_t)std::max(seq[0].size(), flat.size()) > 0x7fffffffLL) return fail(OMF_EINVAL, "too many work items");
+  p->n_enc[0] = (int64_t)seq[0].size();
+  p->n_enc[1] = (int64_t)seq[1].size();
+  p->n_flat = (int64_t)flat.size();
+  p->n_partials = std::max<int64_t>(std::max(np[0], np[1]), 1);
+  p->off_counters = 16;
+  p->off_gran = round16(p->off_counters + 4 * (size_t)p->nt);
+  p->sync_bytes = round16(p->off_gran + 8 * (size_t)p->nt);
+  // the sync block starts the allocation (its per-call memset is 16-byte aligned and sized)
+  size_t o = round16(p->sync_bytes);
+  const size_t o_enc0 = o; o = round16(o + sizeof(Item) * seq[0].size());
+  const size_t o_enc1 = o; o = round16(o + sizeof(Item) * seq[1].size());
+  const size_t o_flat = o; o = round16(o + sizeof(Item) * flat.size());
+  const size_t o_ti0 = o; o = round16(o + sizeof(TensorInfo) * p->nt);
+  const size_t o_ti1 = o; o = round16(o + sizeof(TensorInfo) * p->nt);
+  const size_t o_part = o; o = round16(o + 8 * (size_t)p->n_partials);
+  const size_t o_sizes = o; o = round16(o + 8 * (size_t)p->nt);
+  const size_t o_begins = o; o = round16(o + 8 * (size_t)p->nt);
+  DeviceGuard g(p->device);
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  if (p->d_block) {
+    OMF_HIP(hipDeviceSynchronize());
+    (void)hipFree(p->d_block);
+    p->d_block = nullptr;
+  }
+  OMF_HIP(hipMalloc(&p->d_block, o));
+  uint8_t* base = static_cast<uint8_t*>(p->d_block);
+  p->d_sync = base;
+  p->d_enc[0] = reinterpret_cast<Item*>(base + o_enc0);
+  p->d_enc[1] = reinterpret_cast<Item*>(base + o_enc1);
+  p->d_flat = reinterpret_cast<Item*>(base + o_flat);
+  p->d_tinfo[0] = reinterpret_cast<TensorInfo*>(base + o_ti0);
+  p->d_tinfo[1] = reinterpret_cast<TensorInfo*>(base + o_ti1);
+  p->d_partials = reinterpret_cast<uint64_t*>(base + o_part);
+  p->d_sizes = reinterpret_cast<int64_t*>(base + o_sizes);
+  p->d_begins = reinterpret_cast<int64_t*>(base + o_begins);
+  OMF_HIP(hipMemcpy(p->d_enc[0], seq[0].data(), sizeof(Item) * seq[0].size(), hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_enc[1], seq[1].data(), sizeof(Item) * seq[1].size(), hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_flat, flat.data(), sizeof(Item) * flat.size(), hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_tinfo[0], tinfo[0].data(), sizeof(TensorInfo) * p->nt, hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_tinfo[1], tinfo[1].data(), sizeof(TensorInfo) * p->nt, hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_sizes, p->sizes.data(), 8 * (size_t)p->nt, hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_begins, p->offsets.data(), 8 * (size_t)p->nt, hipMemcpyHostToDevice));
+  OMF_HIP(hipMemset(p->d_sync, 0, p->sync_bytes));
+  return OMF_OK;
+}
+
 extern "C" {
 
 int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntensors, int64_t chunk_elems, int device,
@@ -420,6 +640,13 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
   if (chunk_elems == 0) chunk_elems = kSub;
   if (chunk_elems < kSub || chunk_elems % kSub != 0)
     return fail(OMF_EINVAL, "omf_plan_create: chunk_elems must be a positive multiple of 16384");
+  for (int32_t t = 0; t < ntensors; ++t) {
+    if (sizes[t] <= 0 || offsets[t] < 0 || (offsets[t] & 3))
+      return fail(OMF_EINVAL, "omf_plan_create: tensor " + std::to_string(t) +
+                                  ": size must be > 0 and offset a non-negative multiple of 4");
+    if (t > 0 && offsets[t] < offsets[t - 1] + sizes[t - 1])
+      return fail(OMF_EINVAL, "omf_plan_create: tensors must be ordered and non-overlapping");
+  }
   auto* p = new (std::nothrow) omf_plan();
   if (!p) return fail(OMF_ENOMEM, "omf_plan_create: host allocation failed");
   p->device = device;
@@ -427,94 +654,33 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
   p->chunk = chunk_elems;
   p->sizes.assign(sizes, sizes + ntensors);
   p->offsets.assign(offsets, offsets + ntensors);
-
-  std::vector<TensorInfo> tinfo(ntensors);
-  std::vector<Item> enc, flat;
-  std::vector<std::vector<Item>> quant(ntensors);
-  int64_t pbase = 0;
-  for (int32_t t = 0; t < ntensors; ++t) {
-    const int64_t n = sizes[t], b = offsets[t];
-    if (n <= 0 || b < 0 || (b & 3)) {
-      delete p;
-      return fail(OMF_EINVAL, "omf_plan_create: tensor " + std::to_string(t) +
-                                  ": size must be > 0 and offset a non-negative multiple of 4");
-    }
-    if (t > 0 && b < offsets[t - 1] + sizes[t - 1]) {
-      delete p;
-      return fail(OMF_EINVAL, "omf_plan_create: tensors must be ordered and non-overlapping");
-    }
-    TensorInfo ti{b, n, 0, (int32_t)pbase};
-    if (n <= kSub) {
-      ti.nchunks = 1;
-      Item f{b, b + n, t, kFused, 0, 0};
-      enc.push_back(f);
-      flat.push_back(Item{b, b + n, t, kQuant, 0, 0});
-    } else {
-      const int64_t nc = (n + chunk_elems - 1) / chunk_elems;
-      ti.nchunks = (int32_t)nc;
-      pbase += nc;
-      for (int64_t c = 0; c < nc; ++c) {
-        const int64_t cb = b + c * chunk_elems, ce = std::min(b + n, cb + chunk_elems);
-        enc.push_back(Item{cb, ce, t, kNorm, (int32_t)c, 0});
-        quant[t].push_back(Item{cb, ce, t, kQuant, (int32_t)c, 0});
-        flat.push_back(Item{cb, ce, t, kQuant, (int32_t)c, 0});
-      }
-    }
-    tinfo[t] = ti;
-    // QUANT(t-1) follows the producers of t: one tensor of slack for the norm hand-off.
-    if (t >= 1) enc.insert(enc.end(), quant[t - 1].begin(), quant[t - 1].end());
-  }
-  enc.insert(enc.end(), quant[ntensors - 1].begin(), quant[ntensors - 1].end());
-  p->n_enc = (int64_t)enc.size();
-  p->n_flat = (int64_t)flat.size();
-  p->n_partials = std::max<int64_t>(pbase, 1);
-  if (p->n_enc > 0x7fffffffLL) {
-    delete p;
-    return fail(OMF_EINVAL, "omf_plan_create: too many work items");
-  }
-
-  p->off_counters = 16;
-  p->off_gran = round16(p->off_counters + 4 * (size_t)ntensors);
-  p->sync_bytes = round16(p->off_gran + 8 * (size_t)ntensors);
-  // sync block first (its memset starts at the allocation start, multiple of 16 bytes)
-  const size_t o_sync = 0;
-  const size_t o_enc = round16(o_sync + p->sync_bytes);
-  const size_t o_flat = round16(o_enc + sizeof(Item) * enc.size());
-  const size_t o_tinfo = round16(o_flat + sizeof(Item) * flat.size());
-  const size_t o_part = round16(o_tinfo + sizeof(TensorInfo) * tinfo.size());
-  const size_t o_sizes = round16(o_part + 8 * (size_t)p->n_partials);
-  const size_t o_begins = round16(o_sizes + 8 * (size_t)ntensors);
-  const size_t total = round16(o_begins + 8 * (size_t)ntensors);
   p->arena_end = offsets[ntensors - 1] + sizes[ntensors - 1];
-
-  DeviceGuard g(device);
-  if (!g.ok) {
-    delete p;
-    return fail(OMF_EHIP, "omf_plan_create: hipSetDevice failed");
+  {
+    // Co-resident capacity of the encoder (occupancy x CUs over every instantiation); a
+    // tensor takes the register-resident path only with half of it as margin.
+    DeviceGuard g(device);
+    hipDeviceProp_t prop;
+    if (!g.ok || hipGetDeviceProperties(&prop, device) != hipSuccess) {
+      delete p;
+      return fail(OMF_EHIP, "omf_plan_create: cannot query the device");
+    }
+    const void* kerns[5] = {(const void*)qsgd_encode_ordered<1, false, false>,
+                            (const void*)qsgd_encode_ordered<1, true, false>,
+                            (const void*)qsgd_encode_ordered<4, false, false>,
+                            (const void*)qsgd_encode_ordered<4, true, false>,
+                            (const void*)qsgd_encode_ordered<1, false, true>};
+    int nb_min = 1 << 30;
+    for (int i = 0; i < 5; ++i) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kerns[i], kThreads, 0) != hipSuccess || nb < 1) nb = 1;
+      nb_min = std::min(nb_min, nb);
+    }
+    p->cap = std::max<int64_t>(1, (int64_t)nb_min * prop.multiProcessorCount / 2);
   }
-  hipError_t e = hipMalloc(&p->d_block, total);
-  if (e != hipSuccess) {
+  if (int r = upload_plan(p)) {
+    if (p->d_block) (void)hipFree(p->d_block);
     delete p;
-    return hip_fail(e, "hipMalloc(plan)");
-  }
-  uint8_t* base = static_cast<uint8_t*>(p->d_block);
-  p->d_sync = base + o_sync;
-  p->d_enc = reinterpret_cast<Item*>(base + o_enc);
-  p->d_flat = reinterpret_cast<Item*>(base + o_flat);
-  p->d_tinfo = reinterpret_cast<TensorInfo*>(base + o_tinfo);
-  p->d_partials = reinterpret_cast<uint64_t*>(base + o_part);
-  p->d_sizes = reinterpret_cast<int64_t*>(base + o_sizes);
-  p->d_begins = reinterpret_cast<int64_t*>(base + o_begins);
-  e = hipMemcpy(p->d_enc, enc.data(), sizeof(Item) * enc.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_flat, flat.data(), sizeof(Item) * flat.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_tinfo, tinfo.data(), sizeof(TensorInfo) * tinfo.size(), hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_sizes, sizes, 8 * (size_t)ntensors, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(p->d_begins, offsets, 8 * (size_t)ntensors, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemset(p->d_sync, 0, p->sync_bytes);
-  if (e != hipSuccess) {
-    (void)hipFree(p->d_block);
-    delete p;
-    return hip_fail(e, "omf_plan_create: upload");
+    return r;
   }
   *out = p;
   return OMF_OK;
@@ -528,7 +694,25 @@ int omf_plan_destroy(omf_plan* plan) {
   return OMF_OK;
 }
 
-int64_t omf_plan_encode_items(const omf_plan* plan) { return plan ? plan->n_enc : -1; }
+int64_t omf_plan_encode_items(const omf_plan* plan) { return plan ? plan->n_enc[plan->strategy] : -1; }
+
+int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (strategy != 0 && strategy != 1) return fail(OMF_EINVAL, "strategy must be 0 (resident) or 1 (two-pass)");
+  plan->strategy = strategy;
+  return OMF_OK;
+}
+
+int64_t omf_plan_resident_capacity(const omf_plan* plan) { return plan ? plan->cap : -1; }
+
+int omf_plan_set_resident_capacity(omf_plan* plan, int64_t cap, int64_t wait_us) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (cap < 0 || wait_us < 0) return fail(OMF_EINVAL, "cap and wait_us must be >= 0");
+  if (cap > 0) plan->cap = cap;
+  plan->wait_ticks = wait_us > 0 ? (uint64_t)wait_us * 100ull : kWaitTicks;
+  if (cap > 0) return upload_plan(plan);
+  return OMF_OK;
+}
 
 int omf_plan_check(omf_plan* plan, void* stream) {
   if (!plan) return fail(OMF_EINVAL, "omf_plan_check: plan is NULL");
@@ -536,7 +720,11 @@ int omf_plan_check(omf_plan* plan, void* stream) {
   OMF_HIP(hipStreamSynchronize((hipStream_t)stream));
   uint32_t err = 0;
   OMF_HIP(hipMemcpy(&err, plan->d_sync + 4, 4, hipMemcpyDeviceToHost));
-  if (err) return fail(OMF_ETIMEOUT, "in-kernel norm hand-off timed out");
+  if (err & 2u) {
+    set_error("encoder recomputed a norm after a bounded wait (items not co-resident); results are exact");
+    return 1;
+  }
+  set_error("");
   return OMF_OK;
 }
 
@@ -558,7 +746,6 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
   hipStream_t st = (hipStream_t)stream;
   EncArgs a;
   a.x = x; a.u = u; a.norm_in = norm_in; a.q = q; a.norm_out = norm_out;
-  a.tinfo = p->d_tinfo;
   a.partials = p->d_partials;
   a.ticket = reinterpret_cast<uint32_t*>(p->d_sync);
   a.err = reinterpret_cast<uint32_t*>(p->d_sync + 4);
@@ -567,9 +754,11 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
   a.alpha = alpha;
   a.levels = (float)(1u << s);
   a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32); a.offset = (uint32_t)offset;
+  a.wait_ticks = p->wait_ticks;
   const dim3 blk(kThreads);
   if (norm_in && !norm_only) {
     a.items = p->d_flat;
+    a.tinfo = p->d_tinfo[0];
     const dim3 grid((unsigned)p->n_flat);
     if (width == 1) {
       if (u) hipLaunchKernelGGL((qsgd_quant_flat<1, true>), grid, blk, 0, st, a);
@@ -582,8 +771,9 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
     return OMF_OK;
   }
   OMF_HIP(hipMemsetAsync(p->d_sync, 0, p->sync_bytes, st));
-  a.items = p->d_enc;
-  const dim3 grid((unsigned)p->n_enc);
+  a.items = p->d_enc[p->strategy];
+  a.tinfo = p->d_tinfo[p->strategy];
+  const dim3 grid((unsigned)p->n_enc[p->strategy]);
   if (norm_only) {
     hipLaunchKernelGGL((qsgd_encode_ordered<1, false, true>), grid, blk, 0, st, a);
   } else if (width == 1) {

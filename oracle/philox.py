@@ -6,15 +6,19 @@ published Philox4x32-10 of Salmon et al., "Parallel random numbers: as easy as
 1, 2, 3" (SC'11); ``tests/test_oracle_golden.py`` pins it on the Random123
 known-answer vectors.
 
-Stream layout used by ``omf_qsgd_encode`` (include/omf_codec.h):
-for element ``i`` of tensor ``t`` (tensor-local index) in a call with
-``seed`` and ``offset``::
+Stream layout used by ``omf_qsgd_encode`` (include/omf_codec.h) for element ``i``
+(tensor-local index) of tensor ``t`` in a call with ``seed`` and ``offset``::
 
-    ctr = (i >> 2 & 0xffffffff, i >> 34, t, offset & 0xffffffff)
-    key = (seed & 0xffffffff, seed >> 32)
-    u_i = (philox(ctr, key)[i & 3] & 0xFFFFFF) * 2**-24
+    j = i >> 2 ; m = j >> 8 ; G = ((m >> 2) << 8) | (j & 255)     # 16-element group
+    W = philox(ctr(3G)) ++ philox(ctr(3G+1)) ++ philox(ctr(3G+2))  # 12 words = 384 bits
+    ctr(c) = (c & 0xffffffff, c >> 32, t, offset & 0xffffffff), key = (seed & 0xffffffff, seed >> 32)
+    f = 4 * (m & 3) + (i & 3)                                      # 24-bit field of W
+    u_i = (bits [24 f, 24 f + 24) of W, little-endian) * 2**-24
 
-i.e. the same 24-bit uniform rule as torch's CPU generator.
+i.e. the same 24-bit uniform rule as torch's CPU generator, three Philox calls per
+16 elements.  A group is what one GPU thread quantises from four of its rows
+(rows are 256 float4 = 1024 elements apart), so the kernel derives it from its
+thread id without any cross-lane exchange.
 """
 
 from __future__ import annotations
@@ -53,12 +57,26 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
 
 def philox_uniforms(seed: int, offset: int, tensor_index: int, n: int) -> np.ndarray:
     """The perf-mode uniforms ``u_0..u_{n-1}`` for one tensor (layout above)."""
-    nq = (n + 3) // 4
-    j = np.arange(nq, dtype=np.uint64)
-    c0 = (j & _MASK).astype(np.uint32)
-    c1 = (j >> np.uint64(32)).astype(np.uint32)
-    c2 = np.full(nq, tensor_index & 0xFFFFFFFF, dtype=np.uint32)
-    c3 = np.full(nq, offset & 0xFFFFFFFF, dtype=np.uint32)
-    o = philox4x32_10(c0, c1, c2, c3, seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-    w = np.stack(o, axis=1).reshape(-1)[:n]
-    return ((w & np.uint32(0xFFFFFF)).astype(np.float64) * 2.0**-24).astype(np.float32)
+    i = np.arange(n, dtype=np.int64)
+    j = i >> 2
+    m = j >> 8
+    G = ((m >> 2) << 8) | (j & 255)
+    f = 4 * (m & 3) + (i & 3)
+    groups = np.unique(G)
+    gpos = np.searchsorted(groups, G)
+    words = np.empty((groups.size, 12), dtype=np.uint32)
+    for c in range(3):
+        ctr = (3 * groups.astype(np.uint64) + np.uint64(c))
+        o = philox4x32_10((ctr & _MASK).astype(np.uint32), (ctr >> np.uint64(32)).astype(np.uint32),
+                          np.full(groups.size, tensor_index & 0xFFFFFFFF, dtype=np.uint32),
+                          np.full(groups.size, offset & 0xFFFFFFFF, dtype=np.uint32),
+                          seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+        for w in range(4):
+            words[:, 4 * c + w] = o[w]
+    bit = 24 * f
+    wi = bit >> 5
+    sh = (bit & 31).astype(np.uint64)
+    lo = words[gpos, wi].astype(np.uint64)
+    hi = words[gpos, np.minimum(wi + 1, 11)].astype(np.uint64)
+    val = ((lo | (hi << np.uint64(32))) >> sh) & np.uint64(0xFFFFFF)
+    return (val.astype(np.float64) * 2.0**-24).astype(np.float32)

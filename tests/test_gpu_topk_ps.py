@@ -40,9 +40,17 @@ def test_topk_golden_error_feedback(gpu, golden, golden_index):
             ih, vh = idx.cpu().numpy(), vals.cpu().numpy()
             assert set(ih.tolist()) == set(gidx.tolist()), key
             k = len(gidx)
-            if k * 64 <= n:  # torch.topk's partial-sort path: descending |x| order (no ties in these inputs)
+            ga = np.abs(gval)
+            if k * 64 <= n and len(np.unique(ga)) == len(ga):
+                # torch.topk's partial-sort path: descending |x|; without ties the order is unique
                 assert ih.tobytes() == gidx.tobytes(), key
                 assert vh.tobytes() == gval.tobytes(), key
+            elif k * 64 <= n:  # ties: same magnitude sequence; ours breaks ties by ascending index
+                assert np.array_equal(np.abs(vh), ga), key
+                for a in range(k - 1):
+                    if abs(vh[a]) == abs(vh[a + 1]):
+                        assert ih[a] < ih[a + 1], key
+                assert np.array_equal(vh[np.argsort(ih)], gval[np.argsort(gidx)])
             else:
                 assert np.array_equal(vh[np.argsort(ih)], gval[np.argsort(gidx)])
             res = comp.residual.residuals["w"].cpu().numpy()
