@@ -22,6 +22,7 @@
 // HBM-bound; no MFMA (no contraction).  Coalesced 16 B/lane fp32 loads, non-temporal
 // 16 B/lane fp32 and 4 B/lane int8 payload stores.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -66,6 +67,8 @@ struct EncArgs {
   float levels;  // 2^s as float (exact)
   uint32_t seed_lo, seed_hi, offset;
   uint64_t wait_ticks;  // bounded norm wait (100 MHz ticks)
+  uint32_t epoch;       // per-launch granule tag (never 0)
+  uint32_t n_items;     // items of this launch (the last ticket resets the counter)
 };
 
 struct DecArgs {
@@ -248,19 +251,19 @@ __device__ __forceinline__ void quant_store(const float4 (&v)[V], const EncArgs&
   }
 }
 
-// Load + scale + quantise + store one sub-chunk [b, e).
-template <int WIDTH, bool HAS_U>
+// Load + scale + quantise + store one sub-chunk [b, e) of V rows (V * 1024 elements).
+template <int WIDTH, bool HAS_U, int V = kV>
 __device__ __forceinline__ void quant_sub(const EncArgs& a, int64_t b, int64_t e, int64_t tbegin, int32_t tensor,
                                           float norm) {
-  float4 v[kV];
-  if (e - b == kSub) {
-    load_f4<kV, true>(a.x, b, e, v);
-    scale_f4<kV>(v, a.alpha);
-    quant_store<WIDTH, HAS_U, true, kV>(v, a, b, e, tbegin, tensor, norm);
+  float4 v[V];
+  if (e - b == (int64_t)V * 1024) {
+    load_f4<V, true>(a.x, b, e, v);
+    scale_f4<V>(v, a.alpha);
+    quant_store<WIDTH, HAS_U, true, V>(v, a, b, e, tbegin, tensor, norm);
   } else {
-    load_f4<kV, false>(a.x, b, e, v);
-    scale_f4<kV>(v, a.alpha);
-    quant_store<WIDTH, HAS_U, false, kV>(v, a, b, e, tbegin, tensor, norm);
+    load_f4<V, false>(a.x, b, e, v);
+    scale_f4<V>(v, a.alpha);
+    quant_store<WIDTH, HAS_U, false, V>(v, a, b, e, tbegin, tensor, norm);
   }
 }
 
@@ -268,15 +271,17 @@ __device__ __forceinline__ void quant_sub(const EncArgs& a, int64_t b, int64_t e
 
 // Sum of squares of one item's range, exactly as a NORM item computes it: sub-chunks in
 // order, each thread accumulating its own rows in fp32.
+template <int V>
 __device__ __forceinline__ float chunk_sumsq(const EncArgs& a, int64_t b, int64_t e) {
+  constexpr int64_t S = (int64_t)V * 1024;
   float acc = 0.0f;
-  for (int64_t sb = b; sb < e; sb += kSub) {
-    const int64_t se = min(sb + kSub, e);
-    float4 v[kV];
-    if (se - sb == kSub) load_f4<kV, true>(a.x, sb, se, v);
-    else load_f4<kV, false>(a.x, sb, se, v);
-    scale_f4<kV>(v, a.alpha);
-    acc = sumsq_f4<kV>(v, acc);
+  for (int64_t sb = b; sb < e; sb += S) {
+    const int64_t se = min(sb + S, e);
+    float4 v[V];
+    if (se - sb == S) load_f4<V, true>(a.x, sb, se, v);
+    else load_f4<V, false>(a.x, sb, se, v);
+    scale_f4<V>(v, a.alpha);
+    acc = sumsq_f4<V>(v, acc);
   }
   return acc;
 }
@@ -299,6 +304,8 @@ __device__ __forceinline__ void publish_partial(const EncArgs& a, const TensorIn
     drain_vmem();
     const uint32_t old = add_agent(&a.counters[t], 1u);
     sh.last = (old == (uint32_t)(ti.nchunks - 1)) ? 1u : 0u;
+    // Every partial of t has arrived: reset the counter for the next launch (stream order).
+    if (sh.last) __hip_atomic_store(&a.counters[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   __syncthreads();
   if (sh.last) {
@@ -309,7 +316,7 @@ __device__ __forceinline__ void publish_partial(const EncArgs& a, const TensorIn
     if (threadIdx.x == 0) {
       const float norm = sqrtf((float)tot);
       a.norm_out[t] = norm;
-      st_agent(&a.gran[t], (1ull << 32) | (uint64_t)__float_as_uint(norm));
+      st_agent(&a.gran[t], ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(norm));
     }
   }
 }
@@ -317,6 +324,7 @@ __device__ __forceinline__ void publish_partial(const EncArgs& a, const TensorIn
 // Poll the tensor's granule (one lane, relaxed sc1 loads, bounded).  On timeout (the
 // tensor's items were not all co-resident) recompute every partial exactly as its owner
 // does and fold them in the last arriver's order: identical bits, err bit 2 set.
+template <int V>
 __device__ __forceinline__ float norm_wait_or_recompute(const EncArgs& a, const TensorInfo& ti, int32_t t,
                                                         HandoffShared& sh) {
   if (threadIdx.x == 0) {
@@ -325,7 +333,7 @@ __device__ __forceinline__ float norm_wait_or_recompute(const EncArgs& a, const 
     float nv = 0.0f;
     for (;;) {
       const uint64_t g = ld_agent(&a.gran[t]);
-      if ((g >> 32) == 1u) {
+      if ((uint32_t)(g >> 32) == a.epoch) {
         nv = __uint_as_float((uint32_t)g);
         ok = 1;
         break;
@@ -344,7 +352,7 @@ __device__ __forceinline__ float norm_wait_or_recompute(const EncArgs& a, const 
   double p = 0.0;
   for (int j = 0; j < ti.nchunks; ++j) {
     const int64_t b = ti.begin + (int64_t)j * ti.chunk, e = min(b + ti.chunk, ti.begin + ti.n);
-    const double sj = block_sum_f64((double)chunk_sumsq(a, b, e), sh.red);
+    const double sj = block_sum_f64((double)chunk_sumsq<V>(a, b, e), sh.red);
     if ((j % kThreads) == (int)threadIdx.x) p += sj;
   }
   const double tot = block_sum_f64(p, sh.red);
@@ -354,37 +362,45 @@ __device__ __forceinline__ float norm_wait_or_recompute(const EncArgs& a, const 
 
 // ---------------------------------------------------------------- kernels
 
-template <int WIDTH, bool HAS_U, bool NORM_ONLY>
+// EV: float4 rows per thread of one encode sub-chunk (EV * 1024 elements); RESIDENT items
+// are one sub-chunk, NORM/QUANT items loop over the sub-chunks of their chunk.
+template <int WIDTH, bool HAS_U, bool NORM_ONLY, int EV>
 __global__ __launch_bounds__(kThreads) void qsgd_encode_ordered(EncArgs a) {
+  constexpr int64_t ES = (int64_t)EV * 1024;
   __shared__ HandoffShared sh;
   __shared__ uint32_t s_ticket;
-  if (threadIdx.x == 0) s_ticket = add_agent(a.ticket, 1u);
+  if (threadIdx.x == 0) {
+    const uint32_t tk = add_agent(a.ticket, 1u);
+    // The last ticket of the launch: every workgroup has taken its ticket, reset for the next.
+    if (tk == a.n_items - 1) __hip_atomic_store(a.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_ticket = tk;
+  }
   __syncthreads();
   const Item it = a.items[s_ticket];
   const TensorInfo ti = a.tinfo[it.tensor];
 
   if (it.kind == kResident) {  // one sub-chunk, x read once
-    const bool full = (it.end - it.begin) == kSub;
-    float4 v[kV];
-    if (full) load_f4<kV, true>(a.x, it.begin, it.end, v);
-    else load_f4<kV, false>(a.x, it.begin, it.end, v);
-    scale_f4<kV>(v, a.alpha);
-    publish_partial(a, ti, it.tensor, it.chunk, sumsq_f4<kV>(v, 0.0f), sh);
+    const bool full = (it.end - it.begin) == ES;
+    float4 v[EV];
+    if (full) load_f4<EV, true>(a.x, it.begin, it.end, v);
+    else load_f4<EV, false>(a.x, it.begin, it.end, v);
+    scale_f4<EV>(v, a.alpha);
+    publish_partial(a, ti, it.tensor, it.chunk, sumsq_f4<EV>(v, 0.0f), sh);
     if (NORM_ONLY) return;
-    const float norm = norm_wait_or_recompute(a, ti, it.tensor, sh);
-    if (full) quant_store<WIDTH, HAS_U, true, kV>(v, a, it.begin, it.end, ti.begin, it.tensor, norm);
-    else quant_store<WIDTH, HAS_U, false, kV>(v, a, it.begin, it.end, ti.begin, it.tensor, norm);
+    const float norm = norm_wait_or_recompute<EV>(a, ti, it.tensor, sh);
+    if (full) quant_store<WIDTH, HAS_U, true, EV>(v, a, it.begin, it.end, ti.begin, it.tensor, norm);
+    else quant_store<WIDTH, HAS_U, false, EV>(v, a, it.begin, it.end, ti.begin, it.tensor, norm);
     return;
   }
   if (it.kind == kNorm) {
-    publish_partial(a, ti, it.tensor, it.chunk, chunk_sumsq(a, it.begin, it.end), sh);
+    publish_partial(a, ti, it.tensor, it.chunk, chunk_sumsq<EV>(a, it.begin, it.end), sh);
     return;
   }
   // kQuant: second pass of a large tensor.
   if (NORM_ONLY) return;
-  const float norm = norm_wait_or_recompute(a, ti, it.tensor, sh);
-  for (int64_t b = it.begin; b < it.end; b += kSub)
-    quant_sub<WIDTH, HAS_U>(a, b, min(b + kSub, it.end), ti.begin, it.tensor, norm);
+  const float norm = norm_wait_or_recompute<EV>(a, ti, it.tensor, sh);
+  for (int64_t b = it.begin; b < it.end; b += ES)
+    quant_sub<WIDTH, HAS_U, EV>(a, b, min(b + ES, it.end), ti.begin, it.tensor, norm);
 }
 
 template <int WIDTH, bool HAS_U>
@@ -502,6 +518,8 @@ struct omf_plan {
   int64_t cap = 0;               // tensors of <= cap items take the register-resident path
   int32_t strategy = 1;          // 0 register-resident + two-pass, 1 two-pass only (default: faster on MI355X)
   uint64_t wait_ticks = kWaitTicks;
+  uint32_t epoch = 0;            // last granule tag used (host-side launch counter)
+  int32_t ev = 16;               // encode rows per thread (sub-chunk = ev * 1024 elements)
   int64_t n_enc[2] = {0, 0};
   Item* d_enc[2] = {nullptr, nullptr};
   TensorInfo* d_tinfo[2] = {nullptr, nullptr};
@@ -544,13 +562,14 @@ static void build_sequence(const omf_plan& p, bool resident_ok, std::vector<Item
   std::vector<Item> deferred;
   for (int32_t t = 0; t < p.nt; ++t) {
     const int64_t n = p.sizes[t], b = p.offsets[t];
-    const int64_t ns = (n + kSub - 1) / kSub;
+    const int64_t es = (int64_t)p.ev * 1024;
+    const int64_t ns = (n + es - 1) / es;
     std::vector<Item> q_t;
     if (ns == 1 || (resident_ok && ns <= p.cap)) {
-      tinfo[t] = TensorInfo{b, n, kSub, (int32_t)ns, (int32_t)npart};
+      tinfo[t] = TensorInfo{b, n, es, (int32_t)ns, (int32_t)npart};
       for (int64_t c = 0; c < ns; ++c) {
-        const int64_t cb = b + c * kSub;
-        seq.push_back(Item{cb, std::min(b + n, cb + kSub), t, kResident, (int32_t)c, 0});
+        const int64_t cb = b + c * es;
+        seq.push_back(Item{cb, std::min(b + n, cb + es), t, kResident, (int32_t)c, 0});
       }
       npart += ns;
     } else {
@@ -576,11 +595,13 @@ static int upload_plan(omf_plan* p) {
   int64_t np[2];
   build_sequence(*p, true, seq[0], tinfo[0], np[0]);
   build_sequence(*p, false, seq[1], tinfo[1], np[1]);
+  // Flat items (decode, norm-supplied quantise, Top-K passes): one 16 Ki sub-chunk each,
+  // the fastest decode granularity measured (profiles/r01_notes.md).
   for (int32_t t = 0; t < p->nt; ++t) {
     const int64_t n = p->sizes[t], b = p->offsets[t];
-    for (int64_t c = 0; c * p->chunk < n; ++c) {
-      const int64_t cb = b + c * p->chunk;
-      flat.push_back(Item{cb, std::min(b + n, cb + p->chunk), t, kQuant, (int32_t)c, 0});
+    for (int64_t c = 0; c * kSub < n; ++c) {
+      const int64_t cb = b + c * kSub;
+      flat.push_back(Item{cb, std::min(b + n, cb + kSub), t, kQuant, (int32_t)c, 0});
     }
   }
   if ((int64_t)std::max(seq[0].size(), flat.size()) > 0x7fffffffLL) return fail(OMF_EINVAL, "too many work items");
@@ -637,7 +658,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
   if (!out) return fail(OMF_EINVAL, "omf_plan_create: out is NULL");
   *out = nullptr;
   if (ntensors <= 0 || !sizes || !offsets) return fail(OMF_EINVAL, "omf_plan_create: need >= 1 tensor");
-  if (chunk_elems == 0) chunk_elems = kSub;
+  if (chunk_elems == 0) chunk_elems = 4 * kSub;  // two-pass encode items: 256 KiB of fp32
   if (chunk_elems < kSub || chunk_elems % kSub != 0)
     return fail(OMF_EINVAL, "omf_plan_create: chunk_elems must be a positive multiple of 16384");
   for (int32_t t = 0; t < ntensors; ++t) {
@@ -664,11 +685,18 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
       delete p;
       return fail(OMF_EHIP, "omf_plan_create: cannot query the device");
     }
-    const void* kerns[5] = {(const void*)qsgd_encode_ordered<1, false, false>,
-                            (const void*)qsgd_encode_ordered<1, true, false>,
-                            (const void*)qsgd_encode_ordered<4, false, false>,
-                            (const void*)qsgd_encode_ordered<4, true, false>,
-                            (const void*)qsgd_encode_ordered<1, false, true>};
+    if (const char* ev = getenv("OMF_ENCODE_ROWS")) p->ev = atoi(ev) == 8 ? 8 : 16;  // tuning knob
+    const void* k16[5] = {(const void*)qsgd_encode_ordered<1, false, false, 16>,
+                          (const void*)qsgd_encode_ordered<1, true, false, 16>,
+                          (const void*)qsgd_encode_ordered<4, false, false, 16>,
+                          (const void*)qsgd_encode_ordered<4, true, false, 16>,
+                          (const void*)qsgd_encode_ordered<1, false, true, 16>};
+    const void* k8[5] = {(const void*)qsgd_encode_ordered<1, false, false, 8>,
+                         (const void*)qsgd_encode_ordered<1, true, false, 8>,
+                         (const void*)qsgd_encode_ordered<4, false, false, 8>,
+                         (const void*)qsgd_encode_ordered<4, true, false, 8>,
+                         (const void*)qsgd_encode_ordered<1, false, true, 8>};
+    const void* const* kerns = p->ev == 8 ? k8 : k16;
     int nb_min = 1 << 30;
     for (int i = 0; i < 5; ++i) {
       int nb = 0;
@@ -770,19 +798,29 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }
-  OMF_HIP(hipMemsetAsync(p->d_sync, 0, p->sync_bytes, st));
+  // No per-call memset: tickets and arrival counters are reset in-kernel by their last
+  // user, and granules carry this launch's epoch.
+  if (++p->epoch == 0) ++p->epoch;
+  a.epoch = p->epoch;
+  a.n_items = (uint32_t)p->n_enc[p->strategy];
   a.items = p->d_enc[p->strategy];
   a.tinfo = p->d_tinfo[p->strategy];
   const dim3 grid((unsigned)p->n_enc[p->strategy]);
-  if (norm_only) {
-    hipLaunchKernelGGL((qsgd_encode_ordered<1, false, true>), grid, blk, 0, st, a);
-  } else if (width == 1) {
-    if (u) hipLaunchKernelGGL((qsgd_encode_ordered<1, true, false>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((qsgd_encode_ordered<1, false, false>), grid, blk, 0, st, a);
-  } else {
-    if (u) hipLaunchKernelGGL((qsgd_encode_ordered<4, true, false>), grid, blk, 0, st, a);
-    else hipLaunchKernelGGL((qsgd_encode_ordered<4, false, false>), grid, blk, 0, st, a);
-  }
+#define OMF_ENC(EV)                                                                              \
+  do {                                                                                           \
+    if (norm_only) {                                                                             \
+      hipLaunchKernelGGL((qsgd_encode_ordered<1, false, true, EV>), grid, blk, 0, st, a);        \
+    } else if (width == 1) {                                                                     \
+      if (u) hipLaunchKernelGGL((qsgd_encode_ordered<1, true, false, EV>), grid, blk, 0, st, a); \
+      else hipLaunchKernelGGL((qsgd_encode_ordered<1, false, false, EV>), grid, blk, 0, st, a);  \
+    } else {                                                                                     \
+      if (u) hipLaunchKernelGGL((qsgd_encode_ordered<4, true, false, EV>), grid, blk, 0, st, a); \
+      else hipLaunchKernelGGL((qsgd_encode_ordered<4, false, false, EV>), grid, blk, 0, st, a);  \
+    }                                                                                            \
+  } while (0)
+  if (p->ev == 8) OMF_ENC(8);
+  else OMF_ENC(16);
+#undef OMF_ENC
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }

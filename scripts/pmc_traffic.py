@@ -1,0 +1,59 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic of the codec kernels from two rocprofv3 --pmc passes.
+
+Usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [config bits]
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction
+(MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128 B request of a wide
+coalesced stream, so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.
+"""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def load(d, counter):
+    files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+    per = defaultdict(list)
+    for f in files:
+        for r in csv.DictReader(open(f)):
+            if r.get("Counter_Name") != counter:
+                continue
+            name = r.get("Kernel_Name", "")
+            per[name].append(float(r["Counter_Value"]))
+    return per
+
+
+def short(name):
+    for k in ("qsgd_encode_ordered", "qsgd_decode_flat", "qsgd_quant_flat", "topk_prep_hist", "topk_collect"):
+        if k in name:
+            return k
+    return None
+
+
+def main():
+    fdir, wdir, out = sys.argv[1:4]
+    cfg = sys.argv[4] if len(sys.argv) > 4 else "llama400m"
+    bits = int(sys.argv[5]) if len(sys.argv) > 5 else 4
+    fetch, write = load(fdir, "FETCH_SIZE"), load(wdir, "WRITE_SIZE")
+    res = {}
+    for name, vals in fetch.items():
+        k = short(name)
+        if not k or name not in write:
+            continue
+        f = 2 * 1024 * sum(vals) / len(vals)
+        w = 1024 * sum(write[name]) / len(write[name])
+        res[k] = {"fetch_bytes_corrected": f, "write_bytes": w, "launches": len(vals)}
+    j = {"config": cfg, "bits": bits, "note": "FETCH_SIZE x2 (gfx950 wide-load correction) + WRITE_SIZE, KiB->B, "
+         "average per launch; Infinity-Cache hits are counted as fetches",
+         "bytes_per_launch": {k: round(v["fetch_bytes_corrected"] + v["write_bytes"]) for k, v in res.items()},
+         "detail": res}
+    with open(out, "w") as fh:
+        json.dump(j, fh, indent=1)
+    print(json.dumps(j["bytes_per_launch"]))
+
+
+if __name__ == "__main__":
+    main()
