@@ -143,6 +143,7 @@ int omf_div_f32(float* y, int64_t n, float divisor, void* stream);
  * Order within a tensor: descending |t'|, ties by ascending index (torch.topk's
  * order for k*64 <= n on the reference CPU path; ties there are unspecified).
  * ws: caller workspace of omf_topk_workspace_bytes(plan, ratio) bytes.
+ * Synchronises `stream` once (the candidate count sizes the device-wide sort).
  */
 int64_t omf_topk_k(int64_t numel, double ratio);
 size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio);

@@ -14,7 +14,11 @@
 //                       wave-aggregated atomic per wave as a 64-bit key
 //                       (|t'| bits << 32 | ~index): descending key order = descending
 //                       magnitude, ties by ascending index.
-//   4. segmented descending radix sort of the candidates (rocPRIM).
+//   4. one device-wide radix sort of all candidates (rocPRIM onesweep) on the composite
+//                       key (tensor << 56 | (2^31-1 - |t'|bits) << 25 | index), i.e.
+//                       tensor ascending, magnitude descending, index ascending; when a
+//                       plan exceeds 256 tensors or 2^25 elements per tensor, a segmented
+//                       descending sort of (|t'|bits << 32 | ~index) per tensor instead.
 //   5. topk_gather      first k keys of every tensor -> values / int64 indices; zero
 //                       the selected residual slots.
 // Decode is a scatter (mode 0 zero-fill, 1 overlay, 2 scatter-add).
@@ -138,58 +142,126 @@ __global__ void topk_offsets(const int64_t* __restrict__ tsize,
   }
 }
 
+// Candidates of one item: every |t'| whose bin is >= b1.  Counts are aggregated per
+// sub-chunk (block scan in LDS) so each sub-chunk costs ONE global atomic on its tensor's
+// counter; keys go to the tensor's own region cand[tbegin + pos] (capacity n_t).
+template <bool GLOBAL>
 __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict__ tp, const Item* __restrict__ items,
                                                          const int64_t* __restrict__ tbegin,
                                                          const uint32_t* __restrict__ bin, uint32_t* __restrict__ cnt,
-                                                         uint64_t* __restrict__ cand) {
+                                                         uint32_t* __restrict__ item_cnt, uint64_t* __restrict__ cand) {
+  __shared__ uint32_t s_wsum[kWaves];
+  __shared__ uint32_t s_base;
   const Item it = items[blockIdx.x];
   const uint32_t b1 = bin[it.tensor];
   const int64_t base = tbegin[it.tensor];
-  const int lane = threadIdx.x & 63;
-  for (int64_t b = it.begin; b < it.end; b += kSub) {
-    const int64_t end = min(b + kSub, it.end);
-#pragma unroll 4
-    for (int k = 0; k < kV; ++k) {
-      const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
-      float v[4] = {0.f, 0.f, 0.f, 0.f};
-      int nv = 0;
-      if (e + 4 <= end) {
-        const float4 t = *reinterpret_cast<const float4*>(tp + e);
-        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
-        nv = 4;
-      } else if (e < end) {
-        nv = (int)(end - e);
-        for (int c = 0; c < nv; ++c) v[c] = tp[e + c];
-      }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int CV = 8;                           // rows per pass (register budget)
+  constexpr int64_t CS = (int64_t)CV * kThreads * 4;  // 8192 elements
+  uint32_t item_total = 0;                         // GLOBAL: running offset in the item's region
+  for (int64_t b = it.begin; b < it.end; b += CS) {
+    const int64_t end = min(b + CS, it.end);
+    const uint32_t lim = (uint32_t)(end - b);  // elements of this pass
+    const uint32_t off0 = 4u * threadIdx.x;    // this lane's first element
+    float4 v[CV];
+    uint32_t selm = 0;  // bit 4k+c: element (row k, component c) is a candidate
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const uint32_t key = mag_key(v[c]);
-        const bool sel = (c < nv) && ((key >> kShift) >= b1);
-        const uint64_t m = __ballot(sel);
-        if (m == 0) continue;  // wave-uniform
-        const int leader = __ffsll((long long)m) - 1;
-        uint32_t pos0 = 0;
-        if (lane == leader) pos0 = atomicAdd(&cnt[it.tensor], (uint32_t)__popcll(m));
-        pos0 = __shfl(pos0, leader, 64);
-        if (sel) {
-          const uint32_t rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-          const uint32_t idx = (uint32_t)(e + c - base);
-          cand[base + pos0 + rank] = ((uint64_t)key << 32) | (uint64_t)(~idx);
+    for (int k = 0; k < CV; ++k) {
+      const uint32_t o = off0 + 1024u * k;
+      if (o + 4 <= lim) {
+        v[k] = *reinterpret_cast<const float4*>(tp + b + o);
+      } else {
+        v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (o < lim) v[k].x = tp[b + o];
+        if (o + 1 < lim) v[k].y = tp[b + o + 1];
+        if (o + 2 < lim) v[k].z = tp[b + o + 2];
+      }
+      const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (o + c < lim && (mag_key(vv[c]) >> kShift) >= b1) selm |= 1u << (4 * k + c);
+    }
+    const uint32_t nsel = (uint32_t)__popc(selm);
+    // wave totals -> block scan in LDS
+    uint32_t wtot = nsel;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wtot += __shfl_xor(wtot, o, 64);
+    if (lane == 0) s_wsum[wave] = wtot;
+    __syncthreads();
+    uint32_t wpre = 0, tot = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < kWaves; ++w2) {
+      if (w2 < wave) wpre += s_wsum[w2];
+      tot += s_wsum[w2];
+    }
+    // GLOBAL: the item's candidates go to its own element range (capacity = item size),
+    // counted per item and packed after an exclusive scan — no contended atomics.
+    if (!GLOBAL && threadIdx.x == 0) s_base = tot ? atomicAdd(&cnt[it.tensor], tot) : 0u;
+    __syncthreads();
+    // coalesced writes: per (row, component) the selected lanes of a wave store consecutively
+    uint64_t* dst = GLOBAL ? cand + it.begin + item_total + wpre : cand + base + s_base + wpre;
+    const uint32_t idx0 = (uint32_t)(b - base) + off0;
+    const uint64_t tag = (uint64_t)it.tensor << 56;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    if (wtot) {
+#pragma unroll
+      for (int k = 0; k < CV; ++k) {
+        const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bool sel = (selm >> (4 * k + c)) & 1u;
+          const uint64_t m = __ballot(sel);
+          if (sel) {
+            const uint32_t idx = idx0 + 1024u * k + c;
+            const uint32_t key = mag_key(vv[c]);
+            dst[__popcll(m & lt)] = GLOBAL ? (tag | ((uint64_t)(0x7fffffffu - key) << 25) | (uint64_t)idx)
+                                           : (((uint64_t)key << 32) | (uint64_t)(~idx));
+          }
+          dst += __popcll(m);
         }
       }
     }
+    item_total += tot;
+    __syncthreads();  // s_wsum / s_base reuse
+  }
+  if (GLOBAL && threadIdx.x == 0) item_cnt[blockIdx.x] = item_total;
+}
+
+// Pack every item's candidates (stored at the item's element range) at its scanned offset.
+__global__ __launch_bounds__(kThreads) void topk_compact(const uint64_t* __restrict__ cand,
+                                                         const Item* __restrict__ items,
+                                                         const uint32_t* __restrict__ item_cnt,
+                                                         const uint32_t* __restrict__ item_off,
+                                                         uint64_t* __restrict__ packed) {
+  const Item it = items[blockIdx.x];
+  const uint32_t n = item_cnt[blockIdx.x], dst = item_off[blockIdx.x];
+  for (uint32_t j = threadIdx.x; j < n; j += kThreads) packed[dst + j] = cand[it.begin + j];
+}
+
+// Per-tensor start and count of the packed candidates, from the item scan.
+__global__ void topk_tensor_ranges(const Item* __restrict__ items, int64_t n_items,
+                                   const uint32_t* __restrict__ item_cnt, const uint32_t* __restrict__ item_off,
+                                   int64_t* __restrict__ cstart, uint32_t* __restrict__ cnt) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += (int64_t)gridDim.x * blockDim.x) {
+    const Item it = items[i];
+    if (it.chunk == 0) cstart[it.tensor] = item_off[i];
+    atomicAdd(&cnt[it.tensor], item_cnt[i]);
   }
 }
 
+template <bool GLOBAL>
 __global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict__ tp, float* __restrict__ r,
                                                         const uint64_t* __restrict__ sorted,
                                                         const int64_t* __restrict__ tbegin,
+                                                        const int64_t* __restrict__ cstart,
                                                         const int64_t* __restrict__ kk, const int64_t* __restrict__ koff,
                                                         float* __restrict__ values, int64_t* __restrict__ indices) {
   const int t = blockIdx.y;
   const int64_t k = kk[t], base = tbegin[t], o = koff[t];
+  const int64_t s0 = GLOBAL ? cstart[t] : base;
   for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < k; j += (int64_t)gridDim.x * kThreads) {
-    const uint32_t idx = ~(uint32_t)sorted[base + j];
+    const uint64_t key = sorted[s0 + j];
+    const uint32_t idx = GLOBAL ? (uint32_t)(key & 0x1FFFFFFull) : ~(uint32_t)key;
     const float v = tp[base + idx];
     values[o + j] = v;
     indices[o + j] = (int64_t)idx;
@@ -225,17 +297,38 @@ namespace {
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-size_t sort_tmp_bytes(int64_t size, int32_t nt) {
+bool global_path(const omf_plan* p) {
+  if (omf_plan_access::ntensors(p) > 256) return false;
+  for (int64_t n : omf_plan_access::sizes(p))
+    if (n > (int64_t)1 << 25) return false;
+  return true;
+}
+
+size_t sort_tmp_bytes(const omf_plan* p) {
+  const int64_t size = omf_plan_access::arena_end(p);
+  const int32_t nt = omf_plan_access::ntensors(p);
   size_t bytes = 0;
   uint64_t* dummy = nullptr;
-  uint32_t* off = nullptr;
-  (void)rocprim::segmented_radix_sort_keys_desc(nullptr, bytes, dummy, dummy, (unsigned int)size, (unsigned int)nt, off,
-                                                off, 0, 64, (hipStream_t)0, false);
+  if (global_path(p)) {
+    (void)rocprim::radix_sort_keys(nullptr, bytes, dummy, dummy, (size_t)size, 0, 64, (hipStream_t)0, false);
+    int64_t n_items = 0;
+    (void)omf_plan_access::flat_items(p, &n_items);
+    size_t sb = 0;
+    uint32_t* u = nullptr;
+    (void)rocprim::exclusive_scan(nullptr, sb, u, u, 0u, (size_t)n_items, rocprim::plus<uint32_t>(), (hipStream_t)0,
+                                  false);
+    bytes = std::max(bytes, sb);
+  } else {
+    uint32_t* off = nullptr;
+    (void)rocprim::segmented_radix_sort_keys_desc(nullptr, bytes, dummy, dummy, (unsigned int)size, (unsigned int)nt,
+                                                  off, off, 0, 64, (hipStream_t)0, false);
+  }
   return bytes;
 }
 
 struct WsLayout {
-  size_t hist, bin, cnt, koff, kk, seg_b, seg_e, cand, sorted, tmp, total, tmp_bytes;
+  size_t hist, bin, cnt, cnt_all, koff, kk, seg_b, seg_e, cstart, item_cnt, item_off, cand, sorted, tmp, total,
+      tmp_bytes;
 };
 
 WsLayout layout(const omf_plan* p) {
@@ -246,13 +339,19 @@ WsLayout layout(const omf_plan* p) {
   L.hist = o; o = align256(o + 4 * (size_t)nt * kBins);
   L.bin = o; o = align256(o + 4 * (size_t)nt);
   L.cnt = o; o = align256(o + 4 * (size_t)nt);
+  L.cnt_all = o; o = align256(o + 4);
   L.koff = o; o = align256(o + 8 * (size_t)(nt + 1));
   L.kk = o; o = align256(o + 8 * (size_t)nt);
   L.seg_b = o; o = align256(o + 4 * (size_t)nt);
   L.seg_e = o; o = align256(o + 4 * (size_t)nt);
+  L.cstart = o; o = align256(o + 8 * (size_t)nt);
+  int64_t n_items = 0;
+  (void)omf_plan_access::flat_items(p, &n_items);
+  L.item_cnt = o; o = align256(o + 4 * (size_t)n_items);
+  L.item_off = o; o = align256(o + 4 * (size_t)n_items);
   L.cand = o; o = align256(o + 8 * (size_t)ae);
   L.sorted = o; o = align256(o + 8 * (size_t)ae);
-  L.tmp_bytes = sort_tmp_bytes(ae, nt);
+  L.tmp_bytes = sort_tmp_bytes(p);
   L.tmp = o; o = align256(o + L.tmp_bytes);
   L.total = o;
   return L;
@@ -300,6 +399,9 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
   uint32_t* bin = reinterpret_cast<uint32_t*>(w + L.bin);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
+  int64_t* cstart = reinterpret_cast<int64_t*>(w + L.cstart);
+  uint32_t* item_cnt = reinterpret_cast<uint32_t*>(w + L.item_cnt);
+  uint32_t* item_off = reinterpret_cast<uint32_t*>(w + L.item_off);
   int64_t* koff = reinterpret_cast<int64_t*>(w + L.koff);
   int64_t* kk = reinterpret_cast<int64_t*>(w + L.kk);
   uint32_t* seg_b = reinterpret_cast<uint32_t*>(w + L.seg_b);
@@ -312,7 +414,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   const int64_t* d_sizes = omf_plan_access::d_sizes(plan);
   const int64_t* d_begins = omf_plan_access::d_begins(plan);
 
-  // hist + cnt are contiguous from the workspace start up to L.bin/L.koff: zero them.
+  // hist, bin, cnt and cnt_all precede L.koff: zero them.
   OMF_HIP(hipMemsetAsync(w, 0, L.koff, st));
   hipLaunchKernelGGL(topk_offsets, dim3(1), dim3(64), 0, st, d_sizes, nt, ratio, kk, koff, d_begins, cnt,
                      seg_b, seg_e, 0);
@@ -322,17 +424,40 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   else if (residual_mode == 1) hipLaunchKernelGGL((topk_prep_hist<1>), grid, blk, 0, st, x, residual, items, hist);
   else hipLaunchKernelGGL((topk_prep_hist<2>), grid, blk, 0, st, x, residual, items, hist);
   hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, bin);
-  hipLaunchKernelGGL(topk_collect, grid, blk, 0, st, tp, items, d_begins, bin, cnt, cand);
-  hipLaunchKernelGGL(topk_offsets, dim3(1), dim3(64), 0, st, d_sizes, nt, ratio, kk, koff, d_begins, cnt,
-                     seg_b, seg_e, 1);
-  OMF_HIP(hipGetLastError());
+  const bool glob = global_path(plan);
   size_t tmp_bytes = L.tmp_bytes;
-  OMF_HIP(rocprim::segmented_radix_sort_keys_desc(w + L.tmp, tmp_bytes, cand, sorted,
-                                                  (unsigned int)omf_plan_access::arena_end(plan), (unsigned int)nt,
-                                                  seg_b, seg_e, 0, 64, st, false));
+  if (glob) {
+    hipLaunchKernelGGL((topk_collect<true>), grid, blk, 0, st, tp, items, d_begins, bin, cnt, item_cnt, cand);
+    size_t sb = L.tmp_bytes;
+    OMF_HIP(rocprim::exclusive_scan(w + L.tmp, sb, item_cnt, item_off, 0u, (size_t)n_items,
+                                    rocprim::plus<uint32_t>(), st, false));
+    hipLaunchKernelGGL(topk_tensor_ranges, dim3(64), blk, 0, st, items, n_items, item_cnt, item_off, cstart, cnt);
+    OMF_HIP(hipGetLastError());
+    uint32_t last[2];  // the sort needs the candidate count on the host
+    OMF_HIP(hipMemcpyAsync(&last[0], item_off + n_items - 1, 4, hipMemcpyDeviceToHost, st));
+    OMF_HIP(hipMemcpyAsync(&last[1], item_cnt + n_items - 1, 4, hipMemcpyDeviceToHost, st));
+    OMF_HIP(hipStreamSynchronize(st));
+    const uint64_t total = (uint64_t)last[0] + last[1];
+    hipLaunchKernelGGL(topk_compact, grid, blk, 0, st, cand, items, item_cnt, item_off, sorted);
+    // sort the packed keys back into `cand` (the per-item regions are no longer needed)
+    OMF_HIP(rocprim::radix_sort_keys(w + L.tmp, tmp_bytes, sorted, cand, (size_t)total, 0, 64, st, false));
+  } else {
+    hipLaunchKernelGGL((topk_collect<false>), grid, blk, 0, st, tp, items, d_begins, bin, cnt, item_cnt, cand);
+    hipLaunchKernelGGL(topk_offsets, dim3(1), dim3(64), 0, st, d_sizes, nt, ratio, kk, koff, d_begins, cnt,
+                       seg_b, seg_e, 1);
+    OMF_HIP(hipGetLastError());
+    OMF_HIP(rocprim::segmented_radix_sort_keys_desc(w + L.tmp, tmp_bytes, cand, sorted,
+                                                    (unsigned int)omf_plan_access::arena_end(plan), (unsigned int)nt,
+                                                    seg_b, seg_e, 0, 64, st, false));
+  }
+  const uint64_t* sorted_keys = glob ? cand : sorted;
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((kmax + kThreads - 1) / kThreads, 1024));
-  hipLaunchKernelGGL(topk_gather, dim3(gx, (unsigned)nt), blk, 0, st, tp, residual_mode ? residual : nullptr, sorted,
-                     d_begins, kk, koff, values, indices);
+  if (glob)
+    hipLaunchKernelGGL((topk_gather<true>), dim3(gx, (unsigned)nt), blk, 0, st, tp, residual_mode ? residual : nullptr,
+                       sorted_keys, d_begins, cstart, kk, koff, values, indices);
+  else
+    hipLaunchKernelGGL((topk_gather<false>), dim3(gx, (unsigned)nt), blk, 0, st, tp,
+                       residual_mode ? residual : nullptr, sorted_keys, d_begins, cstart, kk, koff, values, indices);
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }

@@ -77,3 +77,10 @@ for chunk in (65536,):
         ms = tm(fn)
         print(f"chunk {chunk:6d} {nm:30s} {ms:.4f} ms  {bpe * N / ms / 1e6:7.1f} GB/s (counting {bpe} B/elem)")
     print("co-resident:", p.check())
+    # Top-K (k = 1 %) with error feedback over the whole arena
+    res = torch.zeros(p.arena_end, device=dev)
+    p.topk_encode(x, 0.01, residual=res, residual_mode=2)
+    ms = tm(lambda: p.topk_encode(x, 0.01, residual=res, residual_mode=1), reps=5)
+    print(f"topk encode (ratio 0.01, EF)      {ms:.4f} ms  {16.24 * N / ms / 1e6:7.1f} GB/s (algorithmic 16N+24k)")
+    ms = tm(lambda: p.topk_encode(x, 0.01), reps=5)
+    print(f"topk encode (ratio 0.01, no EF)   {ms:.4f} ms  {8.24 * N / ms / 1e6:7.1f} GB/s (algorithmic 8N+24k)")
