@@ -72,10 +72,20 @@ int omf_plan_check(omf_plan* plan, void* stream);
 /* Encoder strategy: 0 = register-resident items for tensors of at most
  * omf_plan_resident_capacity() items (x read once; the workgroup holds its 16 Ki elements
  * while the tensor norm is published) and two-pass items for larger tensors;
- * 1 (default) = two-pass for every tensor (x re-read after the norm; measured faster on
- * MI355X, where waiting workgroups idle their slots — DESIGN.md §4).  Identical payloads given the
- * norm; the norms fold partials over different item sizes, so they agree to rounding. */
+ * 1 = two-pass for every tensor (x re-read after the norm);
+ * 2 = single-read "ring" encoder: persistent workgroups keep each chunk in an LDS ring
+ * until its tensor's norm is complete; tensors larger than the ring's
+ * hold limit take a second read.  Identical payloads given the norm; the norms fold
+ * partials over different chunk sizes, so strategies agree to rounding. */
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy);
+/* Ring encoder tuning / test hook (rebuilds the chunk sequence; not for the hot path):
+ * cfg = kernel configuration (-1 keep), big_mode 0/1 (placement of second-read chunks,
+ * -1 keep), gap = items between a large tensor's first and second pass (-2 keep, -1 one
+ * grid), hold_max = largest tensor (chunks) read once (0 = slots x grid, -1 keep). */
+int omf_plan_set_ring(omf_plan* plan, int32_t cfg, int32_t big_mode, int64_t gap, int64_t hold_max);
+/* Ring encoder facts: out[0] grid, out[1] chunk elements, out[2] items, out[3] hold limit
+ * (chunks), out[4] tensors taking two passes, out[5] configuration. */
+int omf_plan_ring_info(const omf_plan* plan, int64_t* out6);
 /* Largest tensor (in 16 Ki-element items) that takes the register-resident path: half the
  * encoder's co-resident workgroups (occupancy x CUs). */
 int64_t omf_plan_resident_capacity(const omf_plan* plan);

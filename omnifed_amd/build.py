@@ -18,7 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libomf_codec.so")
 
-SOURCES = ["omf_runtime.cpp", "omf_qsgd.hip", "omf_topk.hip"]
+SOURCES = ["omf_runtime.cpp", "omf_qsgd.hip", "omf_qsgd_ring.hip", "omf_topk.hip"]
 
 # Exact IEEE fp32 (no contraction, denormals kept, correctly rounded / and sqrt): the
 # payload must match the reference bit for bit.
@@ -79,6 +79,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stdout.decode(errors="replace"))
     os.replace(tmp, LIB)
+    # the offload linker leaves per-target unbundling temporaries beside the output
+    for f in os.listdir(HERE):
+        if f.startswith("libomf_codec.so.") and ("-amdhsa-" in f or "-linux-gnu" in f):
+            os.remove(os.path.join(HERE, f))
     return LIB
 
 

@@ -137,9 +137,21 @@ class Plan:
         check(lib().omf_plan_set_resident_capacity(self._h, int(cap), int(wait_us)), "omf_plan_set_resident_capacity")
 
     def set_encode_strategy(self, strategy: str) -> None:
-        """'resident' (x read once where it fits, default) or 'ordered' (two-pass everywhere)."""
-        code = {"resident": 0, "ordered": 1}[strategy]
+        """'ring' (single-read encoder), 'ordered' (two-pass everywhere) or 'resident'
+        (register-resident small tensors + two-pass)."""
+        code = {"resident": 0, "ordered": 1, "ring": 2}[strategy]
         check(lib().omf_plan_set_encode_strategy(self._h, code), "omf_plan_set_encode_strategy")
+
+    def set_ring(self, cfg: int = -1, big_mode: int = -1, gap: int = -2, hold_max: int = -1) -> None:
+        """Tuning / test hook of the ring encoder: see omf_plan_set_ring."""
+        check(lib().omf_plan_set_ring(self._h, int(cfg), int(big_mode), int(gap), int(hold_max)), "omf_plan_set_ring")
+
+    @property
+    def ring_info(self) -> Dict[str, int]:
+        out = (ctypes.c_int64 * 6)()
+        check(lib().omf_plan_ring_info(self._h, out), "omf_plan_ring_info")
+        keys = ("grid", "chunk", "items", "hold_max", "two_pass_tensors", "cfg")
+        return dict(zip(keys, (int(v) for v in out)))
 
     def __del__(self):
         h = getattr(self, "_h", None)

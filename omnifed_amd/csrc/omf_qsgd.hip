@@ -28,6 +28,8 @@
 
 #include "../../include/omf_codec.h"
 #include "omf_common.h"
+#include "omf_qsgd_dev.h"
+#include "omf_ring.h"
 
 using namespace omf;
 
@@ -78,46 +80,6 @@ struct DecArgs {
   const Item* items;
   float levels;      // fl32(levels)
   float inv_levels;  // 2^-s when levels is a power of two (exact), else unused
-};
-
-// ---------------------------------------------------------------- element math
-
-// One QSGD level from vn = xs / norm, qsgd.py:50-63: every step after the division is
-// exact in fp32.  Out-of-range or NaN magnitudes follow the reference's x86
-// float->int64 conversion (INT64_MIN, then clamp to 0): the payload element is 0.
-__device__ __forceinline__ int32_t qsgd_level(float vn, float L, float u) {
-  const float a = fabsf(vn);
-  const float sc = __fmul_rn(a, L);
-  const float fl = floorf(sc);
-  const float p = __fsub_rn(sc, fl);
-  float m = fl + ((u < p) ? 1.0f : 0.0f);  // exact: p > 0 implies fl < 2^23
-  m = fminf(m, L);
-  const int32_t mag = (sc < 9.2233720e18f) ? (int32_t)m : 0;  // false for NaN / inf / >= 2^63
-  const int32_t sg = (vn > 0.0f) - (vn < 0.0f);
-  return sg * mag;
-}
-
-// Per-tensor divisor state: IEEE xs / norm, fast (Markstein) when norm is in range.
-struct Divisor {
-  float d, r;
-  bool fast;
-  __device__ __forceinline__ explicit Divisor(float norm) : d(norm), r(1.0f / norm) {
-    const float a = fabsf(norm);
-    fast = a >= 0x1p-100f && a <= 0x1p100f;
-  }
-  __device__ __forceinline__ float4 div4(float4 x) const {
-    if (!fast) return make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
-    float4 q = make_float4(div_markstein(x.x, d, r), div_markstein(x.y, d, r), div_markstein(x.z, d, r),
-                           div_markstein(x.w, d, r));
-    const bool need = div_needs_exact(x.x) | div_needs_exact(x.y) | div_needs_exact(x.z) | div_needs_exact(x.w);
-    if (__any(need)) {  // wave-uniform branch: tiny inputs take the exact division
-      if (div_needs_exact(x.x)) q.x = x.x / d;
-      if (div_needs_exact(x.y)) q.y = x.y / d;
-      if (div_needs_exact(x.z)) q.z = x.z / d;
-      if (div_needs_exact(x.w)) q.w = x.w / d;
-    }
-    return q;
-  }
 };
 
 template <int V, bool FULL>
@@ -214,24 +176,13 @@ __device__ __forceinline__ void quant_store(const float4 (&v)[V], const EncArgs&
       const int k = 4 * g + sl;
       const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
       if (!FULL && e >= end) continue;
-      int32_t q0 = 0, q1 = 0, q2 = 0, q3 = 0;
-      if (!zero) {
-#ifdef OMF_EXP_NODIV  // experiment builds only: price the exact division
-        const float4 vn = make_float4(v[k].x * dv.r, v[k].y * dv.r, v[k].z * dv.r, v[k].w * dv.r);
-#else
-        const float4 vn = dv.div4(v[k]);
-#endif
-        q0 = qsgd_level(vn.x, a.levels, uu[sl].x);
-        q1 = qsgd_level(vn.y, a.levels, uu[sl].y);
-        q2 = qsgd_level(vn.z, a.levels, uu[sl].z);
-        q3 = qsgd_level(vn.w, a.levels, uu[sl].w);
-      }
+      int32_t qq[4];
+      qsgd_quad(v[k], uu[sl], dv, a.levels, zero, qq);
+      const int32_t q0 = qq[0], q1 = qq[1], q2 = qq[2], q3 = qq[3];
       if (WIDTH == 1) {
         int8_t* q8 = reinterpret_cast<int8_t*>(a.q);
         if (FULL || e + 4 <= end) {
-          const uint32_t packed = (uint32_t)(uint8_t)q0 | ((uint32_t)(uint8_t)q1 << 8) |
-                                  ((uint32_t)(uint8_t)q2 << 16) | ((uint32_t)(uint8_t)q3 << 24);
-          store_nt(reinterpret_cast<uint32_t*>(q8 + e), packed);
+          store_nt(reinterpret_cast<uint32_t*>(q8 + e), pack_i8x4(qq));
         } else {
           q8[e] = (int8_t)q0;
           if (e + 1 < end) q8[e + 1] = (int8_t)q1;
@@ -516,7 +467,7 @@ struct omf_plan {
   std::vector<int64_t> sizes, offsets;
   int64_t arena_end = 0;
   int64_t cap = 0;               // tensors of <= cap items take the register-resident path
-  int32_t strategy = 1;          // 0 register-resident + two-pass, 1 two-pass only (default: faster on MI355X)
+  int32_t strategy = 2;          // 0 register-resident + two-pass, 1 two-pass only, 2 single-read ring (default)
   uint64_t wait_ticks = kWaitTicks;
   uint32_t epoch = 0;            // last granule tag used (host-side launch counter)
   int32_t ev = 16;               // encode rows per thread (sub-chunk = ev * 1024 elements)
@@ -531,6 +482,18 @@ struct omf_plan {
   void* d_block = nullptr;      // one allocation for everything above
   uint8_t* d_sync = nullptr;    // [ticket u32, err u32, pad 8][counters u32 x nt, pad16][granules u64 x nt, pad16]
   size_t sync_bytes = 0, off_counters = 16, off_gran = 0;
+  // single-read ("ring") encoder, strategy 2 (omf_qsgd_ring.hip)
+  int32_t ring_cfg = 2;         // omf_qsgd_ring.hip kConfigs: 8 loader + 8 quantiser waves, 64 KiB chunks
+  int32_t ring_grid = 0;
+  int32_t ring_big_mode = 1;     // 0: QUANT chunks of a large tensor ring_gap items after its NORM chunks; 1: NORM first, QUANT last
+  int64_t ring_gap = -1;         // items (-1: one grid)
+  int64_t ring_hold_override = 0;  // > 0: hold limit in chunks (tests)
+  uint32_t ring_dbg = 0;           // experiment switches (OMF_RING_DBG), never set in production
+  uint32_t ring_epoch = 0;
+  int64_t n_ring = 0, n_ring_gran = 0, ring_hold_max = 0, ring_two_pass = 0;
+  omf::ring::Item* d_ring = nullptr;
+  omf::ring::Tensor* d_ring_t = nullptr;
+  uint64_t* d_ring_gran = nullptr;
 };
 
 // Plan internals shared with omf_topk.hip.
@@ -588,6 +551,66 @@ static void build_sequence(const omf_plan& p, bool resident_ok, std::vector<Item
   seq.insert(seq.end(), deferred.begin(), deferred.end());
 }
 
+// Ring sequence: tensors of <= ring_hold_max chunks are HOLD chunks (read once);
+// larger ones are NORM chunks (partial only) plus QUANT chunks (second read), the QUANT
+// chunks placed ring_gap items later (big_mode 0) or at the very end with every NORM
+// chunk first (big_mode 1).  Items are dealt to workgroups round-robin.
+static void build_ring_sequence(omf_plan& p, std::vector<omf::ring::Item>& seq,
+                                std::vector<omf::ring::Tensor>& tens) {
+  namespace R = omf::ring;
+  const R::Config c = R::config(p.ring_cfg);
+  const int64_t ch = R::chunk_elems(c);
+  p.ring_hold_max = p.ring_hold_override > 0 ? p.ring_hold_override : (int64_t)c.slots * p.ring_grid;
+  const int64_t gap = p.ring_gap >= 0 ? p.ring_gap : p.ring_grid;
+  seq.clear();
+  tens.assign(p.nt, R::Tensor{});
+  std::vector<R::Item> front, back;
+  std::vector<std::pair<int64_t, std::vector<R::Item>>> pending;  // (insert when seq.size() >= first, items)
+  int64_t gb = 0;
+  p.ring_two_pass = 0;
+  auto flush = [&](bool all) {
+    for (size_t i = 0; i < pending.size();) {
+      if (all || (int64_t)seq.size() >= pending[i].first) {
+        seq.insert(seq.end(), pending[i].second.begin(), pending[i].second.end());
+        pending.erase(pending.begin() + i);
+      } else {
+        ++i;
+      }
+    }
+  };
+  for (int32_t t = 0; t < p.nt; ++t) {
+    const int64_t n = p.sizes[t], b = p.offsets[t];
+    const int64_t nc = (n + ch - 1) / ch;
+    tens[t] = R::Tensor{b, n, (int32_t)nc, (int32_t)gb, {0, 0}};
+    gb += nc;
+    const bool big = nc > p.ring_hold_max;
+    std::vector<R::Item> quant;
+    for (int64_t k = 0; k < nc; ++k) {
+      const int64_t cb = b + k * ch, ce = std::min(b + n, cb + ch);
+      if (!big) {
+        seq.push_back(R::Item{cb, ce, t, R::kPublish | R::kQuant, (int32_t)k, 0});
+        flush(false);
+      } else {
+        const R::Item norm_it{cb, ce, t, R::kPublish, (int32_t)k, 0};
+        if (p.ring_big_mode == 1) front.push_back(norm_it);
+        else seq.push_back(norm_it);
+        quant.push_back(R::Item{cb, ce, t, R::kQuant, (int32_t)k, 0});
+      }
+    }
+    if (big) {
+      ++p.ring_two_pass;
+      if (p.ring_big_mode == 1) back.insert(back.end(), quant.begin(), quant.end());
+      else pending.emplace_back((int64_t)seq.size() + gap, std::move(quant));
+    }
+  }
+  flush(true);
+  if (p.ring_big_mode == 1) {
+    seq.insert(seq.begin(), front.begin(), front.end());
+    seq.insert(seq.end(), back.begin(), back.end());
+  }
+  p.n_ring_gran = std::max<int64_t>(gb, 1);
+}
+
 // (Re)build both sequences and upload every table into one device allocation.
 static int upload_plan(omf_plan* p) {
   std::vector<Item> seq[2], flat;
@@ -595,6 +618,10 @@ static int upload_plan(omf_plan* p) {
   int64_t np[2];
   build_sequence(*p, true, seq[0], tinfo[0], np[0]);
   build_sequence(*p, false, seq[1], tinfo[1], np[1]);
+  std::vector<omf::ring::Item> rseq;
+  std::vector<omf::ring::Tensor> rtens;
+  build_ring_sequence(*p, rseq, rtens);
+  p->n_ring = (int64_t)rseq.size();
   // Flat items (decode, norm-supplied quantise, Top-K passes): one 16 Ki sub-chunk each,
   // the fastest decode granularity measured (profiles/r01_notes.md).
   for (int32_t t = 0; t < p->nt; ++t) {
@@ -622,6 +649,9 @@ static int upload_plan(omf_plan* p) {
   const size_t o_part = o; o = round16(o + 8 * (size_t)p->n_partials);
   const size_t o_sizes = o; o = round16(o + 8 * (size_t)p->nt);
   const size_t o_begins = o; o = round16(o + 8 * (size_t)p->nt);
+  const size_t o_ring = o; o = round16(o + sizeof(omf::ring::Item) * rseq.size());
+  const size_t o_ring_t = o; o = round16(o + sizeof(omf::ring::Tensor) * rtens.size());
+  const size_t o_ring_g = o; o = round16(o + 8 * (size_t)p->n_ring_gran);
   DeviceGuard g(p->device);
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   if (p->d_block) {
@@ -640,6 +670,9 @@ static int upload_plan(omf_plan* p) {
   p->d_partials = reinterpret_cast<uint64_t*>(base + o_part);
   p->d_sizes = reinterpret_cast<int64_t*>(base + o_sizes);
   p->d_begins = reinterpret_cast<int64_t*>(base + o_begins);
+  p->d_ring = reinterpret_cast<omf::ring::Item*>(base + o_ring);
+  p->d_ring_t = reinterpret_cast<omf::ring::Tensor*>(base + o_ring_t);
+  p->d_ring_gran = reinterpret_cast<uint64_t*>(base + o_ring_g);
   OMF_HIP(hipMemcpy(p->d_enc[0], seq[0].data(), sizeof(Item) * seq[0].size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_enc[1], seq[1].data(), sizeof(Item) * seq[1].size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_flat, flat.data(), sizeof(Item) * flat.size(), hipMemcpyHostToDevice));
@@ -647,6 +680,10 @@ static int upload_plan(omf_plan* p) {
   OMF_HIP(hipMemcpy(p->d_tinfo[1], tinfo[1].data(), sizeof(TensorInfo) * p->nt, hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_sizes, p->sizes.data(), 8 * (size_t)p->nt, hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_begins, p->offsets.data(), 8 * (size_t)p->nt, hipMemcpyHostToDevice));
+  if (!rseq.empty())
+    OMF_HIP(hipMemcpy(p->d_ring, rseq.data(), sizeof(omf::ring::Item) * rseq.size(), hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_ring_t, rtens.data(), sizeof(omf::ring::Tensor) * rtens.size(), hipMemcpyHostToDevice));
+  OMF_HIP(hipMemset(p->d_ring_gran, 0, 8 * (size_t)p->n_ring_gran));  // epoch 0 is never a launch's tag
   OMF_HIP(hipMemset(p->d_sync, 0, p->sync_bytes));
   return OMF_OK;
 }
@@ -704,6 +741,17 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
       nb_min = std::min(nb_min, nb);
     }
     p->cap = std::max<int64_t>(1, (int64_t)nb_min * prop.multiProcessorCount / 2);
+    // Ring encoder: configuration and grid (tuning knobs for experiments only).
+    if (const char* rc = getenv("OMF_RING_CFG")) p->ring_cfg = std::max(0, std::min(atoi(rc), omf::ring::num_configs() - 1));
+    if (const char* bm = getenv("OMF_RING_BIG")) p->ring_big_mode = atoi(bm) == 1 ? 1 : 0;
+    if (const char* gp = getenv("OMF_RING_GAP")) p->ring_gap = atoll(gp);
+    if (const char* dg = getenv("OMF_RING_DBG")) p->ring_dbg = (uint32_t)atoi(dg);
+    if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 2));
+    p->ring_grid = omf::ring::grid_size(p->ring_cfg, device);
+    if (p->ring_grid <= 0) {
+      delete p;
+      return fail(OMF_EHIP, "omf_plan_create: cannot size the ring encoder grid");
+    }
   }
   if (int r = upload_plan(p)) {
     if (p->d_block) (void)hipFree(p->d_block);
@@ -722,16 +770,49 @@ int omf_plan_destroy(omf_plan* plan) {
   return OMF_OK;
 }
 
-int64_t omf_plan_encode_items(const omf_plan* plan) { return plan ? plan->n_enc[plan->strategy] : -1; }
+int64_t omf_plan_encode_items(const omf_plan* plan) {
+  if (!plan) return -1;
+  return plan->strategy == 2 ? plan->n_ring : plan->n_enc[plan->strategy];
+}
 
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
-  if (strategy != 0 && strategy != 1) return fail(OMF_EINVAL, "strategy must be 0 (resident) or 1 (two-pass)");
+  if (strategy < 0 || strategy > 2)
+    return fail(OMF_EINVAL, "strategy must be 0 (resident), 1 (two-pass) or 2 (single-read ring)");
   plan->strategy = strategy;
   return OMF_OK;
 }
 
 int64_t omf_plan_resident_capacity(const omf_plan* plan) { return plan ? plan->cap : -1; }
+
+int omf_plan_set_ring(omf_plan* plan, int32_t cfg, int32_t big_mode, int64_t gap, int64_t hold_max) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (cfg >= omf::ring::num_configs() || cfg < -1) return fail(OMF_EINVAL, "omf_plan_set_ring: bad configuration");
+  if (big_mode < -1 || big_mode > 1 || gap < -2 || hold_max < -1)
+    return fail(OMF_EINVAL, "omf_plan_set_ring: bad arguments");
+  if (cfg >= 0 && cfg != plan->ring_cfg) {
+    DeviceGuard g(plan->device);
+    const int grid = omf::ring::grid_size(cfg, plan->device);
+    if (grid <= 0) return fail(OMF_EHIP, "omf_plan_set_ring: cannot size the grid");
+    plan->ring_cfg = cfg;
+    plan->ring_grid = grid;
+  }
+  if (big_mode >= 0) plan->ring_big_mode = big_mode;
+  if (gap >= -1) plan->ring_gap = gap;
+  if (hold_max >= 0) plan->ring_hold_override = hold_max;
+  return upload_plan(plan);
+}
+
+int omf_plan_ring_info(const omf_plan* plan, int64_t* out) {
+  if (!plan || !out) return fail(OMF_EINVAL, "omf_plan_ring_info: NULL argument");
+  out[0] = plan->ring_grid;
+  out[1] = omf::ring::chunk_elems(omf::ring::config(plan->ring_cfg));
+  out[2] = plan->n_ring;
+  out[3] = plan->ring_hold_max;
+  out[4] = plan->ring_two_pass;
+  out[5] = plan->ring_cfg;
+  return OMF_OK;
+}
 
 int omf_plan_set_resident_capacity(omf_plan* plan, int64_t cap, int64_t wait_us) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
@@ -798,14 +879,34 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }
+  if (p->strategy == 2 && !norm_only) {
+    omf::ring::Args r;
+    r.x = x; r.u = u; r.q = q; r.norm_out = norm_out;
+    r.items = p->d_ring; r.tinfo = p->d_ring_t; r.gran = p->d_ring_gran;
+    r.err = reinterpret_cast<uint32_t*>(p->d_sync + 4);
+    r.n_items = p->n_ring;
+    r.alpha = alpha;
+    r.levels = (float)(1u << s);
+    r.seed_lo = (uint32_t)seed; r.seed_hi = (uint32_t)(seed >> 32); r.offset = (uint32_t)offset;
+    if (++p->ring_epoch == 0) ++p->ring_epoch;
+    r.epoch = p->ring_epoch;
+    r.wait_ticks = p->wait_ticks;
+    r.dbg = p->ring_dbg;
+    const int grid = (int)std::min<int64_t>(p->ring_grid, std::max<int64_t>(p->n_ring, 1));
+    if (omf::ring::launch(p->ring_cfg, width, u != nullptr, r, grid, st) != 0)
+      return fail(OMF_EHIP, "ring encoder launch failed");
+    OMF_HIP(hipGetLastError());
+    return OMF_OK;
+  }
   // No per-call memset: tickets and arrival counters are reset in-kernel by their last
   // user, and granules carry this launch's epoch.
+  const int strat = p->strategy == 2 ? 1 : p->strategy;  // norms-only passes use the two-pass tables
   if (++p->epoch == 0) ++p->epoch;
   a.epoch = p->epoch;
-  a.n_items = (uint32_t)p->n_enc[p->strategy];
-  a.items = p->d_enc[p->strategy];
-  a.tinfo = p->d_tinfo[p->strategy];
-  const dim3 grid((unsigned)p->n_enc[p->strategy]);
+  a.n_items = (uint32_t)p->n_enc[strat];
+  a.items = p->d_enc[strat];
+  a.tinfo = p->d_tinfo[strat];
+  const dim3 grid((unsigned)p->n_enc[strat]);
 #define OMF_ENC(EV)                                                                              \
   do {                                                                                           \
     if (norm_only) {                                                                             \

@@ -1,0 +1,455 @@
+// omf_qsgd_ring.hip — single-read QSGD encoder for the hybrid global hop, MI355X (gfx950).
+//
+// Semantics: SURVEY.md §8a "Exact QSGD semantics" (reference src/omnifed/hybrid/compression/
+// qsgd.py:36-64): one fp32 L2 norm per tensor, then per-element stochastic levels.  The
+// norm of a tensor is known only once all of it has been read, so a straightforward
+// encoder reads x twice (9 N bytes of HBM traffic for an int8 payload).  This one reads
+// it once (5 N):
+//
+//   * persistent workgroups walk a host-built sequence of chunks (item i -> workgroup
+//     i mod grid, so consecutive chunks of a tensor spread over the whole chip);
+//   * a chunk is loaded into registers, its partial sum of squares is published as an
+//     8-byte {epoch, fp32} granule (sc1 store), and the chunk waits in an LDS ring slot
+//     of its workgroup until every granule of its tensor carries this launch's epoch;
+//   * every consumer folds the granules in the same fixed order (thread j sums granules
+//     j, j + NT, ... in fp64, then a fixed block reduction), so the norm is identical in
+//     every workgroup and every run;
+//   * the poll for the ring head is issued BEFORE the next chunk's loads, so waiting for
+//     it (vmcnt counts in order) leaves the chunk loads in flight while the head is
+//     quantised from LDS;
+//   * a workgroup only blocks (ring full) after publishing every chunk it has taken, so
+//     the sequence is deadlock-free for co-resident workgroups; a bounded wait that
+//     expires recomputes the norm from x in the producers' exact order (same bits) and
+//     sets err bit 2 (omf_plan_check returns 1) — the kernel cannot hang.
+//
+// Tensors too large to hold (> slots x grid chunks) are NORM chunks (partial only) plus
+// QUANT chunks (re-read once the norm is known), placed by the plan (omf_qsgd.hip).
+//
+// Element layout inside a chunk (rows of 1024 elements; thread t, float4 k):
+//   row = rows_per_thread * (t >> 8) + k,  element = row * 1024 + 4 * (t & 255)
+// so a wave reads 1 KiB contiguous per instruction and a thread's four consecutive rows
+// form one Philox group of the stream in oracle/philox.py.
+#include "../../include/omf_codec.h"
+#include "omf_common.h"
+#include "omf_qsgd_dev.h"
+#include "omf_ring.h"
+
+namespace omf {
+namespace ring {
+namespace {
+
+// Block-uniform values the compiler cannot prove uniform (barrier votes, LDS reductions):
+// readfirstlane keeps them (and the ring bookkeeping that depends on them) in SGPRs.
+__device__ __forceinline__ int ufirst(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float ufirst(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+__device__ __forceinline__ float4 scale4(float4 v, float alpha) {
+  return make_float4(__fmul_rn(v.x, alpha), __fmul_rn(v.y, alpha), __fmul_rn(v.z, alpha), __fmul_rn(v.w, alpha));
+}
+
+__device__ __forceinline__ float sumsq4(float4 v, float acc) {
+  acc = fmaf(v.x, v.x, acc);
+  acc = fmaf(v.y, v.y, acc);
+  acc = fmaf(v.z, v.z, acc);
+  return fmaf(v.w, v.w, acc);
+}
+
+// Uniforms of Philox group G (3 calls, 16 x 24-bit fields; oracle/philox.py).
+__device__ __forceinline__ void philox_group(const Args& a, uint64_t G, int32_t tensor, float4 (&uu)[4]) {
+  uint32_t w[12];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const uint64_t ctr = 3 * G + c;
+    const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)tensor, a.offset),
+                                  a.seed_lo, a.seed_hi);
+    w[4 * c] = r.x; w[4 * c + 1] = r.y; w[4 * c + 2] = r.z; w[4 * c + 3] = r.w;
+  }
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) uu[sl] = u24x4(w[3 * sl], w[3 * sl + 1], w[3 * sl + 2]);
+}
+
+// Quantise and store rows 4rg .. 4rg+3 at lane position j (float4 j of each row) of the
+// chunk [cb, ce) of tensor `tensor` (chunk offset coff within it); w = those four float4,
+// already scaled by alpha.  Philox group G = (coff/4096 + rg)*256 + j (oracle/philox.py).
+template <int WIDTH, bool HAS_U>
+__device__ __forceinline__ void quant_group_at(const Args& a, const float4 (&w)[4], int rg, int j, int64_t cb,
+                                               int64_t ce, int64_t coff, int32_t tensor, float norm, bool full) {
+  const int n = (int)(ce - cb);
+  float4 uu[4];
+  if (HAS_U) {
+    const float* __restrict__ ub = a.u + cb;
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) {
+      const int e = (4 * rg + sl) * 1024 + 4 * j;
+      if (full || e + 4 <= n) {
+        uu[sl] = *reinterpret_cast<const float4*>(ub + e);
+      } else {
+        uu[sl] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < n) uu[sl].x = ub[e];
+        if (e + 1 < n) uu[sl].y = ub[e + 1];
+        if (e + 2 < n) uu[sl].z = ub[e + 2];
+      }
+    }
+  } else {
+    philox_group(a, ((uint64_t)(coff >> 12) + (uint64_t)rg) * 256u + (uint64_t)j, tensor, uu);
+  }
+  const bool zero = !(norm != 0.0f);  // norm == 0: all-zero payload (reference: dense passthrough)
+  const Divisor dv(norm);
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+    const int e = (4 * rg + sl) * 1024 + 4 * j;
+    if (!full && e >= n) continue;
+    int32_t qq[4];
+    qsgd_quad(w[sl], uu[sl], dv, a.levels, zero, qq);
+    const int32_t q0 = qq[0], q1 = qq[1], q2 = qq[2], q3 = qq[3];
+    if (WIDTH == 1) {
+      int8_t* q8 = reinterpret_cast<int8_t*>(a.q) + cb;
+      if (full || e + 4 <= n) {
+        store_nt(reinterpret_cast<uint32_t*>(q8 + e), pack_i8x4(qq));
+      } else {
+        q8[e] = (int8_t)q0;
+        if (e + 1 < n) q8[e + 1] = (int8_t)q1;
+        if (e + 2 < n) q8[e + 2] = (int8_t)q2;
+      }
+    } else {
+      int32_t* q32 = reinterpret_cast<int32_t*>(a.q) + cb;
+      if (full || e + 4 <= n) {
+        store_nt(q32 + e, make_int4(q0, q1, q2, q3));
+      } else {
+        q32[e] = q0;
+        if (e + 1 < n) q32[e + 1] = q1;
+        if (e + 2 < n) q32[e + 2] = q2;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------- producer/consumer kernel
+//
+// One 1024-thread workgroup per CU: waves 0-7 are LOADERS, waves 8-15 QUANTISERS, and
+// they synchronise only through LDS flags (no workgroup barrier after the prologue), so
+// each role needs only its own registers and a loader's prefetch is never drained by a
+// barrier or by another role's wait.
+//
+// Chunk = ROWS rows of 1024 elements.  Loader wave w owns rows [w*ROWS/8, (w+1)*ROWS/8):
+// lane l loads float4 l, l+64, l+128, l+192 of each row (1 KiB contiguous per wave
+// instruction), reduces them in that order (fp32 fma chain), stores them into the slot
+// (row-major, the same addresses) and publishes its wave partial; the last loader to
+// arrive folds the 8 wave partials in order (fp64), publishes the chunk granule and
+// marks the slot loaded.  Quantiser thread u (0..511) owns row-groups rg = (u>>8)*GPT+h,
+// lane position j = u & 255: the Philox group of oracle/philox.py.
+//
+// Slot life: loaders wait freed[s] >= k-S+1, fill, loaded[s] = k+1; quantiser wave 0
+// resolves the norm (single-chunk partial, cached tensor, or the granule poll) and sets
+// qready[s] = k+1; every quantiser wave quantises its groups, the last sets freed[s] = k+1.
+
+__device__ __forceinline__ uint32_t lds_ld(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_st(uint32_t* p, uint32_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ uint32_t lds_add(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// This wave's LDS writes have landed (LDS only; in-flight global loads stay in flight).
+__device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v) {
+  while (ufirst((int)lds_ld(p)) < (int)v) __builtin_amdgcn_s_sleep(1);
+  asm volatile("" ::: "memory");
+}
+
+// Sum of squares of one loader wave's rows of a chunk, in the loader's exact order.
+template <int ROWS, int LW>
+__device__ __forceinline__ float loader_sumsq(const Args& a, int64_t cb, int n, int w, int lane) {
+  constexpr int RPW = ROWS / LW;
+  const float* __restrict__ xb = a.x + cb;
+  float acc = 0.0f;
+  for (int r = 0; r < RPW; ++r)
+    for (int m = 0; m < 4; ++m) {
+      const int i = (w * RPW + r) * 1024 + 4 * (lane + 64 * m);
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i + 4 <= n) {
+        v = *reinterpret_cast<const float4*>(xb + i);
+      } else {
+        if (i < n) v.x = xb[i];
+        if (i + 1 < n) v.y = xb[i + 1];
+        if (i + 2 < n) v.z = xb[i + 2];
+      }
+      acc = sumsq4(scale4(v, a.alpha), acc);
+    }
+  return acc;
+}
+
+// Granule fold of one tensor by ONE wave: lane l sums granules l, l+64, ... (fp64, in
+// order), then the fixed butterfly.  Identical in every workgroup.
+__device__ __forceinline__ bool poll_norm_wave(const Args& a, const Tensor& ti, int lane, float& norm) {
+  double p = 0.0;
+  int ok = 1;
+  for (int j = lane; j < ti.nchunks; j += 64) {
+    const uint64_t g = ld_agent(&a.gran[ti.gbase + j]);
+    ok &= (uint32_t)(g >> 32) == a.epoch;
+    p += (double)__uint_as_float((uint32_t)g);
+  }
+  if (!__all(ok)) return false;
+  norm = ufirst(sqrtf((float)wave_sum_f64(p)));
+  return true;
+}
+
+// Bounded poll; on expiry recompute every chunk partial exactly as the loaders do (8 wave
+// partials folded in order) and fold them like the poll: same bits, err bit 2 set.
+template <int ROWS, int LW>
+__device__ __forceinline__ float wait_norm_wave(const Args& a, const Tensor& ti, int lane) {
+  constexpr int64_t CH = (int64_t)ROWS * 1024;
+  const uint64_t t0 = wall_clock64();
+  float norm;
+  for (;;) {
+    if (poll_norm_wave(a, ti, lane, norm)) return norm;
+    if (ufirst((int)(wall_clock64() - t0 > a.wait_ticks))) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+  double p = 0.0;
+  for (int c = 0; c < ti.nchunks; ++c) {
+    const int64_t cb = ti.begin + (int64_t)c * CH;
+    const int n = (int)min(CH, ti.begin + ti.n - cb);
+    double fold = 0.0;
+    for (int w = 0; w < LW; ++w) fold += wave_sum_f64((double)loader_sumsq<ROWS, LW>(a, cb, n, w, lane));
+    if ((c & 63) == lane) p += (double)(float)fold;
+  }
+  if (lane == 0) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return ufirst(sqrtf((float)wave_sum_f64(p)));
+}
+
+// ROWS rows per chunk, S LDS slots, LW loader waves (the other 16 - LW quantise), DB:
+// loaders double-buffer their registers (prefetch two chunks ahead).
+template <int ROWS, int S, int LW, bool DB, int WIDTH, bool HAS_U>
+__global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __restrict__ items,
+                                                          const Tensor* __restrict__ tinfo) {
+  // items / tinfo are read-only for the launch: __restrict__ lets the compiler use scalar
+  // (SMEM) loads, whose lgkmcnt waits never drain the in-flight chunk loads and payload
+  // stores the way a vector table load's vmcnt(0) would.
+  constexpr int QW = 16 - LW;               // quantiser waves
+  constexpr int RPW = ROWS / LW;            // rows per loader wave
+  constexpr int VL = RPW * 4;               // float4 per loader lane
+  constexpr int GPT = (ROWS / 4) * 256 / (QW * 64);  // Philox groups per quantiser thread
+  constexpr int CH = ROWS * 1024;           // chunk elements
+  static_assert(ROWS % 4 == 0 && ROWS % LW == 0 && S >= 2, "configuration");
+  static_assert(GPT >= 1 && GPT * QW * 64 == (ROWS / 4) * 256, "quantiser threads must tile the groups");
+  __shared__ float4 slots[S][ROWS * 256];
+  __shared__ double lpart[S][LW];
+  __shared__ float cpart[S], qnorm[S];
+  __shared__ uint32_t arrive[S], loaded[S], freed[S], qdone[S], qready[S];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = ufirst(t >> 6);
+  if (t < S) {
+    arrive[t] = 0; loaded[t] = 0; freed[t] = 0; qdone[t] = 0; qready[t] = 0;
+  }
+  __syncthreads();
+  const int64_t G = gridDim.x, n_items = a.n_items;
+
+  if (wave < LW) {
+    // ------------------------------------------------------------ loader
+    const int w = wave;
+    auto issue = [&](float4 (&v)[VL], const Item& it) {
+      const float* __restrict__ xb = a.x + it.begin;
+      const int n = (int)(it.end - it.begin);
+      if (n == CH) {  // block-uniform: every chunk but a tensor's last
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+          for (int m = 0; m < 4; ++m)
+            v[4 * r + m] = *reinterpret_cast<const float4*>(xb + (w * RPW + r) * 1024 + 4 * (lane + 64 * m));
+      } else {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int i = (w * RPW + r) * 1024 + 4 * (lane + 64 * m);
+            float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (i + 4 <= n) {
+              z = *reinterpret_cast<const float4*>(xb + i);
+            } else {
+              if (i < n) z.x = xb[i];
+              if (i + 1 < n) z.y = xb[i + 1];
+              if (i + 2 < n) z.z = xb[i + 2];
+            }
+            v[4 * r + m] = z;
+          }
+      }
+    };
+    auto step = [&](float4 (&v)[VL], Item& it, int64_t& idx, int64_t& k) {
+      const int s = (int)(k % S);
+      if (k >= S) lds_wait_ge(&freed[s], (uint32_t)(k - S + 1));
+      float acc = 0.0f;
+#pragma unroll
+      for (int q = 0; q < VL; ++q) {
+        v[q] = scale4(v[q], a.alpha);
+        acc = sumsq4(v[q], acc);
+      }
+      if (it.flags & kQuant) {
+#pragma unroll
+        for (int r = 0; r < RPW; ++r)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) slots[s][(w * RPW + r) * 256 + lane + 64 * m] = v[4 * r + m];
+      }
+      const double wp = wave_sum_f64((double)acc);
+      if (lane == 0) lpart[s][w] = wp;
+      lds_drain();
+      const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&arrive[s], 1u) : 0u));
+      if (old == LW - 1) {  // last loader of this chunk
+        double fold = 0.0;
+#pragma unroll
+        for (int j = 0; j < LW; ++j) fold += lpart[s][j];
+        const float part = (float)fold;
+        if (lane == 0) {
+          if (it.flags & kPublish) {
+            const Tensor ti = tinfo[it.tensor];
+            st_agent(&a.gran[ti.gbase + it.chunk], ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(part));
+          }
+          cpart[s] = part;
+          lds_st(&arrive[s], 0u);
+          lds_drain();
+          if (it.flags & kQuant) lds_st(&loaded[s], (uint32_t)(k + 1));
+          else lds_st(&freed[s], (uint32_t)(k + 1));  // NORM chunk: nothing to quantise
+        }
+      }
+      idx += (DB ? 2 : 1) * G;
+      k += DB ? 2 : 1;
+      if (idx < n_items) {
+        it = items[idx];
+        issue(v, it);
+      }
+    };
+    if (DB) {
+      int64_t ia = blockIdx.x, ib = ia + G, ka = 0, kb = 1;
+      float4 va[VL], vb[VL];
+      Item ita{}, itb{};
+      if (ia < n_items) { ita = items[ia]; issue(va, ita); }
+      if (ib < n_items) { itb = items[ib]; issue(vb, itb); }
+      for (;;) {
+        if (ia >= n_items) break;
+        step(va, ita, ia, ka);
+        if (ib >= n_items) break;
+        step(vb, itb, ib, kb);
+      }
+    } else {
+      int64_t ia = blockIdx.x, ka = 0;
+      float4 va[VL];
+      Item ita{};
+      if (ia < n_items) { ita = items[ia]; issue(va, ita); }
+      while (ia < n_items) step(va, ita, ia, ka);
+    }
+    return;
+  }
+
+  // -------------------------------------------------------------- quantiser
+  const int qw = wave - LW;
+  const int u = t - LW * 64;
+  int32_t cached_t = -1;
+  float cached_norm = 0.0f;
+  int64_t k = 0;
+  for (int64_t idx = blockIdx.x; idx < n_items; idx += G, ++k) {
+    const Item it = items[idx];
+    if (!(it.flags & kQuant)) continue;
+    const int s = (int)(k % S);
+    lds_wait_ge(&loaded[s], (uint32_t)(k + 1));
+    const Tensor ti = tinfo[it.tensor];
+    float norm;
+    if (qw == 0) {
+      if ((it.flags & kPublish) && ti.nchunks == 1) {
+        norm = ufirst(sqrtf(cpart[s]));
+      } else if (it.tensor == cached_t) {
+        norm = cached_norm;
+      } else if (a.dbg & 1) {
+        norm = 1.0f;
+      } else {
+        norm = wait_norm_wave<ROWS, LW>(a, ti, lane);
+        cached_t = it.tensor;
+        cached_norm = norm;
+      }
+      if (lane == 0) {
+        qnorm[s] = norm;
+        lds_drain();
+        lds_st(&qready[s], (uint32_t)(k + 1));
+        if (it.chunk == 0) a.norm_out[it.tensor] = norm;
+      }
+    } else {
+      lds_wait_ge(&qready[s], (uint32_t)(k + 1));
+      norm = ufirst(qnorm[s]);
+    }
+    const bool full = it.end - it.begin == CH;
+    const int64_t coff = it.begin - ti.begin;
+#pragma unroll
+    for (int h = 0; h < GPT; ++h) {
+      if (a.dbg & 2) break;
+      const int rg = (u >> 8) * GPT + h, j = u & 255;
+      float4 w4[4];
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) w4[sl] = slots[s][(4 * rg + sl) * 256 + j];
+      quant_group_at<WIDTH, HAS_U>(a, w4, rg, j, it.begin, it.end, coff, it.tensor, norm, full);
+    }
+    lds_drain();
+    const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&qdone[s], 1u) : 0u));
+    if (old == QW - 1 && lane == 0) {
+      lds_st(&qdone[s], 0u);
+      lds_drain();
+      lds_st(&freed[s], (uint32_t)(k + 1));
+    }
+  }
+}
+
+// Instantiated configurations: {rows of 1024 elements per chunk, LDS slots, loader
+// waves, loader double-buffering}.
+constexpr Config kConfigs[] = {
+    {12, 3, 4, 0},  // 48 KiB chunks x 3 slots, 4 loader + 12 quantiser waves
+    {12, 3, 4, 1},  // same, loaders prefetch two chunks
+    {16, 2, 8, 1},  // 64 KiB chunks x 2 slots, 8 + 8 waves
+    {8, 4, 8, 1},   // 32 KiB chunks x 4 slots, 8 + 8 waves
+};
+
+template <int ROWS, int S, int LW, bool DB>
+const void* kernel_ptr(int width, bool has_u) {
+  if (width == 1) {
+    return has_u ? (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 1, true>
+                 : (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 1, false>;
+  }
+  return has_u ? (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 4, true>
+               : (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 4, false>;
+}
+
+const void* kernel_for(int cfg, int width, bool has_u) {
+  switch (cfg) {
+    case 1: return kernel_ptr<12, 3, 4, true>(width, has_u);
+    case 2: return kernel_ptr<16, 2, 8, true>(width, has_u);
+    case 3: return kernel_ptr<8, 4, 8, true>(width, has_u);
+    default: return kernel_ptr<12, 3, 4, false>(width, has_u);
+  }
+}
+
+}  // namespace
+
+int num_configs() { return (int)(sizeof(kConfigs) / sizeof(kConfigs[0])); }
+
+Config config(int cfg) { return kConfigs[(cfg >= 0 && cfg < num_configs()) ? cfg : 0]; }
+
+int grid_size(int cfg, int device) {
+  (void)cfg;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return -1;
+  return prop.multiProcessorCount;  // one 1024-thread workgroup per CU (the LDS ring fills it)
+}
+
+int launch(int cfg, int width, bool has_u, const Args& a, int grid, hipStream_t st) {
+  const void* k = kernel_for(cfg, width == 1 ? 1 : 4, has_u);
+  if (!k) return -1;
+  Args args = a;
+  const Item* items = a.items;
+  const Tensor* tinfo = a.tinfo;
+  void* params[] = {&args, &items, &tinfo};
+  return hipLaunchKernel(k, dim3((unsigned)grid), dim3(1024), params, 0, st) == hipSuccess ? 0 : -1;
+}
+
+}  // namespace ring
+}  // namespace omf

@@ -193,7 +193,7 @@ def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, dev
     out_dev = _out_device(base_tensor, device)
     dev = _gpu_for(out_dev)
     v = torch.from_numpy(values.copy()).to(dev)
-    ix = torch.from_numpy(np.ascontiguousarray(indices)).to(dev)
+    ix = torch.from_numpy(np.array(indices, dtype=np.int64, copy=True)).to(dev)
     y = torch.empty(max(numel, 4), dtype=torch.float32, device=dev)
     if base_tensor is not None:
         y[:numel].copy_(base_tensor.detach().reshape(-1).to(dev, torch.float32))

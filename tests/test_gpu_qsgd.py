@@ -97,9 +97,9 @@ def _mixed_arena(gpu, sizes, seed=3, scale=-9):
     return plan, x.to(gpu), parts
 
 
-@pytest.mark.parametrize("strategy", ["resident", "ordered"])
+@pytest.mark.parametrize("strategy", ["ring", "resident", "ordered"])
 def test_gpu_norm_accuracy_and_single_launch_parity(gpu, strategy):
-    """Single-launch encode (in-kernel norm hand-off; both strategies) vs oracle given the GPU norm."""
+    """Single-launch encode (in-kernel norm hand-off; every strategy) vs oracle given the GPU norm."""
     for s in (3, 4, 8):
         plan, x, parts = _mixed_arena(gpu, MIXED_SIZES, seed=10 * s)
         plan.set_encode_strategy(strategy)
@@ -118,8 +118,11 @@ def test_gpu_norm_accuracy_and_single_launch_parity(gpu, strategy):
             assert qh[o:o + n].tobytes() == want.tobytes(), (s, n)
         # norm-only entry point returns the identical norms
         n2 = plan.qsgd_norms(x)
-        assert torch.equal(n2, norms)
-        plan.set_encode_strategy("ordered")  # restore the default on the cached plan
+        if strategy != "ring":  # the ring folds 64 KiB chunk partials, qsgd_norms 256 KiB items
+            assert torch.equal(n2, norms)
+        else:
+            torch.testing.assert_close(n2, norms, rtol=2e-6, atol=0)
+        plan.set_encode_strategy("ring")  # restore the default on the cached plan
 
 
 def test_strategies_agree_and_fallback_exact(gpu):
@@ -138,7 +141,11 @@ def test_strategies_agree_and_fallback_exact(gpu):
     # the strategies fold partials over different slab sizes: norms agree to rounding, and each
     # payload is exact for its own norm (checked against the oracle elsewhere)
     torch.testing.assert_close(n1, n2, rtol=2e-6, atol=0)
-    for strategy in ("resident", "ordered"):
+    plan.set_encode_strategy("ring")
+    q3, n3 = plan.qsgd_encode(x, 4, seed=3, offset=1)
+    assert plan.check()
+    torch.testing.assert_close(n3, n2, rtol=2e-6, atol=0)
+    for strategy in ("ring", "resident", "ordered"):
         small = codec.Plan([40000] * 8 + [1 << 20], device=gpu)
         small.set_encode_strategy(strategy)
         xs = torch.randn(small.arena_end, device=gpu, generator=g)
@@ -150,6 +157,35 @@ def test_strategies_agree_and_fallback_exact(gpu):
         assert torch.equal(na, nb)
         for o, n in zip(small.offsets, small.sizes):
             assert torch.equal(qa[o:o + n], qb[o:o + n])
+
+
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3])
+@pytest.mark.parametrize("hold", [0, 3])
+def test_ring_configs_match_oracle(gpu, cfg, hold):
+    """Every ring configuration, with large tensors held (hold=0) or taking two passes (hold=3
+    chunks), gives the oracle's payload for its own norms, in both draw modes."""
+    plan, x, parts = _mixed_arena(gpu, MIXED_SIZES + [300_000, 1 << 20], seed=31 + cfg)
+    plan = codec.Plan(plan.sizes, device=gpu)
+    plan.set_encode_strategy("ring")
+    plan.set_ring(cfg=cfg, hold_max=hold)
+    info = plan.ring_info
+    assert info["cfg"] == cfg and (hold == 0 or info["two_pass_tensors"] >= 1)
+    s = 4
+    q, norms = plan.qsgd_encode(x, s, seed=11, offset=5)
+    assert plan.check()
+    qh, nh = q.cpu().numpy(), norms.cpu().numpy()
+    for t, (o, n, p) in enumerate(zip(plan.offsets, plan.sizes, parts)):
+        ref = float(np.sqrt(np.sum(p.astype(np.float64) ** 2)))
+        assert nh[t] == pytest.approx(ref, rel=NORM_RTOL)
+        want = _oracle_q(p, s, float(nh[t]), oracle.philox_uniforms(11, 5, t, n))
+        assert qh[o:o + n].tobytes() == want.tobytes(), (t, n)
+    u_host = np.random.default_rng(cfg).random(plan.arena_end, dtype=np.float32)
+    q8, n8 = plan.qsgd_encode(x, 8, u=_dev(u_host, gpu))
+    assert torch.equal(n8, norms)
+    q8h = q8.cpu().numpy()
+    for t, (o, n, p) in enumerate(zip(plan.offsets, plan.sizes, parts)):
+        want = _oracle_q(p, 8, float(nh[t]), u_host[o:o + n])
+        assert q8h[o:o + n].tobytes() == want.tobytes(), (t, n)
 
 
 def test_philox_mode_matches_numpy_philox(gpu):
