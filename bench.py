@@ -175,7 +175,7 @@ def main():
     dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evd]))
     enc_bytes = (4 + w) * N
     dec_bytes = (w + 4) * N
-    dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, "qsgd_encode_ordered") if enc_ms >= dec_ms else \
+    dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, plan.encoder_kernel) if enc_ms >= dec_ms else \
         (dec_ms, dec_bytes, "qsgd_decode_flat")
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     traffic = None

@@ -86,6 +86,9 @@ int omf_plan_set_ring(omf_plan* plan, int32_t cfg, int32_t big_mode, int64_t gap
 /* Ring encoder facts: out[0] grid, out[1] chunk elements, out[2] items, out[3] hold limit
  * (chunks), out[4] tensors taking two passes, out[5] configuration. */
 int omf_plan_ring_info(const omf_plan* plan, int64_t* out6);
+/* Experiment hook: per-phase cycle totals of ring launches made with OMF_RING_DBG bit 4
+ * set in the environment at plan creation (zeros otherwise); read and reset. */
+int omf_plan_ring_profile(omf_plan* plan, int64_t* out16);
 /* Largest tensor (in 16 Ki-element items) that takes the register-resident path: half the
  * encoder's co-resident workgroups (occupancy x CUs). */
 int64_t omf_plan_resident_capacity(const omf_plan* plan);

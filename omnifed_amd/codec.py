@@ -12,6 +12,7 @@ buffer shorter than the plan assumes.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -93,6 +94,8 @@ class Plan:
         self._h = h
         self._lock = threading.Lock()
         self._topk_ws: Optional[torch.Tensor] = None
+        # the library's default (omf_qsgd.hip), unless an experiment overrides it
+        self.strategy = {"0": "resident", "1": "ordered"}.get(os.environ.get("OMF_ENCODE_STRATEGY", ""), "ring")
 
     @classmethod
     def get(cls, sizes, offsets=None, device=None, chunk: int = 0) -> "Plan":
@@ -141,10 +144,22 @@ class Plan:
         (register-resident small tensors + two-pass)."""
         code = {"resident": 0, "ordered": 1, "ring": 2}[strategy]
         check(lib().omf_plan_set_encode_strategy(self._h, code), "omf_plan_set_encode_strategy")
+        self.strategy = strategy
+
+    @property
+    def encoder_kernel(self) -> str:
+        """Name of the kernel one encode launch runs (profiling / roofline bookkeeping)."""
+        return "qsgd_encode_pc" if self.strategy == "ring" else "qsgd_encode_ordered"
 
     def set_ring(self, cfg: int = -1, big_mode: int = -1, gap: int = -2, hold_max: int = -1) -> None:
         """Tuning / test hook of the ring encoder: see omf_plan_set_ring."""
         check(lib().omf_plan_set_ring(self._h, int(cfg), int(big_mode), int(gap), int(hold_max)), "omf_plan_set_ring")
+
+    def ring_profile(self) -> List[int]:
+        """Experiment hook: per-phase cycle totals (OMF_RING_DBG bit 4), read and reset."""
+        out = (ctypes.c_int64 * 16)()
+        check(lib().omf_plan_ring_profile(self._h, out), "omf_plan_ring_profile")
+        return [int(v) for v in out]
 
     @property
     def ring_info(self) -> Dict[str, int]:

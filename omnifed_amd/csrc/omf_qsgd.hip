@@ -483,7 +483,7 @@ struct omf_plan {
   uint8_t* d_sync = nullptr;    // [ticket u32, err u32, pad 8][counters u32 x nt, pad16][granules u64 x nt, pad16]
   size_t sync_bytes = 0, off_counters = 16, off_gran = 0;
   // single-read ("ring") encoder, strategy 2 (omf_qsgd_ring.hip)
-  int32_t ring_cfg = 2;         // omf_qsgd_ring.hip kConfigs: 8 loader + 8 quantiser waves, 64 KiB chunks
+  int32_t ring_cfg = 0;         // omf_qsgd_ring.hip kConfigs[0]: 64 KiB chunks, 8 loader + 8 quantiser waves
   int32_t ring_grid = 0;
   int32_t ring_big_mode = 1;     // 0: QUANT chunks of a large tensor ring_gap items after its NORM chunks; 1: NORM first, QUANT last
   int64_t ring_gap = -1;         // items (-1: one grid)
@@ -494,6 +494,7 @@ struct omf_plan {
   omf::ring::Item* d_ring = nullptr;
   omf::ring::Tensor* d_ring_t = nullptr;
   uint64_t* d_ring_gran = nullptr;
+  unsigned long long* d_ring_prof = nullptr;  // 16 phase counters (OMF_RING_DBG & 4)
 };
 
 // Plan internals shared with omf_topk.hip.
@@ -588,13 +589,13 @@ static void build_ring_sequence(omf_plan& p, std::vector<omf::ring::Item>& seq,
     for (int64_t k = 0; k < nc; ++k) {
       const int64_t cb = b + k * ch, ce = std::min(b + n, cb + ch);
       if (!big) {
-        seq.push_back(R::Item{cb, ce, t, R::kPublish | R::kQuant, (int32_t)k, 0});
+        seq.push_back(R::Item{cb, ce, b, n, t, R::kPublish | R::kQuant, (int32_t)k, (int32_t)nc, (int32_t)(gb - nc), {0, 0, 0}});
         flush(false);
       } else {
-        const R::Item norm_it{cb, ce, t, R::kPublish, (int32_t)k, 0};
+        const R::Item norm_it{cb, ce, b, n, t, R::kPublish, (int32_t)k, (int32_t)nc, (int32_t)(gb - nc), {0, 0, 0}};
         if (p.ring_big_mode == 1) front.push_back(norm_it);
         else seq.push_back(norm_it);
-        quant.push_back(R::Item{cb, ce, t, R::kQuant, (int32_t)k, 0});
+        quant.push_back(R::Item{cb, ce, b, n, t, R::kQuant, (int32_t)k, (int32_t)nc, (int32_t)(gb - nc), {0, 0, 0}});
       }
     }
     if (big) {
@@ -652,6 +653,7 @@ static int upload_plan(omf_plan* p) {
   const size_t o_ring = o; o = round16(o + sizeof(omf::ring::Item) * rseq.size());
   const size_t o_ring_t = o; o = round16(o + sizeof(omf::ring::Tensor) * rtens.size());
   const size_t o_ring_g = o; o = round16(o + 8 * (size_t)p->n_ring_gran);
+  const size_t o_ring_p = o; o = round16(o + 8 * 16);
   DeviceGuard g(p->device);
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   if (p->d_block) {
@@ -673,6 +675,8 @@ static int upload_plan(omf_plan* p) {
   p->d_ring = reinterpret_cast<omf::ring::Item*>(base + o_ring);
   p->d_ring_t = reinterpret_cast<omf::ring::Tensor*>(base + o_ring_t);
   p->d_ring_gran = reinterpret_cast<uint64_t*>(base + o_ring_g);
+  p->d_ring_prof = reinterpret_cast<unsigned long long*>(base + o_ring_p);
+  OMF_HIP(hipMemset(p->d_ring_prof, 0, 8 * 16));
   OMF_HIP(hipMemcpy(p->d_enc[0], seq[0].data(), sizeof(Item) * seq[0].size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_enc[1], seq[1].data(), sizeof(Item) * seq[1].size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_flat, flat.data(), sizeof(Item) * flat.size(), hipMemcpyHostToDevice));
@@ -803,6 +807,15 @@ int omf_plan_set_ring(omf_plan* plan, int32_t cfg, int32_t big_mode, int64_t gap
   return upload_plan(plan);
 }
 
+int omf_plan_ring_profile(omf_plan* plan, int64_t* out16) {
+  if (!plan || !out16) return fail(OMF_EINVAL, "omf_plan_ring_profile: NULL argument");
+  DeviceGuard g(plan->device);
+  OMF_HIP(hipDeviceSynchronize());
+  OMF_HIP(hipMemcpy(out16, plan->d_ring_prof, 8 * 16, hipMemcpyDeviceToHost));
+  OMF_HIP(hipMemset(plan->d_ring_prof, 0, 8 * 16));
+  return OMF_OK;
+}
+
 int omf_plan_ring_info(const omf_plan* plan, int64_t* out) {
   if (!plan || !out) return fail(OMF_EINVAL, "omf_plan_ring_info: NULL argument");
   out[0] = plan->ring_grid;
@@ -892,6 +905,7 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
     r.epoch = p->ring_epoch;
     r.wait_ticks = p->wait_ticks;
     r.dbg = p->ring_dbg;
+    r.prof = p->d_ring_prof;
     const int grid = (int)std::min<int64_t>(p->ring_grid, std::max<int64_t>(p->n_ring, 1));
     if (omf::ring::launch(p->ring_cfg, width, u != nullptr, r, grid, st) != 0)
       return fail(OMF_EHIP, "ring encoder launch failed");

@@ -45,6 +45,10 @@ __device__ __forceinline__ float ufirst(float v) {
   return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
 }
 
+__device__ __forceinline__ Tensor tensor_of(const Item& it) {
+  return Tensor{it.tbegin, it.tn, it.nchunks, it.gbase, {0, 0}};
+}
+
 __device__ __forceinline__ float4 scale4(float4 v, float alpha) {
   return make_float4(__fmul_rn(v.x, alpha), __fmul_rn(v.y, alpha), __fmul_rn(v.z, alpha), __fmul_rn(v.w, alpha));
 }
@@ -93,7 +97,11 @@ __device__ __forceinline__ void quant_group_at(const Args& a, const float4 (&w)[
       }
     }
   } else {
+#ifdef OMF_EXP_NORNG  // experiment builds only: price the RNG
+    for (int sl = 0; sl < 4; ++sl) uu[sl] = make_float4(0.5f, 0.25f, 0.75f, 0.125f);
+#else
     philox_group(a, ((uint64_t)(coff >> 12) + (uint64_t)rg) * 256u + (uint64_t)j, tensor, uu);
+#endif
   }
   const bool zero = !(norm != 0.0f);  // norm == 0: all-zero payload (reference: dense passthrough)
   const Divisor dv(norm);
@@ -107,7 +115,8 @@ __device__ __forceinline__ void quant_group_at(const Args& a, const float4 (&w)[
     if (WIDTH == 1) {
       int8_t* q8 = reinterpret_cast<int8_t*>(a.q) + cb;
       if (full || e + 4 <= n) {
-        store_nt(reinterpret_cast<uint32_t*>(q8 + e), pack_i8x4(qq));
+        const uint32_t pk = pack_i8x4(qq);
+        if (!(a.dbg & 8) || pk == 0x7f7f7f7fu) store_nt(reinterpret_cast<uint32_t*>(q8 + e), pk);
       } else {
         q8[e] = (int8_t)q0;
         if (e + 1 < n) q8[e + 1] = (int8_t)q1;
@@ -160,6 +169,17 @@ __device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v) {
   while (ufirst((int)lds_ld(p)) < (int)v) __builtin_amdgcn_s_sleep(1);
   asm volatile("" ::: "memory");
 }
+
+// dbg & 4: per-wave phase cycle totals, accumulated locally and flushed once at exit.
+struct Prof {
+  uint64_t c[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  __device__ __forceinline__ void add(int ph, uint64_t cycles) { c[ph] += cycles; }
+  __device__ __forceinline__ void flush(const Args& a) {
+    if ((a.dbg & 4) && (threadIdx.x & 63) == 0)
+      for (int i = 0; i < 8; ++i)
+        if (c[i]) atomicAdd(&a.prof[i], (unsigned long long)c[i]);
+  }
+};
 
 // Sum of squares of one loader wave's rows of a chunk, in the loader's exact order.
 template <int ROWS, int LW>
@@ -237,20 +257,69 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
   constexpr int CH = ROWS * 1024;           // chunk elements
   static_assert(ROWS % 4 == 0 && ROWS % LW == 0 && S >= 2, "configuration");
   static_assert(GPT >= 1 && GPT * QW * 64 == (ROWS / 4) * 256, "quantiser threads must tile the groups");
+  constexpr int PR = 4;  // partial records (per chunk, decoupled from LDS slots)
+  constexpr int NTL = ROWS;   // quantisation tiles per chunk (4 rows x 64 float4 positions each)
+  constexpr int QC = QW - 1;  // claiming quantiser waves (quantiser wave 0 polls norms)
+  constexpr bool HELP = !DB;  // single-buffered loaders have the registers to help quantise
+  constexpr uint32_t PER_USE = NTL + QC + (HELP ? LW : 0);  // claim tickets per quantised use of a slot
   __shared__ float4 slots[S][ROWS * 256];
-  __shared__ double lpart[S][LW];
-  __shared__ float cpart[S], qnorm[S];
-  __shared__ uint32_t arrive[S], loaded[S], freed[S], qdone[S], qready[S];
+  __shared__ double lpart[PR][LW];
+  __shared__ float qnorm[S];
+  __shared__ uint32_t rarrive[PR], rgen[PR];
+  __shared__ uint32_t fill[S], loaded[S], freed[S], qready[S], tclaim[S], tfin[S];
   const int t = threadIdx.x, lane = t & 63;
   const int wave = ufirst(t >> 6);
   if (t < S) {
-    arrive[t] = 0; loaded[t] = 0; freed[t] = 0; qdone[t] = 0; qready[t] = 0;
+    fill[t] = 0; loaded[t] = 0; freed[t] = 0; qready[t] = 0; tclaim[t] = 0; tfin[t] = 0;
+  }
+  if (t < PR) {
+    rarrive[t] = 0;
+    rgen[t] = (uint32_t)t;  // record r first serves chunk r
   }
   __syncthreads();
   const int64_t G = gridDim.x, n_items = a.n_items;
+  const uint64_t t_start = __builtin_readcyclecounter();
+  Prof prof;
+
+  // Claim and quantise tiles of the chunk in slot s (its `use`-th quantised use, chunk k)
+  // until a claim fails.  Every claimer (the QW-1 quantiser waves, and each loader wave
+  // before it refills the slot) takes exactly one failing ticket per use.
+  auto claim_tiles = [&](int s, uint32_t use, int64_t k, const Item& it) {
+    const uint32_t base = PER_USE * use;
+    const bool full = it.end - it.begin == CH;
+    const int64_t coff = it.begin - it.tbegin;
+    float norm = 0.0f;
+    bool have_norm = false;
+    for (;;) {
+      const uint32_t c = (uint32_t)ufirst((int)(lane == 0 ? lds_add(&tclaim[s], 1u) : 0u)) - base;
+      if (c >= (uint32_t)NTL) break;
+      if (!have_norm) {  // a tile is held, so the slot cannot be recycled under us
+        const uint64_t c2 = __builtin_readcyclecounter();
+        lds_wait_ge(&qready[s], (uint32_t)(k + 1));
+        norm = ufirst(qnorm[s]);
+        have_norm = true;
+        prof.add(4, __builtin_readcyclecounter() - c2);
+      }
+      const uint64_t c3 = __builtin_readcyclecounter();
+      const int rg = (int)(c >> 2), j = 64 * (int)(c & 3) + lane;
+      if (!(a.dbg & 2)) {
+        float4 w4[4];
+#pragma unroll
+        for (int sl = 0; sl < 4; ++sl) w4[sl] = slots[s][(4 * rg + sl) * 256 + j];
+        quant_group_at<WIDTH, HAS_U>(a, w4, rg, j, it.begin, it.end, coff, it.tensor, norm, full);
+      }
+      lds_drain();
+      const uint32_t d = ufirst((int)(lane == 0 ? lds_add(&tfin[s], 1u) : 0u));
+      if (d == (uint32_t)NTL * (use + 1) - 1 && lane == 0) lds_st(&freed[s], (uint32_t)(k + 1));
+      prof.add(5, __builtin_readcyclecounter() - c3);
+    }
+  };
 
   if (wave < LW) {
     // ------------------------------------------------------------ loader
+    // A chunk's partial is published as soon as its data lands, before the loader waits
+    // for an LDS slot (and the prefetched chunk is published too before any such wait):
+    // a workgroup whose quantisers fall behind never delays another workgroup's norms.
     const int w = wave;
     auto issue = [&](float4 (&v)[VL], const Item& it) {
       const float* __restrict__ xb = a.x + it.begin;
@@ -279,41 +348,80 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
           }
       }
     };
-    auto step = [&](float4 (&v)[VL], Item& it, int64_t& idx, int64_t& k) {
-      const int s = (int)(k % S);
-      if (k >= S) lds_wait_ge(&freed[s], (uint32_t)(k - S + 1));
+    // Scale, reduce and publish chunk k (data in v).
+    auto publish = [&](float4 (&v)[VL], const Item& it, int64_t k) {
+      const uint64_t c1 = __builtin_readcyclecounter();
       float acc = 0.0f;
 #pragma unroll
       for (int q = 0; q < VL; ++q) {
         v[q] = scale4(v[q], a.alpha);
         acc = sumsq4(v[q], acc);
       }
+      const int r = (int)(k % PR);
+      if (it.flags & kPublish) {
+        const double wp = wave_sum_f64((double)acc);
+        lds_wait_ge(&rgen[r], (uint32_t)k);  // record free (chunk k-PR folded)
+        if (lane == 0) lpart[r][w] = wp;
+        lds_drain();
+        const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&rarrive[r], 1u) : 0u));
+        if (old == LW - 1) {  // last loader wave: fold in wave order, publish the granule
+          double fold = 0.0;
+#pragma unroll
+          for (int j = 0; j < LW; ++j) fold += lpart[r][j];
+          if (lane == 0) {
+            st_agent(&a.gran[it.gbase + it.chunk], ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint((float)fold));
+            lds_st(&rarrive[r], 0u);
+            lds_drain();
+            lds_st(&rgen[r], (uint32_t)(k + PR));
+          }
+        }
+      } else if (w == 0) {  // QUANT chunk: no partial, retire the record
+        lds_wait_ge(&rgen[r], (uint32_t)k);
+        if (lane == 0) lds_st(&rgen[r], (uint32_t)(k + PR));
+      }
+      prof.add(1, __builtin_readcyclecounter() - c1);
+    };
+    // Step on chunk k (already published): wait for its slot (publishing the in-flight
+    // chunk k+1 first if the slot is busy), fill the slot, issue the loads of k+2, then
+    // publish k+1 as soon as its data lands.  So a workgroup's published chunks run one
+    // step ahead of its slot turnover, and a blocked loader holds no unpublished chunk.
+    uint32_t uses[S];  // quantised uses of each slot so far (identical in every wave)
+#pragma unroll
+    for (int q = 0; q < S; ++q) uses[q] = 0;
+    auto step = [&](float4 (&v)[VL], Item& it, int64_t& idx, int64_t& k, float4 (&vo)[VL], const Item& ito,
+                    int64_t idxo, int64_t ko, bool& pubo) {
+      const int s = (int)(k % S);
+      const uint64_t c0 = __builtin_readcyclecounter();
+      if (k >= S) {
+        const Item prev = items[idx - (int64_t)S * G];  // the slot's current occupant, chunk k - S
+        if (HELP && (prev.flags & kQuant)) {  // (single-buffered: no other chunk is held)
+          uint32_t use = 0;
+#pragma unroll
+          for (int q = 0; q < S; ++q)
+            if (q == s) use = uses[q]++;
+          claim_tiles(s, use, k - S, prev);  // help quantise it (takes this wave's failing ticket)
+        }
+        if (ufirst((int)lds_ld(&freed[s])) < (int)(k - S + 1) && DB && idxo < n_items && !pubo) {
+          publish(vo, ito, ko);  // never hold an unpublished chunk while waiting
+          pubo = true;
+        }
+        lds_wait_ge(&freed[s], (uint32_t)(k - S + 1));
+      }
+      prof.add(0, __builtin_readcyclecounter() - c0);
       if (it.flags & kQuant) {
 #pragma unroll
         for (int r = 0; r < RPW; ++r)
 #pragma unroll
           for (int m = 0; m < 4; ++m) slots[s][(w * RPW + r) * 256 + lane + 64 * m] = v[4 * r + m];
-      }
-      const double wp = wave_sum_f64((double)acc);
-      if (lane == 0) lpart[s][w] = wp;
-      lds_drain();
-      const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&arrive[s], 1u) : 0u));
-      if (old == LW - 1) {  // last loader of this chunk
-        double fold = 0.0;
-#pragma unroll
-        for (int j = 0; j < LW; ++j) fold += lpart[s][j];
-        const float part = (float)fold;
-        if (lane == 0) {
-          if (it.flags & kPublish) {
-            const Tensor ti = tinfo[it.tensor];
-            st_agent(&a.gran[ti.gbase + it.chunk], ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(part));
-          }
-          cpart[s] = part;
-          lds_st(&arrive[s], 0u);
+        lds_drain();
+        const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&fill[s], 1u) : 0u));
+        if (old == LW - 1 && lane == 0) {
+          lds_st(&fill[s], 0u);
           lds_drain();
-          if (it.flags & kQuant) lds_st(&loaded[s], (uint32_t)(k + 1));
-          else lds_st(&freed[s], (uint32_t)(k + 1));  // NORM chunk: nothing to quantise
+          lds_st(&loaded[s], (uint32_t)(k + 1));
         }
+      } else if (w == 0 && lane == 0) {
+        lds_st(&freed[s], (uint32_t)(k + 1));  // NORM chunk: the slot stays free
       }
       idx += (DB ? 2 : 1) * G;
       k += DB ? 2 : 1;
@@ -321,92 +429,114 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
         it = items[idx];
         issue(v, it);
       }
+      if (DB && idxo < n_items && !pubo) {
+        publish(vo, ito, ko);
+        pubo = true;
+      }
     };
     if (DB) {
       int64_t ia = blockIdx.x, ib = ia + G, ka = 0, kb = 1;
+      bool pa = true, pb = false;  // chunk 0 is published in the prologue
       float4 va[VL], vb[VL];
       Item ita{}, itb{};
       if (ia < n_items) { ita = items[ia]; issue(va, ita); }
       if (ib < n_items) { itb = items[ib]; issue(vb, itb); }
+      if (ia < n_items) publish(va, ita, ka);
       for (;;) {
         if (ia >= n_items) break;
-        step(va, ita, ia, ka);
+        pa = false;  // the chunk step() loads into va next is unpublished
+        step(va, ita, ia, ka, vb, itb, ib, kb, pb);
         if (ib >= n_items) break;
-        step(vb, itb, ib, kb);
+        pb = false;
+        step(vb, itb, ib, kb, va, ita, ia, ka, pa);
       }
     } else {
       int64_t ia = blockIdx.x, ka = 0;
+      bool pn = true;
       float4 va[VL];
       Item ita{};
-      if (ia < n_items) { ita = items[ia]; issue(va, ita); }
-      while (ia < n_items) step(va, ita, ia, ka);
+      if (ia < n_items) { ita = items[ia]; issue(va, ita); publish(va, ita, ka); }
+      while (ia < n_items) {
+        step(va, ita, ia, ka, va, ita, n_items, ka, pn);
+        if (ia < n_items) publish(va, ita, ka);
+      }
     }
+    prof.add(6, __builtin_readcyclecounter() - t_start);
+    prof.flush(a);
     return;
   }
 
   // -------------------------------------------------------------- quantiser
+  // Wave LW is a dedicated POLLER: it resolves each chunk's norm (its only memory
+  // operations are granule polls, so a poll returns at load latency — a wave with payload
+  // stores in flight would wait for them first: vmcnt retires in order) and publishes it
+  // in the slot's norm record.  The other QW-1 waves CLAIM 64-group tiles of the chunk
+  // (ROWS tiles per chunk) from a per-slot counter: every claimer takes tickets until one
+  // fails, so each use of a slot advances the counter by exactly ROWS + QW - 1 and it
+  // never needs resetting.
   const int qw = wave - LW;
-  const int u = t - LW * 64;
-  int32_t cached_t = -1;
-  float cached_norm = 0.0f;
   int64_t k = 0;
-  for (int64_t idx = blockIdx.x; idx < n_items; idx += G, ++k) {
-    const Item it = items[idx];
-    if (!(it.flags & kQuant)) continue;
-    const int s = (int)(k % S);
-    lds_wait_ge(&loaded[s], (uint32_t)(k + 1));
-    const Tensor ti = tinfo[it.tensor];
-    float norm;
-    if (qw == 0) {
-      if ((it.flags & kPublish) && ti.nchunks == 1) {
-        norm = ufirst(sqrtf(cpart[s]));
-      } else if (it.tensor == cached_t) {
+  Item nx = blockIdx.x < n_items ? items[blockIdx.x] : Item{};
+  if (qw == 0) {
+    int32_t cached_t = -1;
+    float cached_norm = 0.0f;
+    for (int64_t idx = blockIdx.x; idx < n_items; idx += G, ++k) {
+      const Item it = nx;
+      if (idx + G < n_items) nx = items[idx + G];
+      if (!(it.flags & kQuant)) continue;
+      const int s = (int)(k % S);
+      const uint64_t c0 = __builtin_readcyclecounter();
+      float norm;
+      if (it.tensor == cached_t) {
         norm = cached_norm;
       } else if (a.dbg & 1) {
         norm = 1.0f;
       } else {
-        norm = wait_norm_wave<ROWS, LW>(a, ti, lane);
+        norm = wait_norm_wave<ROWS, LW>(a, tensor_of(it), lane);
         cached_t = it.tensor;
         cached_norm = norm;
       }
+      const uint64_t c1 = __builtin_readcyclecounter();
+      prof.add(3, c1 - c0);
+      lds_wait_ge(&loaded[s], (uint32_t)(k + 1));  // the slot's previous chunk is finished
+      prof.add(2, __builtin_readcyclecounter() - c1);
       if (lane == 0) {
         qnorm[s] = norm;
         lds_drain();
         lds_st(&qready[s], (uint32_t)(k + 1));
         if (it.chunk == 0) a.norm_out[it.tensor] = norm;
       }
-    } else {
-      lds_wait_ge(&qready[s], (uint32_t)(k + 1));
-      norm = ufirst(qnorm[s]);
     }
-    const bool full = it.end - it.begin == CH;
-    const int64_t coff = it.begin - ti.begin;
+  } else {
+    uint32_t uses[S];  // quantised uses of each slot so far (identical in every claimer)
 #pragma unroll
-    for (int h = 0; h < GPT; ++h) {
-      if (a.dbg & 2) break;
-      const int rg = (u >> 8) * GPT + h, j = u & 255;
-      float4 w4[4];
+    for (int q = 0; q < S; ++q) uses[q] = 0;
+    for (int64_t idx = blockIdx.x; idx < n_items; idx += G, ++k) {
+      const Item it = nx;
+      if (idx + G < n_items) nx = items[idx + G];  // prefetch: the scalar load overlaps this chunk
+      if (!(it.flags & kQuant)) continue;
+      const int s = (int)(k % S);
+      uint32_t use = 0;
 #pragma unroll
-      for (int sl = 0; sl < 4; ++sl) w4[sl] = slots[s][(4 * rg + sl) * 256 + j];
-      quant_group_at<WIDTH, HAS_U>(a, w4, rg, j, it.begin, it.end, coff, it.tensor, norm, full);
-    }
-    lds_drain();
-    const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&qdone[s], 1u) : 0u));
-    if (old == QW - 1 && lane == 0) {
-      lds_st(&qdone[s], 0u);
-      lds_drain();
-      lds_st(&freed[s], (uint32_t)(k + 1));
+      for (int q = 0; q < S; ++q)
+        if (q == s) use = uses[q]++;
+      const uint64_t c0 = __builtin_readcyclecounter();
+      lds_wait_ge(&loaded[s], (uint32_t)(k + 1));
+      lds_wait_ge(&tclaim[s], PER_USE * use);  // every claimer has left the slot's previous use
+      prof.add(2, __builtin_readcyclecounter() - c0);
+      claim_tiles(s, use, k, it);
     }
   }
+  prof.add(7, __builtin_readcyclecounter() - t_start);
+  prof.flush(a);
 }
 
 // Instantiated configurations: {rows of 1024 elements per chunk, LDS slots, loader
-// waves, loader double-buffering}.
+// waves, loader double-buffering}.  cfg 0 is the default (fastest measured).
 constexpr Config kConfigs[] = {
-    {12, 3, 4, 0},  // 48 KiB chunks x 3 slots, 4 loader + 12 quantiser waves
-    {12, 3, 4, 1},  // same, loaders prefetch two chunks
-    {16, 2, 8, 1},  // 64 KiB chunks x 2 slots, 8 + 8 waves
-    {8, 4, 8, 1},   // 32 KiB chunks x 4 slots, 8 + 8 waves
+    {16, 2, 8, 0},  // 64 KiB chunks x 2 slots, 8 loader + 1 poller + 7 claimer waves, loaders help
+    {16, 2, 8, 1},  // same with double-buffered loaders (no spare registers to help: they only load)
+    {8, 4, 8, 1},   // 32 KiB chunks x 4 slots
 };
 
 template <int ROWS, int S, int LW, bool DB>
@@ -421,10 +551,9 @@ const void* kernel_ptr(int width, bool has_u) {
 
 const void* kernel_for(int cfg, int width, bool has_u) {
   switch (cfg) {
-    case 1: return kernel_ptr<12, 3, 4, true>(width, has_u);
-    case 2: return kernel_ptr<16, 2, 8, true>(width, has_u);
-    case 3: return kernel_ptr<8, 4, 8, true>(width, has_u);
-    default: return kernel_ptr<12, 3, 4, false>(width, has_u);
+    case 1: return kernel_ptr<16, 2, 8, true>(width, has_u);
+    case 2: return kernel_ptr<8, 4, 8, true>(width, has_u);
+    default: return kernel_ptr<16, 2, 8, false>(width, has_u);
   }
 }
 

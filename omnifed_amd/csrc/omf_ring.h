@@ -15,9 +15,13 @@ namespace ring {
 //   kQuant             QUANT  second pass of such a tensor: re-read and quantise
 enum : int32_t { kPublish = 1, kQuant = 2 };
 
+// 64 bytes = one scalar load: the tensor's fields ride along so the hot loops never make
+// a second, dependent table read.
 struct Item {
-  int64_t begin, end;  // arena element range (one chunk of one tensor)
-  int32_t tensor, flags, chunk, pad;
+  int64_t begin, end;    // arena element range (one chunk of one tensor)
+  int64_t tbegin, tn;    // the tensor's range
+  int32_t tensor, flags, chunk, nchunks;
+  int32_t gbase, pad[3];  // the tensor's first granule
 };
 
 struct Tensor {
@@ -41,7 +45,8 @@ struct Args {
   uint32_t seed_lo, seed_hi, offset;
   uint32_t epoch;  // per-launch granule tag (never 0)
   uint64_t wait_ticks;
-  uint32_t dbg;  // experiment builds: 1 = no norm wait (norm := 1), 2 = no quantisation
+  uint32_t dbg;  // experiment switches: 1 = no norm wait (norm := 1), 2 = no quantisation, 4 = time phases
+  unsigned long long* prof;  // dbg & 4: per-phase cycle totals (omf_plan_ring_profile)
 };
 
 struct Config {

@@ -14,7 +14,7 @@ sys.path.insert(0, ".")
 from omnifed_amd import codec, shapes  # noqa: E402
 
 dev = torch.device("cuda", 0)
-cfgs = [int(c) for c in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0, 1, 2]
+cfgs = [int(c) for c in sys.argv[1].split(",")] if len(sys.argv) > 1 else [5]
 modes = [(0, -1), (1, -1)]
 
 

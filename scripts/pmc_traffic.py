@@ -27,7 +27,8 @@ def load(d, counter):
 
 
 def short(name):
-    for k in ("qsgd_encode_ordered", "qsgd_decode_flat", "qsgd_quant_flat", "topk_prep_hist", "topk_collect"):
+    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_decode_flat", "qsgd_quant_flat", "topk_prep_hist",
+              "topk_collect"):
         if k in name:
             return k
     return None
