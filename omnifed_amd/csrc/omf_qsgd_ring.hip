@@ -536,7 +536,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
 constexpr Config kConfigs[] = {
     {16, 2, 8, 0},  // 64 KiB chunks x 2 slots, 8 loader + 1 poller + 7 claimer waves, loaders help
     {16, 2, 8, 1},  // same with double-buffered loaders (no spare registers to help: they only load)
-    {8, 4, 8, 1},   // 32 KiB chunks x 4 slots
+    {8, 4, 8, 1},   // 32 KiB chunks x 4 slots (per-chunk synchronisation dominates: slower)
 };
 
 template <int ROWS, int S, int LW, bool DB>

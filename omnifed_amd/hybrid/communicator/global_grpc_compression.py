@@ -10,6 +10,10 @@ work happens, not what is produced:
 * ``encode_updates_dict`` encodes every QSGD tensor of the dict in ONE kernel
   launch (``omf_qsgd_encode`` over an update arena) and fetches the payload
   arena with one device-to-host copy;
+* ``decode_updates_dict`` decodes every QSGD layer of a message in ONE launch from
+  one pinned staging buffer (one host-to-device copy of the payloads), and
+  ``decode_updates_into`` (client downlink, global_grpc_client.py:98-111) writes the
+  decoded tensors straight into the model's device tensors;
 * decoders take an optional ``device=`` (default: the reference's placement —
   ``base_tensor.device`` when given, else CPU).
 """
@@ -36,6 +40,28 @@ GlobalHybridCompressor = Union[TopKCompression, QSGDQuantCompression]
 
 _QSGD_NUMPY_DTYPES = {8: np.int8, 32: np.int32}
 _QSGD_TORCH_DTYPES = {8: torch.int8, 32: torch.int32}
+
+
+class _PinnedStaging:
+    """Reusable page-locked host buffers (one per purpose), grown on demand.
+
+    Payload bytes cross PCIe once per message through these: a pageable tensor's
+    ``.cpu()`` / ``.to(dev)`` would stage through a driver bounce buffer instead.
+    Callers copy out of a buffer before it is reused (protobuf ``bytes`` are copies).
+    """
+
+    def __init__(self):
+        self._bufs: Dict[str, torch.Tensor] = {}
+
+    def get(self, key: str, nbytes: int) -> torch.Tensor:
+        b = self._bufs.get(key)
+        if b is None or b.numel() < nbytes:
+            b = torch.empty(max(int(nbytes), 4096), dtype=torch.uint8, pin_memory=True)
+            self._bufs[key] = b
+        return b[:nbytes]
+
+
+_STAGING = _PinnedStaging()
 
 
 def compression_mode_name(compressor: Optional[GlobalHybridCompressor]) -> str:
@@ -272,8 +298,10 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
         plan, q, norms = encode_many(flats, compressor.s, dev, compressor.rng, compressor._next_call())
         levels = 2**compressor.s
         width, _ = choose_qsgd_storage_width(levels)
-        q_host = q.cpu().numpy()
-        host_norms = norms.cpu().tolist()
+        staged = _STAGING.get("encode", q.numel() * q.element_size()).view(q.dtype)
+        staged.copy_(q, non_blocking=True)  # one D2H of the payload arena (w bytes per element)
+        host_norms = norms.cpu().tolist()  # synchronises the stream: the payload copy has landed
+        q_host = staged.numpy()
         for i, o, n, nv in zip(comp_idx, plan.offsets, plan.sizes, host_norms):
             if nv != 0:
                 results[i] = (q_host[o:o + n].tobytes(), nv)
@@ -290,14 +318,110 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
     return layers
 
 
+def _decode_qsgd_batch(layers, dev: torch.device):
+    """Decode QSGD layers that share (width, level) in ONE launch.
+
+    The payloads are packed into one pinned buffer in a plan's arena layout, copied to
+    the GPU once, and decoded by one ``omf_qsgd_decode``; returns the decoded fp32 arena
+    and the plan (layer i at ``[plan.offsets[i], + plan.sizes[i])``).
+    """
+    width, level = layers[0].width, layers[0].level
+    np_dt = _QSGD_NUMPY_DTYPES[width]
+    sizes = [max(int(np.prod(tuple(L.original_shape))), 1) for L in layers]
+    plan = codec.Plan.get(sizes, device=dev)
+    itemsize = np.dtype(np_dt).itemsize
+    host = _STAGING.get("decode", plan.arena_end * itemsize).numpy().view(np_dt)
+    norms = np.zeros(plan.nt, dtype=np.float32)
+    for i, (L, o) in enumerate(zip(layers, plan.offsets)):
+        q = np.frombuffer(L.values_data, dtype=np_dt)
+        host[o:o + q.size] = q
+        norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
+    qd = torch.empty(plan.arena_end, dtype=_QSGD_TORCH_DTYPES[width], device=dev)
+    qd.copy_(torch.from_numpy(host), non_blocking=True)  # one H2D of every payload
+    nd = torch.from_numpy(norms).to(dev, non_blocking=False)
+    y = plan.qsgd_decode(qd, width, level, nd)
+    # the staging buffer is reused by the next call: make sure this copy has been consumed
+    torch.cuda.current_stream(dev).synchronize()
+    return y, plan
+
+
+def _validate_layer(layer):
+    """The checks decode_layer_tensor makes before any work (global_grpc_compression.py:
+    145-146, 164-171, 193-194, 204), so a batched decode raises for the same first layer."""
+    ct = layer.compression_type or ""
+    if ct == "":
+        if not layer.param_shape:
+            raise ValueError(f"Dense layer {layer.layer_name!r} missing param_shape")
+    elif ct == TOPK_COMPRESSION_NAME:
+        if not layer.values_data or not layer.indices_data:
+            raise ValueError(f"Compressed layer {layer.layer_name!r} missing values/indices")
+    elif ct == QSGD_COMPRESSION_NAME:
+        _check_qsgd_layer(layer)
+    else:
+        raise ValueError(f"Unsupported compression_type={ct!r}")
+
+
+def _qsgd_groups(proto_layers):
+    """Validate every layer in message order; QSGD layers grouped by (width, level)."""
+    groups: Dict[tuple, list] = {}
+    for L in proto_layers:
+        _validate_layer(L)
+        if L.compression_type == QSGD_COMPRESSION_NAME:
+            groups.setdefault((L.width, L.level), []).append(L)
+    return groups
+
+
 def decode_updates_dict(proto_layers, *, base_updates: Optional[Dict[str, torch.Tensor]] = None,
                         device=None) -> Dict[str, torch.Tensor]:
-    """global_grpc_compression.py:214-223."""
+    """global_grpc_compression.py:214-223; every QSGD layer of a (width, level) in one launch.
+
+    Placement as the reference: CPU tensors unless ``device`` is given (QSGD ignores
+    ``base_tensor``, :198-202); with ``device="cuda"`` nothing but the payload crosses PCIe.
+    """
+    proto_layers = list(proto_layers)
+    out_dev = _out_device(None, device)
+    decoded: Dict[str, torch.Tensor] = {}
+    groups = _qsgd_groups(proto_layers)
+    if groups:
+        dev = _gpu_for(out_dev)
+        for layers in groups.values():
+            y, plan = _decode_qsgd_batch(layers, dev)
+            if out_dev.type == "cpu":
+                y = y.cpu()  # one D2H for the whole group; returned tensors are views of it
+            for L, o, n in zip(layers, plan.offsets, plan.sizes):
+                decoded[L.layer_name] = y[o:o + n].view(tuple(L.original_shape))
     out: Dict[str, torch.Tensor] = {}
     for layer in proto_layers:
+        if layer.layer_name in decoded and layer.compression_type == QSGD_COMPRESSION_NAME:
+            out[layer.layer_name] = decoded[layer.layer_name]
+            continue
         base = None if base_updates is None else base_updates.get(layer.layer_name)
         out[layer.layer_name] = decode_layer_tensor(layer, base_tensor=base, device=device)
     return out
+
+
+def decode_updates_into(proto_layers, targets: Dict[str, torch.Tensor]) -> None:
+    """Client downlink (global_grpc_client.py:98-111): decode each layer into ``targets[name]``.
+
+    Equivalent to ``target.copy_(decode_layer_tensor(layer, base_tensor=target).to(...))``
+    for every layer whose name is in ``targets``: QSGD layers are decoded in one launch per
+    (width, level) and copied device-to-device; Top-K layers are scattered onto the target
+    in place (the reference's overlay-on-a-copy); dense layers are copied.
+    """
+    proto_layers = [L for L in proto_layers if L.layer_name in targets]
+    groups = _qsgd_groups(proto_layers)
+    for layers in groups.values():
+        dev = _gpu_for(targets[layers[0].layer_name].device)
+        y, plan = _decode_qsgd_batch(layers, dev)
+        for L, o, n in zip(layers, plan.offsets, plan.sizes):
+            t = targets[L.layer_name]
+            t.copy_(y[o:o + n].view(tuple(L.original_shape)).to(t.dtype))
+    for L in proto_layers:
+        if L.compression_type == QSGD_COMPRESSION_NAME:
+            continue
+        t = targets[L.layer_name]
+        dec = decode_layer_tensor(L, base_tensor=t, device=t.device)
+        t.copy_(dec.to(t.dtype))
 
 
 __all__: List[str] = [
@@ -306,6 +430,7 @@ __all__: List[str] = [
     "compression_mode_name",
     "decode_layer_tensor",
     "decode_updates_dict",
+    "decode_updates_into",
     "encode_layer_state",
     "encode_updates_dict",
     "hybrid_global_compressor_from_cfg",

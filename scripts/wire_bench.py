@@ -1,0 +1,52 @@
+"""Host-inclusive wire path timing: the drop-in's user-visible API on Llama-400M.
+
+encode_updates_dict : device gradients -> one encode launch -> one pinned D2H of the
+                      int8 payload arena -> 183 LayerState messages (bytes copies)
+decode_updates_dict : LayerStates -> pinned staging -> one H2D -> one decode launch
+                      (device="cuda": stays on the GPU; default: CPU tensors, as the reference)
+decode_updates_into : client downlink straight into the model's device tensors
+"""
+import json
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from omnifed_amd import shapes  # noqa: E402
+from omnifed_amd.hybrid.communicator.global_grpc_compression import (  # noqa: E402
+    build_global_compressor, decode_updates_dict, decode_updates_into, encode_updates_dict)
+
+dev = torch.device("cuda", 0)
+cfg = sys.argv[1] if len(sys.argv) > 1 else "llama400m"
+named = shapes.model_shapes(cfg)
+g = torch.Generator(device=dev).manual_seed(0)
+upd = {n: torch.randn(s, device=dev, generator=g) * 1e-3 for n, s in named}
+N = sum(t.numel() for t in upd.values())
+comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev)
+targets = {n: torch.empty_like(t) for n, t in upd.items()}
+
+
+def tm(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return sorted(ts)[len(ts) // 2]
+
+
+layers = encode_updates_dict(upd, comp)
+res = {"config": cfg, "elements": N, "tensors": len(named),
+       "encode_updates_dict_ms": tm(lambda: encode_updates_dict(upd, comp)) * 1e3,
+       "decode_updates_dict_gpu_ms": tm(lambda: decode_updates_dict(layers, device=dev)) * 1e3,
+       "decode_updates_into_ms": tm(lambda: decode_updates_into(layers, targets)) * 1e3,
+       "decode_updates_dict_cpu_ms": tm(lambda: decode_updates_dict(layers)) * 1e3}
+for k in ("encode_updates_dict_ms", "decode_updates_dict_gpu_ms", "decode_updates_into_ms",
+          "decode_updates_dict_cpu_ms"):
+    res[k.replace("_ms", "_fp32_GBs")] = round(4 * N / (res[k] * 1e-3) / 1e9, 2)
+    res[k] = round(res[k], 2)
+print(json.dumps(res), flush=True)
