@@ -123,6 +123,17 @@ int omf_qsgd_encode(omf_plan* plan, const float* x, float alpha, int32_t bit_wid
 int omf_qsgd_norms(omf_plan* plan, const float* x, float alpha, float* norm_out, void* stream);
 
 /*
+ * Fused PS step: avg_out = acc / divisor (IEEE fp32 division, as the reference's
+ * `acc / total_samples` in CentralServerServicer._apply_model_updates,
+ * src/omnifed/hybrid/communicator/global_grpc_server.py:155-171) and the QSGD encode of avg
+ * for the downlink (_send_current_model, :213-234 -> encode_layer_state) in ONE launch
+ * with the ring encoder (acc read once); other strategies run divide + encode.
+ * Arguments after avg_out as omf_qsgd_encode (no alpha, no norm_in).  avg_out may equal acc.
+ */
+int omf_ps_apply_encode(omf_plan* plan, const float* acc, float divisor, float* avg_out, int32_t bit_width,
+                        const float* u, uint64_t seed, uint64_t offset, void* q_out, float* norm_out, void* stream);
+
+/*
  * QSGD decode, all tensors in one launch.
  * Replaces QSGDQuantCompression.decompress_quantized (qsgd.py:84-96) as called by
  * _decode_qsgd_layer (global_grpc_compression.py:163-182), and — with

@@ -45,6 +45,8 @@ SIGNATURES = {
     "omf_plan_ring_profile": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64)]),
     "omf_qsgd_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p, _c_p, _c_p]),
     "omf_qsgd_norms": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_p]),
+    "omf_ps_apply_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p,
+                                           _c_p]),
     "omf_qsgd_decode": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
     "omf_div_f32": (ctypes.c_int, [_c_p, _c_i64, _c_f32, _c_p]),
     "omf_topk_k": (_c_i64, [_c_i64, _c_f64]),

@@ -208,6 +208,42 @@ class Plan:
                   "omf_qsgd_encode")
         return q_out, norm_out
 
+    def ps_apply_encode(self, acc: torch.Tensor, divisor: float, bit_width: int,
+                        avg_out: Optional[torch.Tensor] = None, u: Optional[torch.Tensor] = None, seed: int = 0,
+                        offset: int = 0, q_out: Optional[torch.Tensor] = None,
+                        norm_out: Optional[torch.Tensor] = None, stream: Optional[int] = None):
+        """Fused PS step (omf_ps_apply_encode): ``avg = acc / divisor`` and its QSGD payload.
+
+        Returns ``(avg, q, norms)``; ``avg_out`` may be ``acc`` itself (in place).
+        """
+        s = int(bit_width)
+        if not 0 <= s <= 30:
+            raise ValueError("bit_width must be in [0, 30]")
+        if not float(divisor) != 0.0:
+            raise ValueError("divisor must be non-zero")
+        width = storage_width(2 ** s)
+        qdt = torch.int8 if width == 8 else torch.int32
+        dev = self.device
+        _need(acc, "acc", torch.float32, dev, self.arena_end, 16)
+        if avg_out is None:
+            avg_out = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
+        _need(avg_out, "avg_out", torch.float32, dev, self.arena_end, 16)
+        if q_out is None:
+            q_out = torch.empty(self.arena_end, dtype=qdt, device=dev)
+        _need(q_out, "q_out", qdt, dev, self.arena_end, 4 if width == 8 else 16)
+        if norm_out is None:
+            norm_out = torch.empty(self.nt, dtype=torch.float32, device=dev)
+        _need(norm_out, "norm_out", torch.float32, dev, self.nt, 4)
+        if u is not None:
+            _need(u, "u", torch.float32, dev, self.arena_end, 16)
+        st = stream if stream is not None else _stream(dev)
+        with self._lock:
+            check(lib().omf_ps_apply_encode(self._h, _ptr(acc), float(divisor), _ptr(avg_out), s, _ptr(u),
+                                            int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset) & 0xFFFFFFFFFFFFFFFF,
+                                            _ptr(q_out), _ptr(norm_out), ctypes.c_void_p(st)),
+                  "omf_ps_apply_encode")
+        return avg_out, q_out, norm_out
+
     def qsgd_norms(self, x: torch.Tensor, alpha: float = 1.0, norm_out: Optional[torch.Tensor] = None,
                    stream: Optional[int] = None) -> torch.Tensor:
         dev = self.device

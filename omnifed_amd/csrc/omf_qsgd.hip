@@ -856,7 +856,8 @@ static int check_bits(int32_t s) {
 }
 
 static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, const float* u, uint64_t seed,
-                       uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream) {
+                       uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream,
+                       float divisor = 0.0f, float* xout = nullptr) {
   if (!p) return fail(OMF_EINVAL, "plan is NULL");
   if (int r = check_bits(s)) return r;
   const int width = (1 << s) <= 127 ? 1 : 4;
@@ -899,6 +900,9 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
     r.err = reinterpret_cast<uint32_t*>(p->d_sync + 4);
     r.n_items = p->n_ring;
     r.alpha = alpha;
+    r.divisor = divisor;
+    r.divide = divisor != 0.0f ? 1u : 0u;
+    r.xout = xout;
     r.levels = (float)(1u << s);
     r.seed_lo = (uint32_t)seed; r.seed_hi = (uint32_t)(seed >> 32); r.offset = (uint32_t)offset;
     if (++p->ring_epoch == 0) ++p->ring_epoch;
@@ -943,6 +947,24 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
 int omf_qsgd_encode(omf_plan* plan, const float* x, float alpha, int32_t bit_width, const float* u, uint64_t seed,
                     uint64_t offset, const float* norm_in, void* q_out, float* norm_out, void* stream) {
   return encode_impl(plan, x, alpha, bit_width, u, seed, offset, norm_in, q_out, norm_out, false, stream);
+}
+
+int omf_ps_apply_encode(omf_plan* p, const float* acc, float divisor, float* avg_out, int32_t bit_width,
+                        const float* u, uint64_t seed, uint64_t offset, void* q_out, float* norm_out, void* stream) {
+  if (!p) return fail(OMF_EINVAL, "plan is NULL");
+  if (!acc || !avg_out) return fail(OMF_EINVAL, "omf_ps_apply_encode: acc and avg_out must be non-NULL");
+  if (!(divisor != 0.0f)) return fail(OMF_EINVAL, "omf_ps_apply_encode: divisor must be non-zero");
+  if (!aligned(avg_out, 16)) return fail(OMF_EINVAL, "omf_ps_apply_encode: avg_out must be 16-byte aligned");
+  if (p->strategy == 2)  // one launch: read acc once, write avg and the payload
+    return encode_impl(p, acc, 1.0f, bit_width, u, seed, offset, nullptr, q_out, norm_out, false, stream, divisor,
+                       avg_out);
+  // other strategies: the same results in two passes
+  DeviceGuard g(p->device);
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  if (avg_out != acc)
+    OMF_HIP(hipMemcpyAsync(avg_out, acc, 4 * (size_t)p->arena_end, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  if (int r = omf_div_f32(avg_out, p->arena_end, divisor, stream)) return r;
+  return encode_impl(p, avg_out, 1.0f, bit_width, u, seed, offset, nullptr, q_out, norm_out, false, stream);
 }
 
 int omf_qsgd_norms(omf_plan* plan, const float* x, float alpha, float* norm_out, void* stream) {

@@ -53,6 +53,13 @@ __device__ __forceinline__ float4 scale4(float4 v, float alpha) {
   return make_float4(__fmul_rn(v.x, alpha), __fmul_rn(v.y, alpha), __fmul_rn(v.z, alpha), __fmul_rn(v.w, alpha));
 }
 
+// The encoder's input transform: the client weighting x * alpha (global_grpc.py:101-123),
+// or the PS average x / total_samples (global_grpc_server.py:155-171), bit-exact.
+__device__ __forceinline__ float4 prologue4(const Args& a, float4 v) {
+  if (a.divide) return Divisor(a.divisor).div4(v);
+  return scale4(v, a.alpha);
+}
+
 __device__ __forceinline__ float sumsq4(float4 v, float acc) {
   acc = fmaf(v.x, v.x, acc);
   acc = fmaf(v.y, v.y, acc);
@@ -198,7 +205,7 @@ __device__ __forceinline__ float loader_sumsq(const Args& a, int64_t cb, int n, 
         if (i + 1 < n) v.y = xb[i + 1];
         if (i + 2 < n) v.z = xb[i + 2];
       }
-      acc = sumsq4(scale4(v, a.alpha), acc);
+      acc = sumsq4(prologue4(a, v), acc);
     }
   return acc;
 }
@@ -354,8 +361,26 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
       float acc = 0.0f;
 #pragma unroll
       for (int q = 0; q < VL; ++q) {
-        v[q] = scale4(v[q], a.alpha);
+        v[q] = prologue4(a, v[q]);
         acc = sumsq4(v[q], acc);
+      }
+      if (a.xout && (it.flags & kPublish)) {  // PS fusion: write the averaged parameters once
+        float* __restrict__ ob = a.xout + it.begin;
+        const int n = (int)(it.end - it.begin);
+#pragma unroll
+        for (int r2 = 0; r2 < RPW; ++r2)
+#pragma unroll
+          for (int m = 0; m < 4; ++m) {
+            const int i = (w * RPW + r2) * 1024 + 4 * (lane + 64 * m);
+            const float4 o = v[4 * r2 + m];
+            if (n == CH || i + 4 <= n) {
+              store_nt(ob + i, o);
+            } else {
+              if (i < n) ob[i] = o.x;
+              if (i + 1 < n) ob[i + 1] = o.y;
+              if (i + 2 < n) ob[i + 2] = o.z;
+            }
+          }
       }
       const int r = (int)(k % PR);
       if (it.flags & kPublish) {

@@ -42,6 +42,11 @@ struct Args {
   int64_t n_items;
   float alpha;
   float levels;
+  // PS fusion (omf_ps_apply_encode): divide != 0 -> the encoder's input is x / divisor
+  // (IEEE, correctly rounded) instead of x * alpha, and xout (if set) receives it.
+  float divisor;
+  uint32_t divide;
+  float* xout;
   uint32_t seed_lo, seed_hi, offset;
   uint32_t epoch;  // per-launch granule tag (never 0)
   uint64_t wait_ticks;

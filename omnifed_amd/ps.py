@@ -111,6 +111,39 @@ class DeviceAggregator:
         self.update_count += 1
         self.total_samples += int(number_samples)
 
+    def apply_and_encode(self, compressor, total_samples: Optional[int] = None):
+        """Fused ``_apply_model_updates`` + the first downlink ``_send_current_model``
+        (global_grpc_server.py:155-171, 213-234): one launch divides the accumulator by the
+        sample count (in place: it becomes the averaged model, as ``param.data = avg``) and
+        QSGD-encodes the average.  Returns ``(avg views by name, LayerState list)``; later
+        requests re-encode the average independently, as the reference does per request.
+        """
+        from .hybrid.compression.qsgd import QSGDQuantCompression, choose_qsgd_storage_width
+        from .hybrid.communicator.global_grpc_compression import qsgd_layer_from_payload, _encode_dense_layer
+
+        if not isinstance(compressor, QSGDQuantCompression) or not self.compute_mean:
+            avg = self.apply(total_samples)
+            from .hybrid.communicator.global_grpc_compression import encode_updates_dict
+            return avg, encode_updates_dict(avg, compressor)
+        total = self.total_samples if total_samples is None else int(total_samples)
+        s = compressor.s
+        seed = int(torch.randint(0, 2**62, (1,)).item())
+        _, q, norms = self.plan.ps_apply_encode(self.acc, float(total), s, avg_out=self.acc, seed=seed,
+                                                offset=compressor._next_call())
+        levels = 2**s
+        width, _ = choose_qsgd_storage_width(levels)
+        qh = q.cpu().numpy()
+        nh = norms.cpu().tolist()
+        avg = {n: self._slice(n).view(self.shapes[n]) for n in self.names}
+        layers = []
+        for i, n in enumerate(self.names):
+            o, k = self.plan.offsets[i], self.plan.sizes[i]
+            if nh[i] != 0 and int(np.prod(self.shapes[n])) > 0:
+                layers.append(qsgd_layer_from_payload(n, self.shapes[n], qh[o:o + k].tobytes(), nh[i], width, levels))
+            else:
+                layers.append(_encode_dense_layer(n, avg[n]))
+        return avg, layers
+
     def apply(self, total_samples: Optional[int] = None) -> Dict[str, torch.Tensor]:
         """_apply_model_updates (global_grpc_server.py:155-171): acc / total_samples per tensor."""
         total = self.total_samples if total_samples is None else int(total_samples)

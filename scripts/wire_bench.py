@@ -45,6 +45,27 @@ res = {"config": cfg, "elements": N, "tensors": len(named),
        "decode_updates_dict_gpu_ms": tm(lambda: decode_updates_dict(layers, device=dev)) * 1e3,
        "decode_updates_into_ms": tm(lambda: decode_updates_into(layers, targets)) * 1e3,
        "decode_updates_dict_cpu_ms": tm(lambda: decode_updates_dict(layers)) * 1e3}
+# fused PS step (omf_ps_apply_encode) vs divide + encode, device-resident
+from omnifed_amd import codec  # noqa: E402
+
+plan = codec.Plan.get([t.numel() for t in upd.values()], device=dev)
+acc = torch.randn(plan.arena_end, device=dev, generator=g)
+avg = torch.empty_like(acc)
+q = torch.empty(plan.arena_end, dtype=torch.int8, device=dev)
+nr = torch.empty(plan.nt, device=dev)
+
+
+def separate():
+    avg.copy_(acc)
+    codec.div_(avg, 40.0)
+    plan.qsgd_encode(avg, 4, q_out=q, norm_out=nr, seed=1)
+
+
+res["ps_fused_apply_encode_ms"] = tm(lambda: plan.ps_apply_encode(acc, 40.0, 4, avg_out=avg, q_out=q, norm_out=nr,
+                                                                   seed=1), reps=10) * 1e3
+res["ps_divide_then_encode_ms"] = tm(separate, reps=10) * 1e3
+res["ps_fused_apply_encode_ms"] = round(res["ps_fused_apply_encode_ms"], 4)
+res["ps_divide_then_encode_ms"] = round(res["ps_divide_then_encode_ms"], 4)
 for k in ("encode_updates_dict_ms", "decode_updates_dict_gpu_ms", "decode_updates_into_ms",
           "decode_updates_dict_cpu_ms"):
     res[k.replace("_ms", "_fp32_GBs")] = round(4 * N / (res[k] * 1e-3) / 1e9, 2)

@@ -91,3 +91,56 @@ def test_batched_decode_errors_in_message_order(gpu):
     odd = pb.LayerState(layer_name="x", compression_type="Nope")
     with pytest.raises(ValueError, match="Unsupported compression_type"):
         decode_updates_dict([odd])
+
+
+@pytest.mark.parametrize("strategy", ["ring", "ordered"])
+def test_fused_ps_apply_encode(gpu, strategy):
+    """avg = acc / total (numpy fp32 division, bit for bit) and its payload = encode(avg) with the
+    same draws — in one launch (ring) or divide + encode (other strategies)."""
+    from omnifed_amd import codec
+
+    sizes = [5, 16384, 70001, 1 << 20, 3000]
+    plan = codec.Plan(sizes, device=gpu)
+    plan.set_encode_strategy(strategy)
+    g = torch.Generator(device=gpu).manual_seed(9)
+    acc = torch.randn(plan.arena_end, device=gpu, generator=g) * 3.0
+    total = 7
+    avg, q, norms = plan.ps_apply_encode(acc, float(total), 4, seed=21, offset=4)
+    assert plan.check()
+    want = acc.cpu().numpy() / np.float32(total)
+    got = avg.cpu().numpy()
+    for o, n in zip(plan.offsets, plan.sizes):
+        assert got[o:o + n].tobytes() == want[o:o + n].tobytes()
+    q2, n2 = plan.qsgd_encode(torch.from_numpy(want).to(gpu), 4, seed=21, offset=4)
+    assert torch.equal(norms, n2)
+    for o, n in zip(plan.offsets, plan.sizes):
+        assert torch.equal(q[o:o + n], q2[o:o + n])
+    # in place (the PS's accumulator becomes the averaged model)
+    acc2 = acc.clone()
+    plan.ps_apply_encode(acc2, float(total), 4, avg_out=acc2, seed=21, offset=4)
+    for o, n in zip(plan.offsets, plan.sizes):
+        assert torch.equal(acc2[o:o + n], avg[o:o + n])
+
+
+def test_device_aggregator_apply_and_encode(gpu):
+    from omnifed_amd.ps import DeviceAggregator
+
+    named = [("a", (33, 7)), ("b", (1000,)), ("c", (4, 4, 4))]
+    agg = DeviceAggregator(named, device=gpu)
+    comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=8, device=gpu)
+    for seed, ns in ((1, 10), (2, 30)):
+        g = torch.Generator().manual_seed(seed)
+        u = {n: torch.randn(s, generator=g) for n, s in named}
+        agg.accumulate_layers(encode_updates_dict(u, comp), number_samples=ns)
+    acc_before = agg.acc.clone()  # the PS sum of decoded updates, in arrival order
+    avg, layers = agg.apply_and_encode(comp)
+    assert agg.total_samples == 40
+    want = acc_before.cpu().numpy() / np.float32(40)
+    for (n, s), L in zip(named, layers):
+        i = agg.index[n]
+        o, k = agg.plan.offsets[i], agg.plan.sizes[i]
+        assert avg[n].cpu().numpy().reshape(-1).tobytes() == want[o:o + k].tobytes()
+        assert L.layer_name == n and L.compression_type == "QSGDQuantCompression"
+        dec = decode_layer_tensor(L)
+        norm = float(np.frombuffer(L.meta_tensor, np.float32)[0])
+        assert float((dec - avg[n].cpu()).abs().max()) <= norm / L.level * (1 + 1e-6)
