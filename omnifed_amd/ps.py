@@ -121,7 +121,8 @@ class DeviceAggregator:
         from .hybrid.compression.qsgd import QSGDQuantCompression, choose_qsgd_storage_width
         from .hybrid.communicator.global_grpc_compression import qsgd_layer_from_payload, _encode_dense_layer
 
-        if not isinstance(compressor, QSGDQuantCompression) or not self.compute_mean:
+        if (not isinstance(compressor, QSGDQuantCompression) or not self.compute_mean
+                or compressor.rng != "philox"):  # parity mode draws MT19937 uniforms on the host
             avg = self.apply(total_samples)
             from .hybrid.communicator.global_grpc_compression import encode_updates_dict
             return avg, encode_updates_dict(avg, compressor)

@@ -14,7 +14,7 @@ x = torch.randn(p.arena_end, device=dev) * 1e-3
 q = torch.empty(p.arena_end, dtype=torch.int8, device=dev)
 nr = torch.empty(p.nt, device=dev)
 p.set_encode_strategy("ring")
-for cfg in (5,):
+for cfg in (0,):
     for bm in (1,):
         p.set_ring(cfg=cfg, big_mode=bm)
         for _ in range(2):
@@ -32,7 +32,7 @@ for cfg in (5,):
 if int(os.environ.get("OMF_RING_DBG", "0")) & 4:
     names = ["L wait free slot", "L load+reduce", "Q wait loaded", "poller resolve", "Q wait norm", "Q tiles",
              "L total", "Q total"]
-    for cfg in (5,):
+    for cfg in (0,):
         p.set_ring(cfg=cfg, big_mode=1)
         p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1)
         p.ring_profile()
