@@ -25,7 +25,7 @@ SOURCES = ["omf_runtime.cpp", "omf_qsgd.hip", "omf_qsgd_ring.hip", "omf_topk.hip
 FLAGS = [
     "--offload-arch=gfx950",
     "-O3",
-    "-std=c++17",
+    "-std=c++20",
     "-fPIC",
     "-ffp-contract=off",
     "-fno-gpu-flush-denormals-to-zero",

@@ -556,11 +556,82 @@ static void build_sequence(const omf_plan& p, bool resident_ok, std::vector<Item
 // larger ones are NORM chunks (partial only) plus QUANT chunks (second read), the QUANT
 // chunks placed ring_gap items later (big_mode 0) or at the very end with every NORM
 // chunk first (big_mode 1).  Items are dealt to workgroups round-robin.
+// Register-resident encoder (omf_qsgd_ring.hip qsgd_encode_rr): every single-read tensor
+// lies inside one row of `grid` consecutive items, so all its chunks are at the same
+// position of their workgroups.  Rows are packed first-fit decreasing; gaps are filled
+// with NORM items of the multi-row ("big") tensors, or with empty items when none are
+// left.  Layout: [whole rows of big NORM items][packed rows][remaining big NORM items]
+// [big QUANT items] — every NORM item precedes its tensor's QUANT items.
+static void build_rr_sequence(omf_plan& p, int64_t ch, std::vector<omf::ring::Item>& seq,
+                              std::vector<omf::ring::Tensor>& tens) {
+  namespace R = omf::ring;
+  const int64_t G = std::max<int32_t>(p.ring_grid, 1);
+  p.ring_hold_max = p.ring_hold_override > 0 ? std::min<int64_t>(G, p.ring_hold_override) : G;
+  seq.clear();
+  tens.assign(p.nt, R::Tensor{});
+  std::vector<R::Item> norm_items, quant_items;
+  std::vector<std::pair<int64_t, int32_t>> regular;  // (chunks, tensor)
+  int64_t gb = 0;
+  p.ring_two_pass = 0;
+  auto item = [&](int32_t t, int64_t k, int32_t flags) {
+    const int64_t n = p.sizes[t], b = p.offsets[t], cb = b + k * ch;
+    return R::Item{cb, std::min(b + n, cb + ch), b, n, t, flags, (int32_t)k, tens[t].nchunks, tens[t].gbase, {0, 0, 0}};
+  };
+  for (int32_t t = 0; t < p.nt; ++t) {
+    const int64_t nc = (p.sizes[t] + ch - 1) / ch;
+    tens[t] = R::Tensor{p.offsets[t], p.sizes[t], (int32_t)nc, (int32_t)gb, {0, 0}};
+    gb += nc;
+    if (nc <= p.ring_hold_max) {
+      regular.emplace_back(nc, t);
+    } else {
+      ++p.ring_two_pass;
+      for (int64_t k = 0; k < nc; ++k) norm_items.push_back(item(t, k, R::kPublish));
+      for (int64_t k = 0; k < nc; ++k) quant_items.push_back(item(t, k, R::kQuant));
+    }
+  }
+  std::stable_sort(regular.begin(), regular.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+  std::vector<std::vector<int32_t>> rows;
+  std::vector<int64_t> room;
+  for (const auto& r : regular) {
+    size_t i = 0;
+    while (i < rows.size() && room[i] < r.first) ++i;
+    if (i == rows.size()) {
+      rows.emplace_back();
+      room.push_back(G);
+    }
+    rows[i].push_back(r.second);
+    room[i] -= r.first;
+  }
+  // Gap fillers come from the back of the NORM list; whole rows of the rest lead.
+  size_t nfill = 0;
+  for (size_t i = 0; i + 1 < rows.size(); ++i) nfill += (size_t)room[i];
+  nfill = std::min(nfill, norm_items.size());
+  const size_t avail = norm_items.size() - nfill;
+  const size_t lead = avail / (size_t)G * (size_t)G;
+  seq.insert(seq.end(), norm_items.begin(), norm_items.begin() + (ptrdiff_t)lead);
+  size_t tail = lead;                           // next NORM item not yet placed (after the lead rows)
+  size_t fill = norm_items.size() - nfill;      // next gap filler
+  for (size_t i = 0; i < rows.size(); ++i) {
+    for (int32_t t : rows[i])
+      for (int64_t k = 0; k < tens[t].nchunks; ++k) seq.push_back(item(t, k, R::kPublish | R::kQuant));
+    if (i + 1 < rows.size()) {
+      for (int64_t g = 0; g < room[i]; ++g) {
+        if (fill < norm_items.size()) seq.push_back(norm_items[fill++]);
+        else seq.push_back(R::Item{0, 0, 0, 0, 0, 0, 0, 0, 0, {0, 0, 0}});  // empty: keeps rows aligned
+      }
+    }
+  }
+  seq.insert(seq.end(), norm_items.begin() + (ptrdiff_t)tail, norm_items.begin() + (ptrdiff_t)(norm_items.size() - nfill));
+  seq.insert(seq.end(), quant_items.begin(), quant_items.end());
+  p.n_ring_gran = std::max<int64_t>(gb, 1);
+}
+
 static void build_ring_sequence(omf_plan& p, std::vector<omf::ring::Item>& seq,
                                 std::vector<omf::ring::Tensor>& tens) {
   namespace R = omf::ring;
   const R::Config c = R::config(p.ring_cfg);
   const int64_t ch = R::chunk_elems(c);
+  if (c.kind == 1) return build_rr_sequence(p, ch, seq, tens);
   p.ring_hold_max = p.ring_hold_override > 0 ? p.ring_hold_override : (int64_t)c.slots * p.ring_grid;
   const int64_t gap = p.ring_gap >= 0 ? p.ring_gap : p.ring_grid;
   seq.clear();

@@ -34,6 +34,8 @@
 #include "omf_qsgd_dev.h"
 #include "omf_ring.h"
 
+#include <utility>
+
 namespace omf {
 namespace ring {
 namespace {
@@ -142,6 +144,88 @@ __device__ __forceinline__ void quant_group_at(const Args& a, const float4 (&w)[
   }
 }
 
+// ---------------------------------------------------------------- buffer-op helpers
+// Chunk-relative buffer descriptors, range-checked by the hardware per dword (loads out of
+// range read 0, stores out of range are dropped; a descriptor of 0 bytes turns an access
+// into a no-op).  Every access of a thread uses ONE 32-bit lane offset plus a scalar row
+// offset, a tensor's partial last chunk needs no guard, and a step can issue the same
+// memory instructions whatever it has to do — hipcc counts its vmcnt waits only across
+// straight-line loads (a branch around a load makes it wait vmcnt(0), draining every
+// prefetch in flight: cdna_hip_programming.md §5, trap (c)).
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+constexpr int kAuxNT = 2;    // cache policy nt: streamed once
+constexpr int kAuxSC1 = 16;  // sc1: agent-coherent (granules cross the XCDs' private L2s)
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t chunk_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+// float4 of row `sl` (byte offset voff + sl * 4 KiB).
+__device__ __forceinline__ float4 ld_row(__amdgpu_buffer_rsrc_t r, int voff, int sl) {
+  const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, sl * 4096, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ void st_row(__amdgpu_buffer_rsrc_t r, int voff, int sl, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(
+      (u32x4_t){__float_as_uint(v.x), __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)}, r, voff,
+      sl * 4096, kAuxNT);
+}
+// Four levels of row `sl` (element offset eoff of the row-0 float4).  int8: one packed
+// dword (the descriptor spans the chunk rounded up to 4 bytes: the tail of a partial last
+// dword lands in the arena's alignment padding as zeros).
+template <int WIDTH>
+__device__ __forceinline__ void st_levels(__amdgpu_buffer_rsrc_t r, int eoff, int sl, const int32_t (&qq)[4]) {
+  if (WIDTH == 1) {
+    __builtin_amdgcn_raw_buffer_store_b32(pack_i8x4(qq), r, eoff, sl * 1024, kAuxNT);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4_t){(uint32_t)qq[0], (uint32_t)qq[1], (uint32_t)qq[2], (uint32_t)qq[3]},
+                                           r, 4 * eoff, sl * 4096, kAuxNT);
+  }
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t payload_rsrc(const Args& a, int width, int64_t begin, int64_t n) {
+  return chunk_rsrc(static_cast<int8_t*>(a.q) + begin * width, width == 1 ? (n + 3) & ~int64_t(3) : 4 * n);
+}
+
+// One Philox group of the register-resident kernel: rows 4rg .. 4rg+3 at float4 column j,
+// held in w (already scaled).  The Philox words are consumed as they are produced (same
+// stream and bits as philox_group: row sl takes words 3sl .. 3sl+2 of the group's three
+// calls), so at most one call's output and two carried words are live beside the chunk
+// buffers.  HAS_U: caller uniforms (parity mode) through the chunk-relative descriptor ru.
+template <int WIDTH, bool HAS_U>
+__device__ __forceinline__ void quant_group_rr(const Args& a, const float4 (&w)[4], int rg, int j, int64_t coff,
+                                               int32_t tensor, float norm, __amdgpu_buffer_rsrc_t rq,
+                                               __amdgpu_buffer_rsrc_t ru, int voff) {
+  const bool zero = !(norm != 0.0f);
+  const Divisor dv(norm);
+  auto row = [&](int sl, float4 u) {
+    int32_t qq[4];
+    qsgd_quad(w[sl], u, dv, a.levels, zero, qq);
+    st_levels<WIDTH>(rq, voff >> 2, sl, qq);
+  };
+  if (HAS_U) {
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) row(sl, ld_row(ru, voff, sl));
+    return;
+  }
+  // counter 3G + c, G = ((coff >> 12) + rg) * 256 + j: a uniform 64-bit part plus 3j + c < 2^10
+  // (kept 32-bit: a per-lane 64-bit counter base costs two registers for the whole loop)
+  const uint64_t base = 3 * ((((uint64_t)(coff >> 12) + (uint64_t)rg)) << 8);
+  const uint32_t blo = (uint32_t)base, bhi = (uint32_t)(base >> 32);
+  auto call = [&](uint32_t c) {
+    const uint32_t add = 3u * (uint32_t)j + c;
+    const uint32_t lo = blo + add;
+    const uint32_t hi = bhi + (lo < add ? 1u : 0u);
+    return philox4x32_10(make_uint4(lo, hi, (uint32_t)tensor, a.offset), a.seed_lo, a.seed_hi);
+  };
+  const uint4 r0 = call(0);
+  row(0, u24x4(r0.x, r0.y, r0.z));
+  const uint4 r1 = call(1);
+  row(1, u24x4(r0.w, r1.x, r1.y));
+  const uint4 r2 = call(2);
+  row(2, u24x4(r1.z, r1.w, r2.x));
+  row(3, u24x4(r2.y, r2.z, r2.w));
+}
+
 // ---------------------------------------------------------------- producer/consumer kernel
 //
 // One 1024-thread workgroup per CU: waves 0-7 are LOADERS, waves 8-15 QUANTISERS, and
@@ -225,11 +309,11 @@ __device__ __forceinline__ bool poll_norm_wave(const Args& a, const Tensor& ti, 
   return true;
 }
 
-// Bounded poll; on expiry recompute every chunk partial exactly as the loaders do (8 wave
-// partials folded in order) and fold them like the poll: same bits, err bit 2 set.
-template <int ROWS, int LW>
-__device__ __forceinline__ float wait_norm_wave(const Args& a, const Tensor& ti, int lane) {
-  constexpr int64_t CH = (int64_t)ROWS * 1024;
+// Bounded poll; on expiry recompute every chunk partial with `partial(cb, n)` (the
+// producers' exact order) and fold them like the poll: same bits, err bit 2 set.
+template <class Partial>
+__device__ __forceinline__ float wait_norm_poll(const Args& a, const Tensor& ti, int lane, int64_t ch,
+                                                Partial partial) {
   const uint64_t t0 = wall_clock64();
   float norm;
   for (;;) {
@@ -239,14 +323,23 @@ __device__ __forceinline__ float wait_norm_wave(const Args& a, const Tensor& ti,
   }
   double p = 0.0;
   for (int c = 0; c < ti.nchunks; ++c) {
-    const int64_t cb = ti.begin + (int64_t)c * CH;
-    const int n = (int)min(CH, ti.begin + ti.n - cb);
-    double fold = 0.0;
-    for (int w = 0; w < LW; ++w) fold += wave_sum_f64((double)loader_sumsq<ROWS, LW>(a, cb, n, w, lane));
-    if ((c & 63) == lane) p += (double)(float)fold;
+    const int64_t cb = ti.begin + (int64_t)c * ch;
+    const int n = (int)min(ch, ti.begin + ti.n - cb);
+    const float part = partial(cb, n);
+    if ((c & 63) == lane) p += (double)part;
   }
   if (lane == 0) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return ufirst(sqrtf((float)wave_sum_f64(p)));
+}
+
+// The LDS ring's chunk partial: LW loader-wave partials folded in order.
+template <int ROWS, int LW>
+__device__ __forceinline__ float wait_norm_wave(const Args& a, const Tensor& ti, int lane) {
+  return wait_norm_poll(a, ti, lane, (int64_t)ROWS * 1024, [&](int64_t cb, int n) {
+    double fold = 0.0;
+    for (int w = 0; w < LW; ++w) fold += wave_sum_f64((double)loader_sumsq<ROWS, LW>(a, cb, n, w, lane));
+    return (float)fold;
+  });
 }
 
 // ROWS rows per chunk, S LDS slots, LW loader waves (the other 16 - LW quantise), DB:
@@ -424,6 +517,10 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
 #pragma unroll
           for (int q = 0; q < S; ++q)
             if (q == s) use = uses[q]++;
+          // Like every claimer: not before all claimers have left the slot's previous use.
+          // (freed only says its tiles are done; a late claimer's failing ticket may still
+          // be outstanding, and a ticket taken before it would steal this use's tile 0.)
+          lds_wait_ge(&tclaim[s], PER_USE * use);
           claim_tiles(s, use, k - S, prev);  // help quantise it (takes this wave's failing ticket)
         }
         if (ufirst((int)lds_ld(&freed[s])) < (int)(k - S + 1) && DB && idxo < n_items && !pubo) {
@@ -556,12 +653,454 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
   prof.flush(a);
 }
 
+// ---------------------------------------------------------------- register-resident kernel
+//
+// Every wave streams its own part of each chunk through registers: no LDS staging and no
+// producer/consumer hand-off.  Thread t owns the Philox group (rg = t >> 8, j = t & 255)
+// of every 64 KiB chunk: rows 4rg .. 4rg+3 at float4 column j (a wave reads 1 KiB
+// contiguous per instruction).  Position p of a workgroup is its p-th item (sequence index
+// blockIdx.x + p * grid).  With D register buffers per thread, step p:
+//   1. issues the loads of position p+D-1 (its buffer was freed by step p-1);
+//   2. publishes position p+1 as soon as it lands (prologue; thread fp32 chain -> wave
+//      fp64 butterfly -> the 16 wave partials folded in wave order in LDS -> one granule);
+//   3. resolves the norm of position p's tensor: wave 0 (the poller) consumes the granule
+//      poll it issued at the end of step p-1 (or polls again) and hands the norm to the
+//      other waves through LDS;
+//   4. quantises position p from registers and stores the payload;
+//   5. (poller) issues the granule poll for position p+1's tensor.  It is consumed in step
+//      p+1 before anything else waits on memory, so its wait (vmcnt retires in issue
+//      order) covers only what was issued before it, never step p+1's chunk loads.
+// The plan packs every single-read tensor inside one sequence row (all its chunks share
+// one position; omf_qsgd.hip build_ring_sequence), so position p's norm needs only
+// position-p publishes, which every workgroup makes one step before it needs a norm:
+// deadlock-free, with a quantisation step of slack for workgroups that lag.  Tensors of
+// more than one row are NORM items (publish only, never wait) ahead of their QUANT items.
+
+// The register-resident chunk partial (fallback recompute): thread (w, lane)'s four
+// float4 in row order, wave butterfly, waves folded in order — the publish order exactly.
+__device__ __forceinline__ float rr_chunk_partial(const Args& a, int64_t cb, int n, int lane) {
+  const __amdgpu_buffer_rsrc_t rx = chunk_rsrc(a.x + cb, 4 * (int64_t)n);
+  double fold = 0.0;
+  for (int w = 0; w < 16; ++w) {
+    const int voff = 4 * ((w >> 2) * 4096 + 4 * (((w & 3) << 6) + lane));
+    float acc = 0.0f;
+    for (int sl = 0; sl < 4; ++sl) acc = sumsq4(prologue4(a, ld_row(rx, voff, sl)), acc);
+    fold += wave_sum_f64((double)acc);
+  }
+  return (float)fold;
+}
+
+template <int D, int L, int WIDTH, bool HAS_U>
+__global__ __launch_bounds__(1024, 4) void qsgd_encode_rr(Args a, const Item* __restrict__ items,
+                                                          const Tensor* __restrict__ tinfo) {
+  static_assert(L >= 1 && D >= L + 2, "step p publishes p+L while p+L+1 .. p+D-1 stay in flight");
+  constexpr int CH = 16 * 1024, NW = 16, PR = 4;
+  constexpr int NP = 4;  // granules per lane of an early poll (tensors of <= 256 chunks)
+  __shared__ double lpart[PR][NW];
+  __shared__ uint32_t rarrive[PR], rgen[PR];
+  __shared__ float qnorm[2];
+  __shared__ uint32_t qflag[2], qdone[2];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = ufirst(t >> 6);
+  const int rg = wave >> 2, j = ((wave & 3) << 6) + lane;
+  const int voff = 4 * (rg * 4096 + 4 * j);  // byte offset of this thread's row-0 float4 in a chunk
+  if (t < PR) {
+    rarrive[t] = 0;
+    rgen[t] = (uint32_t)t;
+  }
+  if (t < 2) {
+    qflag[t] = 0;
+    qdone[t] = 0;
+    qnorm[t] = 0.0f;
+  }
+  __syncthreads();
+  const int64_t G = gridDim.x, n_items = a.n_items;
+  const int64_t npos = (n_items - (int64_t)blockIdx.x + G - 1) / G;
+  // Position p's item; past the end an empty item (no flags, no elements), so that every
+  // step issues the same memory instructions (zero-size descriptors) without a branch.
+  auto item_at = [&](int64_t p) __attribute__((always_inline)) -> Item {
+    Item it = items[(int64_t)blockIdx.x + min(p, npos - 1) * G];
+    if (p >= npos) {
+      it.flags = 0;
+      it.end = it.begin;
+    }
+    return it;
+  };
+
+  auto load = [&](float4 (&v)[4], int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    const __amdgpu_buffer_rsrc_t rx = chunk_rsrc(a.x + it.begin, 4 * (it.end - it.begin));
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) v[sl] = ld_row(rx, voff, sl);
+  };
+
+  uint32_t npub = 0;  // publishes so far (identical in every wave)
+  auto publish = [&](float4 (&v)[4], int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    const bool pub = (it.flags & kPublish) != 0;
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) v[sl] = prologue4(a, v[sl]);
+    // PS fusion: the averaged parameters, written once (a no-op descriptor otherwise)
+    const __amdgpu_buffer_rsrc_t ro =
+        chunk_rsrc(a.xout ? a.xout + it.begin : a.x, a.xout && pub ? 4 * (it.end - it.begin) : 0);
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) st_row(ro, voff, sl, v[sl]);
+    bool last = false;
+    double fold = 0.0;
+    if (pub) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) acc = sumsq4(v[sl], acc);
+      const double wp = wave_sum_f64((double)acc);
+      const int r = (int)(npub % PR);
+      lds_wait_ge(&rgen[r], npub);  // record free (publish npub - PR folded)
+      if (lane == 0) lpart[r][wave] = wp;
+      lds_drain();
+      const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&rarrive[r], 1u) : 0u));
+      if (old == NW - 1) {  // last wave in: fold in wave order
+        last = true;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) fold += lpart[r][w];
+        if (lane == 0) {
+          lds_st(&rarrive[r], 0u);
+          lds_drain();
+          lds_st(&rgen[r], npub + PR);
+        }
+      }
+      ++npub;
+    }
+    // the granule (sc1 store of lane 0 of the last wave; every other lane stores nothing)
+    const __amdgpu_buffer_rsrc_t rgr = chunk_rsrc(a.gran + it.gbase + it.chunk, last && lane == 0 ? 8 : 0);
+    __builtin_amdgcn_raw_buffer_store_b64((u32x2_t){__float_as_uint((float)fold), a.epoch}, rgr, 0, 0, kAuxSC1);
+  };
+
+  // Norm hand-off: resolution r uses LDS slot r & 1; wave 0 writes it once the other 15
+  // waves have read the slot's previous use (qdone), and raises qflag.
+  int32_t cached_t = -1;
+  float cached_norm = 0.0f;
+  uint32_t nres = 0;
+  u32x2_t pg[NP];
+  int32_t pend_t = -1;  // tensor of wave 0's outstanding early poll
+  auto consume_poll = [&](const Item& it, float& norm) __attribute__((always_inline)) -> bool {
+    double sum = 0.0;  // poll_norm_wave's fold
+    int ok = 1;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      if (lane + 64 * i < it.nchunks) {
+        ok &= pg[i].y == a.epoch;
+        sum += (double)__uint_as_float(pg[i].x);
+      }
+    }
+    if (!__all(ok)) return false;
+    norm = ufirst(sqrtf((float)wave_sum_f64(sum)));
+    return true;
+  };
+  auto resolve = [&](const Item& it) __attribute__((always_inline)) -> float {
+    if (it.tensor == cached_t) return cached_norm;
+    const int s = (int)(nres & 1);
+    const uint32_t use = nres >> 1;
+    ++nres;
+    float norm = 1.0f;
+    if (wave == 0) {
+      bool ok = (a.dbg & 1) != 0;
+      if (!ok && pend_t == it.tensor) ok = consume_poll(it, norm);
+      if (!ok)
+        norm = wait_norm_poll(a, tensor_of(it), lane, CH,
+                              [&](int64_t cb, int n) { return rr_chunk_partial(a, cb, n, lane); });
+      lds_wait_ge(&qdone[s], (uint32_t)(NW - 1) * use);
+      if (lane == 0) {
+        qnorm[s] = norm;
+        lds_drain();
+        lds_st(&qflag[s], use + 1);
+      }
+    } else {
+      lds_wait_ge(&qflag[s], use + 1);
+      norm = ufirst(qnorm[s]);
+      if (lane == 0) lds_add(&qdone[s], 1u);
+    }
+    cached_t = it.tensor;
+    cached_norm = norm;
+    return norm;
+  };
+
+  auto quantise = [&](const float4 (&v)[4], int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    const int64_t n = it.end - it.begin;
+    if (it.flags & kQuant) {
+      const float norm = resolve(it);
+      if (it.chunk == 0 && wave == 0 && lane == 0) a.norm_out[it.tensor] = norm;
+      const __amdgpu_buffer_rsrc_t ru = chunk_rsrc(HAS_U ? a.u + it.begin : a.x, HAS_U ? 4 * n : 0);
+      if (!(a.dbg & 2))
+        quant_group_rr<WIDTH, HAS_U>(a, v, rg, j, it.begin - it.tbegin, it.tensor, norm,
+                                     payload_rsrc(a, WIDTH, it.begin, n), ru, voff);
+    } else {  // the same stores, through a no-op descriptor
+      const __amdgpu_buffer_rsrc_t rq = chunk_rsrc(a.q, 0);
+      const int32_t zq[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) st_levels<WIDTH>(rq, voff >> 2, sl, zq);
+    }
+  };
+
+  // Early poll for position p's tensor: wave 0 reads the granules when p needs a new norm;
+  // every other wave (and wave 0 otherwise) issues the same loads through a no-op descriptor.
+  auto poll_next = [&](int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    const bool need = wave == 0 && (it.flags & kQuant) && it.tensor != cached_t && it.nchunks <= 64 * NP &&
+                      !(a.dbg & 1);
+    const __amdgpu_buffer_rsrc_t rp = chunk_rsrc(a.gran + it.gbase, need ? 8 * (int64_t)it.nchunks : 0);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) pg[i] = __builtin_amdgcn_raw_buffer_load_b64(rp, 8 * (lane + 64 * i), 0, kAuxSC1);
+    pend_t = need ? it.tensor : -1;
+  };
+
+  // Buffer indices must be compile-time constants (registers, not scratch): each step of a
+  // D-step round is instantiated with its own index.  Steps past the end are empty.
+  float4 buf[D][4];
+  auto step = [&](int64_t p0, auto bc) __attribute__((always_inline)) {
+    constexpr int b = decltype(bc)::value;
+    const int64_t p = p0 + b;
+    load(buf[(b + D - 1) % D], p + D - 1);
+    publish(buf[(b + L) % D], p + L);
+    quantise(buf[b], p);
+    poll_next(p + 1);
+  };
+  auto round = [&](int64_t p0, auto seq) __attribute__((always_inline)) {
+    [&]<int... B>(std::integer_sequence<int, B...>) __attribute__((always_inline)) {
+      (step(p0, std::integral_constant<int, B>{}), ...);
+    }(seq);
+  };
+  auto prologue = [&]<int... B>(std::integer_sequence<int, B...>) __attribute__((always_inline)) {
+    (load(buf[B], B), ...);
+  };
+  auto prologue_pub = [&]<int... B>(std::integer_sequence<int, B...>) __attribute__((always_inline)) {
+    (publish(buf[B], B), ...);
+  };
+  prologue(std::make_integer_sequence<int, D - 1>{});
+  prologue_pub(std::make_integer_sequence<int, L>{});
+  for (int64_t p0 = 0; p0 < npos; p0 += D) round(p0, std::make_integer_sequence<int, D>{});
+}
+
+template <int WIDTH, bool HAS_U>
+__global__ __launch_bounds__(1024, 4) void qsgd_encode_rr2(Args a, const Item* __restrict__ items,
+                                                          const Tensor* __restrict__ tinfo) {
+  constexpr int L = 2;  // step p publishes p+2
+  constexpr int CH = 16 * 1024, NW = 16, PR = 4;
+  constexpr int NP = 4;  // granules per lane of an early poll (tensors of <= 256 chunks)
+  __shared__ float4 hold[2][4][1024];  // published chunks p+1, p+2 wait here for their norms
+  __shared__ double lpart[PR][NW];
+  __shared__ uint32_t rarrive[PR], rgen[PR];
+  __shared__ float qnorm[2];
+  __shared__ uint32_t qflag[2], qdone[2];
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = ufirst(t >> 6);
+  const int rg = wave >> 2, j = ((wave & 3) << 6) + lane;
+  const int voff = 4 * (rg * 4096 + 4 * j);  // byte offset of this thread's row-0 float4 in a chunk
+  if (t < PR) {
+    rarrive[t] = 0;
+    rgen[t] = (uint32_t)t;
+  }
+  if (t < 2) {
+    qflag[t] = 0;
+    qdone[t] = 0;
+    qnorm[t] = 0.0f;
+  }
+  __syncthreads();
+  const int64_t G = gridDim.x, n_items = a.n_items;
+  const int64_t npos = (n_items - (int64_t)blockIdx.x + G - 1) / G;
+  // Position p's item; past the end an empty item (no flags, no elements), so that every
+  // step issues the same memory instructions (zero-size descriptors) without a branch.
+  auto item_at = [&](int64_t p) __attribute__((always_inline)) -> Item {
+    Item it = items[(int64_t)blockIdx.x + min(p, npos - 1) * G];
+    if (p >= npos) {
+      it.flags = 0;
+      it.end = it.begin;
+    }
+    return it;
+  };
+
+  auto load = [&](float4 (&v)[4], int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    const __amdgpu_buffer_rsrc_t rx = chunk_rsrc(a.x + it.begin, 4 * (it.end - it.begin));
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) v[sl] = ld_row(rx, voff, sl);
+  };
+
+  uint32_t npub = 0;  // publishes so far (identical in every wave)
+  auto publish = [&](float4 (&v)[4], int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    const bool pub = (it.flags & kPublish) != 0;
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) v[sl] = prologue4(a, v[sl]);
+    // PS fusion: the averaged parameters, written once (a no-op descriptor otherwise)
+    const __amdgpu_buffer_rsrc_t ro =
+        chunk_rsrc(a.xout ? a.xout + it.begin : a.x, a.xout && pub ? 4 * (it.end - it.begin) : 0);
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) st_row(ro, voff, sl, v[sl]);
+    bool last = false;
+    double fold = 0.0;
+    if (pub) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) acc = sumsq4(v[sl], acc);
+      const double wp = wave_sum_f64((double)acc);
+      const int r = (int)(npub % PR);
+      lds_wait_ge(&rgen[r], npub);  // record free (publish npub - PR folded)
+      if (lane == 0) lpart[r][wave] = wp;
+      lds_drain();
+      const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&rarrive[r], 1u) : 0u));
+      if (old == NW - 1) {  // last wave in: fold in wave order
+        last = true;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) fold += lpart[r][w];
+        if (lane == 0) {
+          lds_st(&rarrive[r], 0u);
+          lds_drain();
+          lds_st(&rgen[r], npub + PR);
+        }
+      }
+      ++npub;
+    }
+    // the granule (sc1 store of lane 0 of the last wave; every other lane stores nothing)
+    const __amdgpu_buffer_rsrc_t rgr = chunk_rsrc(a.gran + it.gbase + it.chunk, last && lane == 0 ? 8 : 0);
+    __builtin_amdgcn_raw_buffer_store_b64((u32x2_t){__float_as_uint((float)fold), a.epoch}, rgr, 0, 0, kAuxSC1);
+  };
+
+  // Norm hand-off: resolution r uses LDS slot r & 1.  At the START of step p wave 0
+  // resolves position p's norm (consuming the poll it issued a whole step earlier, or
+  // polling again) and writes the slot once the other 15 waves have read its previous use
+  // (qdone); the other waves read it when they reach the quantisation of p.
+  int32_t cached_t = -1;
+  float cached_norm = 0.0f;
+  uint32_t nres = 0;
+  int rd_slot = -1;      // other waves: the slot holding a norm not read yet
+  uint32_t rd_use = 0;
+  u32x2_t pg[NP];
+  int32_t pend_t = -1;   // tensor of wave 0's outstanding early poll
+  auto consume_poll = [&](const Item& it, float& norm) __attribute__((always_inline)) -> bool {
+    double sum = 0.0;  // poll_norm_wave's fold
+    int ok = 1;
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      if (lane + 64 * i < it.nchunks) {
+        ok &= pg[i].y == a.epoch;
+        sum += (double)__uint_as_float(pg[i].x);
+      }
+    }
+    if (!__all(ok)) return false;
+    norm = ufirst(sqrtf((float)wave_sum_f64(sum)));
+    return true;
+  };
+  auto resolve_early = [&](int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    if (!(it.flags & kQuant) || it.tensor == cached_t) return;
+    const int s = (int)(nres & 1);
+    const uint32_t use = nres >> 1;
+    ++nres;
+    cached_t = it.tensor;
+    if (wave == 0) {
+      float norm = 1.0f;
+      bool ok = (a.dbg & 1) != 0;
+      if (!ok && pend_t == it.tensor) ok = consume_poll(it, norm);
+      if (!ok)
+        norm = wait_norm_poll(a, tensor_of(it), lane, CH,
+                              [&](int64_t cb, int n) { return rr_chunk_partial(a, cb, n, lane); });
+      lds_wait_ge(&qdone[s], (uint32_t)(NW - 1) * use);
+      if (lane == 0) {
+        qnorm[s] = norm;
+        lds_drain();
+        lds_st(&qflag[s], use + 1);
+      }
+      cached_norm = norm;
+    } else {
+      rd_slot = s;
+      rd_use = use;
+    }
+  };
+  auto quantise = [&](const float4 (&v)[4], int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    const int64_t n = it.end - it.begin;
+    if (it.flags & kQuant) {
+      if (rd_slot >= 0) {
+        lds_wait_ge(&qflag[rd_slot], rd_use + 1);
+        cached_norm = ufirst(qnorm[rd_slot]);
+        if (lane == 0) lds_add(&qdone[rd_slot], 1u);
+        rd_slot = -1;
+      }
+      const float norm = cached_norm;
+      if (it.chunk == 0 && wave == 0 && lane == 0) a.norm_out[it.tensor] = norm;
+      const __amdgpu_buffer_rsrc_t ru = chunk_rsrc(HAS_U ? a.u + it.begin : a.x, HAS_U ? 4 * n : 0);
+      if (!(a.dbg & 2))
+        quant_group_rr<WIDTH, HAS_U>(a, v, rg, j, it.begin - it.tbegin, it.tensor, norm,
+                                     payload_rsrc(a, WIDTH, it.begin, n), ru, voff);
+    } else {  // the same stores, through a no-op descriptor
+      const __amdgpu_buffer_rsrc_t rq = chunk_rsrc(a.q, 0);
+      const int32_t zq[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) st_levels<WIDTH>(rq, voff >> 2, sl, zq);
+    }
+  };
+
+  // Early poll for position p's tensor (issued after p-1's norm is resolved): wave 0 reads
+  // the granules when p needs a new norm; every other wave (and wave 0 otherwise) issues
+  // the same loads through a no-op descriptor.
+  auto poll_next = [&](int64_t p) __attribute__((always_inline)) {
+    const Item it = item_at(p);
+    const bool need = wave == 0 && (it.flags & kQuant) && it.tensor != cached_t && it.nchunks <= 64 * NP &&
+                      !(a.dbg & 1);
+    const __amdgpu_buffer_rsrc_t rp = chunk_rsrc(a.gran + it.gbase, need ? 8 * (int64_t)it.nchunks : 0);
+#pragma unroll
+    for (int i = 0; i < NP; ++i) pg[i] = __builtin_amdgcn_raw_buffer_load_b64(rp, 8 * (lane + 64 * i), 0, kAuxSC1);
+    pend_t = need ? it.tensor : -1;
+  };
+
+  // Chunk c is loaded into register buffer rb[c % 3] (chunks p+3, p+4 in flight during step
+  // p), published from there into LDS slot hold[c % 2], and quantised from registers after
+  // its step reads it back.  Indices are compile-time constants: a round is 6 steps.
+  float4 rb[3][4], qb[4];
+  auto park = [&](const float4 (&v)[4], int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) hold[slot][sl][t] = v[sl];
+  };
+  auto unpark = [&](float4 (&v)[4], int slot) __attribute__((always_inline)) {
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) v[sl] = hold[slot][sl][t];
+  };
+  auto step = [&](int64_t p0, auto bc) __attribute__((always_inline)) {
+    constexpr int b = decltype(bc)::value;
+    const int64_t p = p0 + b;
+    resolve_early(p);                // consumes the poll issued a step ago
+    poll_next(p + 1);                // publishes of p+1 were made a step ago, everywhere
+    unpark(qb, b % 2);               // chunk p leaves its slot ...
+    publish(rb[(b + 2) % 3], p + 2);  // ... which chunk p+2 takes
+    park(rb[(b + 2) % 3], b % 2);
+    load(rb[(b + 2) % 3], p + 5);
+    quantise(qb, p);
+  };
+  auto round = [&](int64_t p0, auto seq) __attribute__((always_inline)) {
+    [&]<int... B>(std::integer_sequence<int, B...>) __attribute__((always_inline)) {
+      (step(p0, std::integral_constant<int, B>{}), ...);
+    }(seq);
+  };
+  load(rb[0], 0);
+  load(rb[1], 1);
+  load(rb[2], 2);
+  publish(rb[0], 0);
+  park(rb[0], 0);
+  load(rb[0], 3);
+  publish(rb[1], 1);
+  park(rb[1], 1);
+  load(rb[1], 4);
+  for (int64_t p0 = 0; p0 < npos; p0 += 6) round(p0, std::make_integer_sequence<int, 6>{});
+}
+
 // Instantiated configurations: {rows of 1024 elements per chunk, LDS slots, loader
 // waves, loader double-buffering}.  cfg 0 is the default (fastest measured).
 constexpr Config kConfigs[] = {
     {16, 2, 8, 0},  // 64 KiB chunks x 2 slots, 8 loader + 1 poller + 7 claimer waves, loaders help
     {16, 2, 8, 1},  // same with double-buffered loaders (no spare registers to help: they only load)
     {8, 4, 8, 1},   // 32 KiB chunks x 4 slots (per-chunk synchronisation dominates: slower)
+    {16, 4, 0, 0, 1},  // register-resident: 64 KiB chunks, 4 register buffers per thread, lookahead 1
+    {16, 3, 0, 0, 1},  // register streams + 2 LDS slots for published chunks: lookahead 2
 };
 
 template <int ROWS, int S, int LW, bool DB>
@@ -574,8 +1113,19 @@ const void* kernel_ptr(int width, bool has_u) {
                : (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 4, false>;
 }
 
+// Caller uniforms (parity mode) hold 16 more registers per thread: 3 buffers keep them unspilled.
+template <int D, int L>
+const void* kernel_ptr_rr(int width, bool has_u) {
+  if (width == 1) return has_u ? (const void*)qsgd_encode_rr<3, 1, 1, true> : (const void*)qsgd_encode_rr<D, L, 1, false>;
+  return has_u ? (const void*)qsgd_encode_rr<3, 1, 4, true> : (const void*)qsgd_encode_rr<D, L, 4, false>;
+}
+
 const void* kernel_for(int cfg, int width, bool has_u) {
   switch (cfg) {
+    case 3: return kernel_ptr_rr<4, 1>(width, has_u);
+    case 4:
+      if (width == 1) return has_u ? (const void*)qsgd_encode_rr2<1, true> : (const void*)qsgd_encode_rr2<1, false>;
+      return has_u ? (const void*)qsgd_encode_rr2<4, true> : (const void*)qsgd_encode_rr2<4, false>;
     case 1: return kernel_ptr<16, 2, 8, true>(width, has_u);
     case 2: return kernel_ptr<8, 4, 8, true>(width, has_u);
     default: return kernel_ptr<16, 2, 8, false>(width, has_u);

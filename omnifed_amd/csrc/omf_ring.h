@@ -59,6 +59,8 @@ struct Config {
   int slots;    // LDS ring slots (each one chunk)
   int loaders;  // loader waves of the 16 (the rest quantise)
   int dbuf;     // loaders prefetch two chunks ahead
+  int kind = 0;  // 0: LDS ring (qsgd_encode_pc); 1: register-resident (qsgd_encode_rr, slots =
+                 // register buffers per thread; the plan packs single-read tensors in one row)
 };
 
 int num_configs();

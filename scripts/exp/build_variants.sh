@@ -2,7 +2,7 @@
 # Experiment builds of the codec library (never shipped): RNG cost variants.
 set -e
 cd "$(dirname "$0")/../.."
-F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude"
+F="--offload-arch=gfx950 -O3 -std=c++20 -fPIC -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude"
 build() {
   local name=$1; shift
   mkdir -p scripts/exp/_build/$name

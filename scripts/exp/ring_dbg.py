@@ -8,13 +8,14 @@ sys.path.insert(0, ".")
 from omnifed_amd import codec, shapes  # noqa: E402
 
 dev = torch.device("cuda", 0)
-sizes = [shapes.numel(s) for _, s in shapes.model_shapes(sys.argv[1] if len(sys.argv) > 1 else "llama400m")]
+sizes = [shapes.numel(s) for _, s in shapes.model_shapes("llama400m")]
+cfgs = [int(c) for c in sys.argv[1].split(",")] if len(sys.argv) > 1 else [0]
 p = codec.Plan(sizes, device=dev)
 x = torch.randn(p.arena_end, device=dev) * 1e-3
 q = torch.empty(p.arena_end, dtype=torch.int8, device=dev)
 nr = torch.empty(p.nt, device=dev)
 p.set_encode_strategy("ring")
-for cfg in (0,):
+for cfg in cfgs:
     for bm in (1,):
         p.set_ring(cfg=cfg, big_mode=bm)
         for _ in range(2):
@@ -32,14 +33,16 @@ for cfg in (0,):
 if int(os.environ.get("OMF_RING_DBG", "0")) & 4:
     names = ["L wait free slot", "L load+reduce", "Q wait loaded", "poller resolve", "Q wait norm", "Q tiles",
              "L total", "Q total"]
-    for cfg in (0,):
+    for cfg in cfgs:
+        if cfg == 3:
+            names = ["-", "publish", "resolve norm", "quantise", "-", "-", "total", "-"]
         p.set_ring(cfg=cfg, big_mode=1)
         p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1)
         p.ring_profile()
         p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1)
         prof = p.ring_profile()
         lw, qw = 8, 8
-        waves = {0: lw, 1: lw, 2: qw, 3: 1, 4: qw - 1, 5: qw, 6: lw, 7: qw}
+        waves = {0: lw, 1: lw, 2: qw, 3: 1, 4: qw - 1, 5: qw, 6: lw, 7: qw} if cfg != 3 else {i: 16 for i in range(8)}
         for i, nm in enumerate(names):
             per_wave = prof[i] / (256 * waves[i])
             print(f"  {nm:18s} {per_wave / 2400:10.1f} us/wave (shader cycles / 2.4 GHz)", flush=True)

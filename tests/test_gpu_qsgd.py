@@ -159,7 +159,7 @@ def test_strategies_agree_and_fallback_exact(gpu):
             assert torch.equal(qa[o:o + n], qb[o:o + n])
 
 
-@pytest.mark.parametrize("cfg", [0, 1, 2])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
 @pytest.mark.parametrize("hold", [0, 3])
 def test_ring_configs_match_oracle(gpu, cfg, hold):
     """Every ring configuration, with large tensors held (hold=0) or taking two passes (hold=3

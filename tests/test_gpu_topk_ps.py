@@ -152,7 +152,7 @@ def test_wire_roundtrip_and_reference_tests(gpu):
     assert layer.compression_type == "TopKCompression" and len(layer.param_update) == 0
     dec = decode_layer_tensor(layer, base_tensor=base)
     mask = torch.ones(16, dtype=torch.bool)
-    mask[np.frombuffer(layer.indices_data, dtype=np.int64)] = False
+    mask[torch.from_numpy(np.frombuffer(layer.indices_data, dtype=np.int64).copy())] = False
     assert torch.allclose(dec.reshape(-1)[mask], base.reshape(-1)[mask])
 
     comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4)
