@@ -157,9 +157,11 @@ int omf_div_f32(float* y, int64_t n, float divisor, void* stream);
  * Replaces TopKCompression.compress (src/omnifed/hybrid/compression/topk.py:33-42)
  * with ResidualUpdates.compensate/update (src/omnifed/hybrid/compression/core.py:26-37)
  * and topk_sparse (topk.py:10-15):
- *   residual_mode 0: t' = x                       (no error-feedback state)
- *   residual_mode 1: t' = residual + x, then residual := t' - desparse(selection)
- *   residual_mode 2: t' = x,            then residual := t' - desparse(selection)
+ *   a = fl32(alpha * x): the client weighting param * batch_samples
+ *       (global_grpc.py:101-123) fused in; alpha = 1 leaves x's bits unchanged.
+ *   residual_mode 0: t' = a                       (no error-feedback state)
+ *   residual_mode 1: t' = residual + a, then residual := t' - desparse(selection)
+ *   residual_mode 2: t' = a,            then residual := t' - desparse(selection)
  *                    (first call for a name: the reference has no residual yet)
  *   k_t = max(1, int(n_t * ratio))  (omf_topk_k); the k_t largest |t'| of tensor t;
  *   values (fp32 t') / indices (tensor-local int64) of tensor t are written at
@@ -167,12 +169,13 @@ int omf_div_f32(float* y, int64_t n, float divisor, void* stream);
  * Order within a tensor: descending |t'|, ties by ascending index (torch.topk's
  * order for k*64 <= n on the reference CPU path; ties there are unspecified).
  * ws: caller workspace of omf_topk_workspace_bytes(plan, ratio) bytes.
- * Synchronises `stream` once (the candidate count sizes the device-wide sort).
+ * Synchronises `stream` once (the candidate count sizes the device-wide sort), twice
+ * when a sampled threshold has to be redone exactly for some tensor.
  */
 int64_t omf_topk_k(int64_t numel, double ratio);
 size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio);
 int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,
-                    float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream);
+                    float alpha, float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream);
 
 /*
  * Top-K decode of ONE tensor of n elements: topk_desparse (topk.py:18-21),

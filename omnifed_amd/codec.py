@@ -286,8 +286,10 @@ class Plan:
 
     def topk_encode(self, x: torch.Tensor, ratio: float, residual: Optional[torch.Tensor] = None,
                     residual_mode: int = 0, values: Optional[torch.Tensor] = None,
-                    indices: Optional[torch.Tensor] = None, stream: Optional[int] = None):
-        """Returns ``(values, indices, ks)``; tensor t's selection at ``[sum(ks[:t]), +ks[t])``."""
+                    indices: Optional[torch.Tensor] = None, stream: Optional[int] = None, alpha: float = 1.0):
+        """Returns ``(values, indices, ks)``; tensor t's selection at ``[sum(ks[:t]), +ks[t])``.
+
+        ``alpha``: the client weighting (t' = residual + fl32(alpha * x)), fused in."""
         dev = self.device
         ks = self.topk_ks(ratio)
         for n, k in zip(self.sizes, ks):
@@ -314,7 +316,7 @@ class Plan:
             if self._topk_ws is None or self._topk_ws.numel() < need:
                 self._topk_ws = torch.empty(need, dtype=torch.uint8, device=dev)
             check(L.omf_topk_encode(self._h, _ptr(x), _ptr(residual) if residual_mode else None, int(residual_mode),
-                                    float(ratio), _ptr(values), _ptr(indices), _ptr(self._topk_ws),
+                                    float(ratio), float(alpha), _ptr(values), _ptr(indices), _ptr(self._topk_ws),
                                     ctypes.c_size_t(self._topk_ws.numel()), ctypes.c_void_p(st)),
                   "omf_topk_encode")
         return values, indices, ks

@@ -1,27 +1,34 @@
 // omf_topk.hip — Top-K sparsification with error feedback, MI355X (gfx950).
 //
 // Semantics: src/omnifed/hybrid/compression/topk.py:10-47 + core.py:19-37 (reference):
-//   t' = residual + x ; k = max(1, int(n * ratio)) ; the k largest |t'| ;
+//   t' = residual + alpha * x ; k = max(1, int(n * ratio)) ; the k largest |t'| ;
 //   residual := t' - desparse(values, indices)  (= t' with the selected slots set to t'-t').
+// alpha is the client weighting param * batch_samples (global_grpc.py:101-123), fused in;
+// alpha = 1 leaves x's bits unchanged.
 //
-// Passes (all tensors of a plan per launch):
-//   1. topk_prep_hist   read x (+residual), write t' into the residual buffer, and a
-//                       1024-bin histogram of the top 10 bits of |t'| (exponent + 2
-//                       mantissa bits) per tensor (LDS histogram, non-zero bins flushed).
-//   2. topk_select_bin  per tensor: the bin b1 holding the k-th largest magnitude.
-//   3. topk_collect     re-read t'; every element whose bin >= b1 is a candidate
-//                       (about 1-2.5 % of a gradient at k = 1 %), appended with one
-//                       wave-aggregated atomic per wave as a 64-bit key
-//                       (|t'| bits << 32 | ~index): descending key order = descending
-//                       magnitude, ties by ascending index.
-//   4. one device-wide radix sort of all candidates (rocPRIM onesweep) on the composite
-//                       key (tensor << 56 | (2^31-1 - |t'|bits) << 25 | index), i.e.
-//                       tensor ascending, magnitude descending, index ascending; when a
-//                       plan exceeds 256 tensors or 2^25 elements per tensor, a segmented
-//                       descending sort of (|t'|bits << 32 | ~index) per tensor instead.
-//   5. topk_gather      first k keys of every tensor -> values / int64 indices; zero
-//                       the selected residual slots.
+// Passes (all tensors of a plan per launch; <= 256 tensors of <= 2^25 elements):
+//   1. topk_sample      one t' per max(256, n/32Ki) elements (hashed offset) -> per-tensor
+//                       8192-bin histogram of the top 13 bits of |t'| (exponent + 5 mantissa
+//                       bits), aggregated in LDS.
+//   2. topk_threshold   per tensor: the bin whose suffix holds k*S/n + 5 sqrt(k*S/n) + 25 of
+//                       the S samples — a threshold below the k-th magnitude with ~5 sigma of
+//                       margin (tensors too small to sample keep every element).
+//   3. topk_fused       ONE streaming pass: read x (+ residual), write t' into the residual,
+//                       and append every |t'| at or above the threshold (~1.1-1.8 k) as a
+//                       64-bit key (tensor << 56 | (2^31-1 - |t'|bits) << 25 | index) into the
+//                       item's own region (one block scan per 8 Ki elements, no contended
+//                       atomics).
+//   4. topk_check       candidates per tensor from the item scan; a tensor whose sample put
+//                       the threshold too high (fewer than k) is redone exactly from t': its
+//                       1024-bin histogram, the bin of the k-th magnitude, a re-collection.
+//   5. one device-wide radix sort of the candidates (rocPRIM onesweep): tensor ascending,
+//      magnitude descending, index ascending (= torch's partial-sort order when k*64 <= n).
+//   6. topk_gather      first k keys of every tensor -> values / int64 indices; zero the
+//                       selected residual slots.
+// Larger plans take the exact path (histogram of every t', collection, a segmented
+// descending sort of (|t'|bits << 32 | ~index) per tensor).
 // Decode is a scatter (mode 0 zero-fill, 1 overlay, 2 scatter-add).
+#include <cmath>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -37,7 +44,13 @@ using namespace omf;
 namespace {
 
 constexpr int kBins = 1024;
-constexpr int kShift = 21;  // key (31 bits) >> 21 -> 10-bit bin
+constexpr int kShift = 21;  // key (31 bits) >> 21 -> 10-bit bin (exact path)
+constexpr int kSBits = 13;  // sample histogram: exponent + 5 mantissa bits
+constexpr int kSBins = 1 << kSBits;
+constexpr int kSShift = 31 - kSBits;
+constexpr int kSStride = 256;   // at least 256 elements per sample ...
+constexpr int kSMax = 32768;    // ... and at most 32 Ki samples per tensor
+constexpr int kSBlocks = 64;    // sampling blocks per tensor (<= 2 samples per thread)
 constexpr int kV = 16;
 constexpr int64_t kSub = (int64_t)kV * kThreads * 4;
 
@@ -47,16 +60,255 @@ struct Item {
   int32_t tensor, kind, chunk, pad;
 };
 
-
 __device__ __forceinline__ uint32_t mag_key(float v) { return __float_as_uint(v) & 0x7fffffffu; }
 
-template <int MODE>  // 0: t' = x ; 1: t' = r + x, r := t' ; 2: t' = x, r := t'
+__device__ __forceinline__ uint32_t hash32(uint32_t h) {  // murmur3 finaliser
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  return h ^ (h >> 16);
+}
+
+// t' of one element: MODE 0/2: alpha * x ; MODE 1: r + alpha * x (the reference's order).
+template <int MODE>
+__device__ __forceinline__ float tprime(float x, float r, float alpha) {
+  const float t = __fmul_rn(x, alpha);
+  return MODE == 1 ? __fadd_rn(r, t) : t;
+}
+
+// Per tensor: k, the output offset, and the tensor's flat-item range (items are 16 Ki
+// sub-chunks in tensor order: omf_qsgd.hip upload_plan).  One block; nt may exceed it.
+__global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict__ tsize, int32_t nt, double ratio,
+                                                       int64_t* __restrict__ kk, int64_t* __restrict__ koff,
+                                                       uint32_t* __restrict__ tfirst, uint32_t* __restrict__ tlast) {
+  __shared__ int64_t s_k[kThreads], s_i[kThreads];
+  int64_t carry_k = 0, carry_i = 0;
+  for (int32_t t0 = 0; t0 < nt; t0 += kThreads) {
+    const int32_t t = t0 + (int32_t)threadIdx.x;
+    int64_t k = 0, ni = 0;
+    if (t < nt) {
+      k = (int64_t)((double)tsize[t] * ratio);
+      if (k < 1) k = 1;
+      ni = (tsize[t] + kSub - 1) / kSub;
+    }
+    s_k[threadIdx.x] = k;
+    s_i[threadIdx.x] = ni;
+    __syncthreads();
+    for (int o = 1; o < kThreads; o <<= 1) {  // inclusive scans
+      const int64_t ak = threadIdx.x >= (unsigned)o ? s_k[threadIdx.x - o] : 0;
+      const int64_t ai = threadIdx.x >= (unsigned)o ? s_i[threadIdx.x - o] : 0;
+      __syncthreads();
+      s_k[threadIdx.x] += ak;
+      s_i[threadIdx.x] += ai;
+      __syncthreads();
+    }
+    if (t < nt) {
+      kk[t] = k;
+      koff[t] = carry_k + s_k[threadIdx.x] - k;
+      tfirst[t] = (uint32_t)(carry_i + s_i[threadIdx.x] - ni);
+      tlast[t] = (uint32_t)(carry_i + s_i[threadIdx.x] - 1);
+      if (t == nt - 1) koff[nt] = carry_k + s_k[threadIdx.x];
+    }
+    carry_k += s_k[kThreads - 1];
+    carry_i += s_i[kThreads - 1];
+    __syncthreads();
+  }
+}
+
+// Pass 1: sample histograms.  grid (kSBlocks, nt); block b of tensor t takes samples
+// b*256 + j, stepping by kSBlocks*256; sample s reads element s*stride + hash(.) % span.
+__device__ __forceinline__ int64_t sample_stride(int64_t n) {
+  return max((int64_t)kSStride, (n + kSMax - 1) / kSMax);
+}
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void topk_sample(const float* __restrict__ x, const float* __restrict__ r,
+                                                        float alpha, const int64_t* __restrict__ tbegin,
+                                                        const int64_t* __restrict__ tsize,
+                                                        uint32_t* __restrict__ shist) {
+  __shared__ uint32_t h[kSBins];
+  const int t = blockIdx.y;
+  const int64_t base = tbegin[t], n = tsize[t];
+  const int64_t stride = sample_stride(n), ns = (n + stride - 1) / stride;
+  if ((int64_t)blockIdx.x * kThreads >= ns) return;  // small tensors use few blocks
+  for (int b = threadIdx.x; b < kSBins; b += kThreads) h[b] = 0;
+  __syncthreads();
+  for (int64_t s = (int64_t)blockIdx.x * kThreads + threadIdx.x; s < ns; s += (int64_t)kSBlocks * kThreads) {
+    const int64_t lo = s * stride;
+    const uint32_t span = (uint32_t)min(stride, n - lo);
+    const int64_t e = base + lo + (int64_t)(hash32((uint32_t)lo ^ ((uint32_t)t * 0x9E3779B9u)) % span);
+    const float v = tprime<MODE>(x[e], MODE == 1 ? r[e] : 0.0f, alpha);
+    atomicAdd(&h[mag_key(v) >> kSShift], 1u);
+  }
+  __syncthreads();
+  uint32_t* ht = shist + (size_t)t * kSBins;
+  for (int b = threadIdx.x; b < kSBins; b += kThreads)
+    if (h[b]) atomicAdd(&ht[b], h[b]);
+}
+
+// Pass 2: per tensor, the sample-histogram bin of the threshold (0 = every element).
+__global__ __launch_bounds__(1024) void topk_threshold(const uint32_t* __restrict__ shist,
+                                                       const int64_t* __restrict__ kk,
+                                                       const int64_t* __restrict__ tsize, uint32_t* __restrict__ tbin) {
+  constexpr int PER = kSBins / 1024;
+  __shared__ uint32_t part[1024];
+  const int t = blockIdx.x;
+  const uint32_t* ht = shist + (size_t)t * kSBins;
+  uint32_t c[PER], loc = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    c[j] = ht[PER * threadIdx.x + j];
+    loc += c[j];
+  }
+  part[threadIdx.x] = loc;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive suffix scan
+    const uint32_t add = threadIdx.x + o < 1024 ? part[threadIdx.x + o] : 0u;
+    __syncthreads();
+    part[threadIdx.x] += add;
+    __syncthreads();
+  }
+  const uint32_t S = part[0];
+  const double m = (double)kk[t] * (double)S / (double)max(tsize[t], (int64_t)1);
+  const double want = m + 5.0 * sqrt(m) + 25.0;
+  if (m < 16.0 || want >= (double)S) {  // too few samples to trust: keep every element
+    if (threadIdx.x == 0) tbin[t] = 0;
+    return;
+  }
+  const uint32_t target = (uint32_t)ceil(want);
+  uint32_t above = threadIdx.x + 1 < 1024 ? part[threadIdx.x + 1] : 0u;  // samples in higher bins
+  for (int j = PER - 1; j >= 0; --j) {
+    if (above < target && above + c[j] >= target) tbin[t] = PER * threadIdx.x + j;  // exactly one match
+    above += c[j];
+  }
+}
+
+// Append the selected elements of one 8 Ki-element pass of an item to the item's region
+// (block scan of the per-lane counts; coalesced per (row, component)).
+struct PassCollector {
+  uint32_t* s_wsum;  // kWaves
+  __device__ __forceinline__ uint32_t append(const float4 (&v)[8], uint32_t selm, uint64_t* dst, uint32_t idx0,
+                                             uint64_t tag) const {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t nsel = (uint32_t)__popc(selm);
+    uint32_t wtot = nsel;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) wtot += __shfl_xor(wtot, o, 64);
+    if (lane == 0) s_wsum[wave] = wtot;
+    __syncthreads();
+    uint32_t wpre = 0, tot = 0;
+#pragma unroll
+    for (int w2 = 0; w2 < kWaves; ++w2) {
+      if (w2 < wave) wpre += s_wsum[w2];
+      tot += s_wsum[w2];
+    }
+    __syncthreads();  // s_wsum reuse by the next pass
+    dst += wpre;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    if (wtot) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          const bool sel = (selm >> (4 * k + c)) & 1u;
+          const uint64_t m = __ballot(sel);
+          if (sel) {
+            const uint32_t idx = idx0 + 1024u * k + c;
+            dst[__popcll(m & lt)] = tag | ((uint64_t)(0x7fffffffu - mag_key(vv[c])) << 25) | (uint64_t)idx;
+          }
+          dst += __popcll(m);
+        }
+      }
+    }
+    return tot;
+  }
+};
+
+// Pass 3: t' (written to the residual in the EF modes) and the candidates above the
+// sampled threshold, per item.  MODE 0: t' = alpha x (not stored); 1: r := r + alpha x;
+// 2: r := alpha x.
+template <int MODE>
+__global__ __launch_bounds__(kThreads, MODE == 0 ? 4 : 6) void topk_fused(const float* __restrict__ x, float* __restrict__ r, float alpha,
+                                                       const Item* __restrict__ items,
+                                                       const int64_t* __restrict__ tbegin,
+                                                       const uint32_t* __restrict__ tbin,
+                                                       uint32_t* __restrict__ item_cnt, uint64_t* __restrict__ cand) {
+  __shared__ uint32_t s_wsum[kWaves];
+  const Item it = items[blockIdx.x];
+  const uint32_t thr = tbin[it.tensor];
+  const int64_t base = tbegin[it.tensor];
+  constexpr int64_t CS = 8 * kThreads * 4;  // 8192 elements per pass
+  const PassCollector col{s_wsum};
+  const uint64_t tag = (uint64_t)it.tensor << 56;
+  uint32_t item_total = 0;
+  for (int64_t b = it.begin; b < it.end; b += CS) {
+    const uint32_t lim = (uint32_t)(min(b + CS, it.end) - b);
+    const uint32_t off0 = 4u * threadIdx.x;
+    float4 v[8];
+    uint32_t selm = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const uint32_t o = off0 + 1024u * k;
+      float vv[4] = {0.f, 0.f, 0.f, 0.f};
+      if (o + 4 <= lim) {
+        const float4 xv = *reinterpret_cast<const float4*>(x + b + o);
+        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (MODE == 1) rv = *reinterpret_cast<const float4*>(r + b + o);
+        vv[0] = tprime<MODE>(xv.x, rv.x, alpha);
+        vv[1] = tprime<MODE>(xv.y, rv.y, alpha);
+        vv[2] = tprime<MODE>(xv.z, rv.z, alpha);
+        vv[3] = tprime<MODE>(xv.w, rv.w, alpha);
+        if (MODE != 0) *reinterpret_cast<float4*>(r + b + o) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+      } else {
+        for (uint32_t c = 0; c < 4 && o + c < lim; ++c) {
+          vv[c] = tprime<MODE>(x[b + o + c], MODE == 1 ? r[b + o + c] : 0.0f, alpha);
+          if (MODE != 0) r[b + o + c] = vv[c];
+        }
+      }
+      v[k] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (o + c < lim && (mag_key(vv[c]) >> kSShift) >= thr) selm |= 1u << (4 * k + c);
+    }
+    item_total += col.append(v, selm, cand + it.begin + item_total, (uint32_t)(b - base) + off0, tag);
+  }
+  if (threadIdx.x == 0) item_cnt[blockIdx.x] = item_total;
+}
+
+// Candidates per tensor from the item scan; flag the tensors whose threshold was too high.
+__global__ __launch_bounds__(kThreads) void topk_check(int32_t nt, const int64_t* __restrict__ kk,
+                                                       const uint32_t* __restrict__ tfirst,
+                                                       const uint32_t* __restrict__ tlast,
+                                                       const uint32_t* __restrict__ item_cnt,
+                                                       const uint32_t* __restrict__ item_off, int64_t n_items,
+                                                       int64_t* __restrict__ cstart, uint32_t* __restrict__ cnt,
+                                                       uint32_t* __restrict__ flag, uint32_t* __restrict__ status) {
+  for (int32_t t = threadIdx.x; t < nt; t += kThreads) {
+    const uint32_t f = tfirst[t], l = tlast[t];
+    const uint32_t c = item_off[l] + item_cnt[l] - item_off[f];
+    cstart[t] = item_off[f];
+    cnt[t] = c;
+    const uint32_t redo = (int64_t)c < kk[t] ? 1u : 0u;
+    flag[t] = redo;
+    if (redo) atomicOr(&status[1], 1u);
+  }
+  if (threadIdx.x == 0) status[0] = item_off[n_items - 1] + item_cnt[n_items - 1];
+}
+
+// Exact path, pass 1 (and the per-tensor redo): t' and its 1024-bin histogram per tensor.
+// MODE as topk_fused.  flag != null: only the flagged tensors (a redo reads t' as x with
+// MODE 0 and alpha = the scale of t').
+template <int MODE>
 __global__ __launch_bounds__(kThreads) void topk_prep_hist(const float* __restrict__ x, float* __restrict__ r,
-                                                           const Item* __restrict__ items, uint32_t* __restrict__ hist) {
+                                                           float alpha, const Item* __restrict__ items,
+                                                           const uint32_t* __restrict__ flag,
+                                                           uint32_t* __restrict__ hist) {
   __shared__ uint32_t h[kBins];
+  const Item it = items[blockIdx.x];
+  if (flag && !flag[it.tensor]) return;  // block-uniform
   for (int b = threadIdx.x; b < kBins; b += kThreads) h[b] = 0;
   __syncthreads();
-  const Item it = items[blockIdx.x];
   for (int64_t b = it.begin; b < it.end; b += kSub) {
     const int64_t end = min(b + kSub, it.end);
 #pragma unroll 4
@@ -67,20 +319,18 @@ __global__ __launch_bounds__(kThreads) void topk_prep_hist(const float* __restri
       const bool full = e + 4 <= end;
       const int nv = full ? 4 : (int)(end - e);
       if (full) {
-        float4 t = *reinterpret_cast<const float4*>(x + e);
-        if (MODE == 1) {
-          const float4 rr = *reinterpret_cast<const float4*>(r + e);
-          t.x = __fadd_rn(rr.x, t.x); t.y = __fadd_rn(rr.y, t.y);
-          t.z = __fadd_rn(rr.z, t.z); t.w = __fadd_rn(rr.w, t.w);
-        }
-        if (MODE != 0) *reinterpret_cast<float4*>(r + e) = t;
-        v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+        const float4 xv = *reinterpret_cast<const float4*>(x + e);
+        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (MODE == 1) rv = *reinterpret_cast<const float4*>(r + e);
+        v[0] = tprime<MODE>(xv.x, rv.x, alpha);
+        v[1] = tprime<MODE>(xv.y, rv.y, alpha);
+        v[2] = tprime<MODE>(xv.z, rv.z, alpha);
+        v[3] = tprime<MODE>(xv.w, rv.w, alpha);
+        if (MODE != 0) *reinterpret_cast<float4*>(r + e) = make_float4(v[0], v[1], v[2], v[3]);
       } else {
         for (int c = 0; c < nv; ++c) {
-          float t = x[e + c];
-          if (MODE == 1) t = __fadd_rn(r[e + c], t);
-          if (MODE != 0) r[e + c] = t;
-          v[c] = t;
+          v[c] = tprime<MODE>(x[e + c], MODE == 1 ? r[e + c] : 0.0f, alpha);
+          if (MODE != 0) r[e + c] = v[c];
         }
       }
       for (int c = 0; c < nv; ++c) atomicAdd(&h[mag_key(v[c]) >> kShift], 1u);
@@ -92,11 +342,14 @@ __global__ __launch_bounds__(kThreads) void topk_prep_hist(const float* __restri
     if (h[b]) atomicAdd(&ht[b], h[b]);
 }
 
-// One block per tensor: b1 = max bin with suffix count >= k.
+// One block per tensor: b1 = max bin with suffix count >= k (flag: only flagged tensors).
 __global__ __launch_bounds__(kThreads) void topk_select_bin(const uint32_t* __restrict__ hist,
-                                                            const int64_t* __restrict__ kk, uint32_t* __restrict__ bin) {
+                                                            const int64_t* __restrict__ kk,
+                                                            const uint32_t* __restrict__ flag,
+                                                            uint32_t* __restrict__ bin) {
   __shared__ uint32_t s_part[kThreads];
   const int t = blockIdx.x;
+  if (flag && !flag[t]) return;
   const uint32_t* ht = hist + (size_t)t * kBins;
   // thread i owns bins [4i, 4i+4); suffix sums over threads from the top.
   uint32_t c[4], loc = 0;
@@ -104,8 +357,7 @@ __global__ __launch_bounds__(kThreads) void topk_select_bin(const uint32_t* __re
   for (int j = 0; j < 4; ++j) { c[j] = ht[4 * threadIdx.x + j]; loc += c[j]; }
   s_part[threadIdx.x] = loc;
   __syncthreads();
-  // inclusive suffix scan (Hillis-Steele) over s_part
-  for (int o = 1; o < kThreads; o <<= 1) {
+  for (int o = 1; o < kThreads; o <<= 1) {  // inclusive suffix scan (Hillis-Steele)
     const uint32_t add = (threadIdx.x + o < kThreads) ? s_part[threadIdx.x + o] : 0u;
     __syncthreads();
     s_part[threadIdx.x] += add;
@@ -119,70 +371,65 @@ __global__ __launch_bounds__(kThreads) void topk_select_bin(const uint32_t* __re
   }
 }
 
-__global__ void topk_offsets(const int64_t* __restrict__ tsize,
-                             int32_t nt, double ratio, int64_t* __restrict__ kk, int64_t* __restrict__ koff,
-                             const int64_t* __restrict__ tbegin, const uint32_t* __restrict__ cnt,
-                             uint32_t* __restrict__ seg_b, uint32_t* __restrict__ seg_e, int phase) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  if (phase == 0) {
-    int64_t acc = 0;
-    for (int t = 0; t < nt; ++t) {
-      int64_t k = (int64_t)((double)tsize[t] * ratio);
-      if (k < 1) k = 1;
-      kk[t] = k;
-      koff[t] = acc;
-      acc += k;
-    }
-    koff[nt] = acc;
-  } else {
-    for (int t = 0; t < nt; ++t) {
-      seg_b[t] = (uint32_t)tbegin[t];
-      seg_e[t] = (uint32_t)(tbegin[t] + cnt[t]);
-    }
+// Segment bounds of the exact path's per-tensor sort.
+__global__ void topk_segments(int32_t nt, const int64_t* __restrict__ tbegin, const uint32_t* __restrict__ cnt,
+                              uint32_t* __restrict__ seg_b, uint32_t* __restrict__ seg_e) {
+  for (int32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < nt; t += gridDim.x * blockDim.x) {
+    seg_b[t] = (uint32_t)tbegin[t];
+    seg_e[t] = (uint32_t)(tbegin[t] + cnt[t]);
   }
 }
 
-// Candidates of one item: every |t'| whose bin is >= b1.  Counts are aggregated per
-// sub-chunk (block scan in LDS) so each sub-chunk costs ONE global atomic on its tensor's
-// counter; keys go to the tensor's own region cand[tbegin + pos] (capacity n_t).
+// Exact-path candidates of one item: every t' (= scale * tp) whose bin is >= b1.
+// GLOBAL: composite keys into the item's own region, counted per item (redo: flagged
+// tensors only).  Otherwise (|t'|bits << 32 | ~index) appended to the tensor's region
+// through one atomic per block pass.
 template <bool GLOBAL>
-__global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict__ tp, const Item* __restrict__ items,
+__global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict__ tp, float scale,
+                                                         const Item* __restrict__ items,
                                                          const int64_t* __restrict__ tbegin,
-                                                         const uint32_t* __restrict__ bin, uint32_t* __restrict__ cnt,
+                                                         const uint32_t* __restrict__ bin,
+                                                         const uint32_t* __restrict__ flag, uint32_t* __restrict__ cnt,
                                                          uint32_t* __restrict__ item_cnt, uint64_t* __restrict__ cand) {
   __shared__ uint32_t s_wsum[kWaves];
   __shared__ uint32_t s_base;
   const Item it = items[blockIdx.x];
+  if (flag && !flag[it.tensor]) return;  // block-uniform
   const uint32_t b1 = bin[it.tensor];
   const int64_t base = tbegin[it.tensor];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int CV = 8;                           // rows per pass (register budget)
-  constexpr int64_t CS = (int64_t)CV * kThreads * 4;  // 8192 elements
-  uint32_t item_total = 0;                         // GLOBAL: running offset in the item's region
+  constexpr int CV = 8;
+  constexpr int64_t CS = (int64_t)CV * kThreads * 4;
+  const PassCollector col{s_wsum};
+  const uint64_t tag = (uint64_t)it.tensor << 56;
+  uint32_t item_total = 0;
   for (int64_t b = it.begin; b < it.end; b += CS) {
-    const int64_t end = min(b + CS, it.end);
-    const uint32_t lim = (uint32_t)(end - b);  // elements of this pass
-    const uint32_t off0 = 4u * threadIdx.x;    // this lane's first element
+    const uint32_t lim = (uint32_t)(min(b + CS, it.end) - b);
+    const uint32_t off0 = 4u * threadIdx.x;
     float4 v[CV];
-    uint32_t selm = 0;  // bit 4k+c: element (row k, component c) is a candidate
+    uint32_t selm = 0;
 #pragma unroll
     for (int k = 0; k < CV; ++k) {
       const uint32_t o = off0 + 1024u * k;
+      float vv[4] = {0.f, 0.f, 0.f, 0.f};
       if (o + 4 <= lim) {
-        v[k] = *reinterpret_cast<const float4*>(tp + b + o);
+        const float4 t4 = *reinterpret_cast<const float4*>(tp + b + o);
+        vv[0] = t4.x; vv[1] = t4.y; vv[2] = t4.z; vv[3] = t4.w;
       } else {
-        v[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (o < lim) v[k].x = tp[b + o];
-        if (o + 1 < lim) v[k].y = tp[b + o + 1];
-        if (o + 2 < lim) v[k].z = tp[b + o + 2];
+        for (uint32_t c = 0; c < 4 && o + c < lim; ++c) vv[c] = tp[b + o + c];
       }
-      const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) vv[c] = __fmul_rn(vv[c], scale);
+      v[k] = make_float4(vv[0], vv[1], vv[2], vv[3]);
 #pragma unroll
       for (int c = 0; c < 4; ++c)
         if (o + c < lim && (mag_key(vv[c]) >> kShift) >= b1) selm |= 1u << (4 * k + c);
     }
+    if (GLOBAL) {
+      item_total += col.append(v, selm, cand + it.begin + item_total, (uint32_t)(b - base) + off0, tag);
+      continue;
+    }
     const uint32_t nsel = (uint32_t)__popc(selm);
-    // wave totals -> block scan in LDS
     uint32_t wtot = nsel;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) wtot += __shfl_xor(wtot, o, 64);
@@ -194,14 +441,10 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
       if (w2 < wave) wpre += s_wsum[w2];
       tot += s_wsum[w2];
     }
-    // GLOBAL: the item's candidates go to its own element range (capacity = item size),
-    // counted per item and packed after an exclusive scan — no contended atomics.
-    if (!GLOBAL && threadIdx.x == 0) s_base = tot ? atomicAdd(&cnt[it.tensor], tot) : 0u;
+    if (threadIdx.x == 0) s_base = tot ? atomicAdd(&cnt[it.tensor], tot) : 0u;
     __syncthreads();
-    // coalesced writes: per (row, component) the selected lanes of a wave store consecutively
-    uint64_t* dst = GLOBAL ? cand + it.begin + item_total + wpre : cand + base + s_base + wpre;
+    uint64_t* dst = cand + base + s_base + wpre;
     const uint32_t idx0 = (uint32_t)(b - base) + off0;
-    const uint64_t tag = (uint64_t)it.tensor << 56;
     const uint64_t lt = (1ull << lane) - 1ull;
     if (wtot) {
 #pragma unroll
@@ -213,15 +456,12 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
           const uint64_t m = __ballot(sel);
           if (sel) {
             const uint32_t idx = idx0 + 1024u * k + c;
-            const uint32_t key = mag_key(vv[c]);
-            dst[__popcll(m & lt)] = GLOBAL ? (tag | ((uint64_t)(0x7fffffffu - key) << 25) | (uint64_t)idx)
-                                           : (((uint64_t)key << 32) | (uint64_t)(~idx));
+            dst[__popcll(m & lt)] = ((uint64_t)mag_key(vv[c]) << 32) | (uint64_t)(~idx);
           }
           dst += __popcll(m);
         }
       }
     }
-    item_total += tot;
     __syncthreads();  // s_wsum / s_base reuse
   }
   if (GLOBAL && threadIdx.x == 0) item_cnt[blockIdx.x] = item_total;
@@ -238,20 +478,9 @@ __global__ __launch_bounds__(kThreads) void topk_compact(const uint64_t* __restr
   for (uint32_t j = threadIdx.x; j < n; j += kThreads) packed[dst + j] = cand[it.begin + j];
 }
 
-// Per-tensor start and count of the packed candidates, from the item scan.
-__global__ void topk_tensor_ranges(const Item* __restrict__ items, int64_t n_items,
-                                   const uint32_t* __restrict__ item_cnt, const uint32_t* __restrict__ item_off,
-                                   int64_t* __restrict__ cstart, uint32_t* __restrict__ cnt) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_items; i += (int64_t)gridDim.x * blockDim.x) {
-    const Item it = items[i];
-    if (it.chunk == 0) cstart[it.tensor] = item_off[i];
-    atomicAdd(&cnt[it.tensor], item_cnt[i]);
-  }
-}
-
 template <bool GLOBAL>
-__global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict__ tp, float* __restrict__ r,
-                                                        const uint64_t* __restrict__ sorted,
+__global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict__ tp, float scale,
+                                                        float* __restrict__ r, const uint64_t* __restrict__ sorted,
                                                         const int64_t* __restrict__ tbegin,
                                                         const int64_t* __restrict__ cstart,
                                                         const int64_t* __restrict__ kk, const int64_t* __restrict__ koff,
@@ -262,7 +491,7 @@ __global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict_
   for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < k; j += (int64_t)gridDim.x * kThreads) {
     const uint64_t key = sorted[s0 + j];
     const uint32_t idx = GLOBAL ? (uint32_t)(key & 0x1FFFFFFull) : ~(uint32_t)key;
-    const float v = tp[base + idx];
+    const float v = __fmul_rn(tp[base + idx], scale);
     values[o + j] = v;
     indices[o + j] = (int64_t)idx;
     if (r) r[base + idx] = __fsub_rn(v, v);
@@ -326,22 +555,30 @@ size_t sort_tmp_bytes(const omf_plan* p) {
   return bytes;
 }
 
+// Workspace: everything up to `zero_end` is cleared once per call.
 struct WsLayout {
-  size_t hist, bin, cnt, cnt_all, koff, kk, seg_b, seg_e, cstart, item_cnt, item_off, cand, sorted, tmp, total,
-      tmp_bytes;
+  size_t hist, shist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
+      item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes;
 };
 
 WsLayout layout(const omf_plan* p) {
   const int32_t nt = omf_plan_access::ntensors(p);
   const int64_t ae = omf_plan_access::arena_end(p);
+  const bool glob = global_path(p);
   WsLayout L;
   size_t o = 0;
   L.hist = o; o = align256(o + 4 * (size_t)nt * kBins);
+  L.shist = o; o = align256(o + (glob ? 4 * (size_t)nt * kSBins : 0));
   L.bin = o; o = align256(o + 4 * (size_t)nt);
   L.cnt = o; o = align256(o + 4 * (size_t)nt);
-  L.cnt_all = o; o = align256(o + 4);
+  L.flag = o; o = align256(o + 4 * (size_t)nt);
+  L.status = o; o = align256(o + 16);
+  L.zero_end = o;
+  L.tbin = o; o = align256(o + 4 * (size_t)nt);
   L.koff = o; o = align256(o + 8 * (size_t)(nt + 1));
   L.kk = o; o = align256(o + 8 * (size_t)nt);
+  L.tfirst = o; o = align256(o + 4 * (size_t)nt);
+  L.tlast = o; o = align256(o + 4 * (size_t)nt);
   L.seg_b = o; o = align256(o + 4 * (size_t)nt);
   L.seg_e = o; o = align256(o + 4 * (size_t)nt);
   L.cstart = o; o = align256(o + 8 * (size_t)nt);
@@ -372,7 +609,7 @@ size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio) {
   return layout(plan).total;
 }
 
-int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,
+int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio, float alpha,
                     float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
   if (!x || !values || !indices || !ws) return fail(OMF_EINVAL, "x, values, indices and ws must be non-NULL");
@@ -397,15 +634,21 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   hipStream_t st = (hipStream_t)stream;
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
+  uint32_t* shist = reinterpret_cast<uint32_t*>(w + L.shist);
   uint32_t* bin = reinterpret_cast<uint32_t*>(w + L.bin);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
+  uint32_t* flag = reinterpret_cast<uint32_t*>(w + L.flag);
+  uint32_t* status = reinterpret_cast<uint32_t*>(w + L.status);
+  uint32_t* tbin = reinterpret_cast<uint32_t*>(w + L.tbin);
+  int64_t* koff = reinterpret_cast<int64_t*>(w + L.koff);
+  int64_t* kk = reinterpret_cast<int64_t*>(w + L.kk);
+  uint32_t* tfirst = reinterpret_cast<uint32_t*>(w + L.tfirst);
+  uint32_t* tlast = reinterpret_cast<uint32_t*>(w + L.tlast);
+  uint32_t* seg_b = reinterpret_cast<uint32_t*>(w + L.seg_b);
+  uint32_t* seg_e = reinterpret_cast<uint32_t*>(w + L.seg_e);
   int64_t* cstart = reinterpret_cast<int64_t*>(w + L.cstart);
   uint32_t* item_cnt = reinterpret_cast<uint32_t*>(w + L.item_cnt);
   uint32_t* item_off = reinterpret_cast<uint32_t*>(w + L.item_off);
-  int64_t* koff = reinterpret_cast<int64_t*>(w + L.koff);
-  int64_t* kk = reinterpret_cast<int64_t*>(w + L.kk);
-  uint32_t* seg_b = reinterpret_cast<uint32_t*>(w + L.seg_b);
-  uint32_t* seg_e = reinterpret_cast<uint32_t*>(w + L.seg_e);
   uint64_t* cand = reinterpret_cast<uint64_t*>(w + L.cand);
   uint64_t* sorted = reinterpret_cast<uint64_t*>(w + L.sorted);
   const int32_t nt = omf_plan_access::ntensors(plan);
@@ -413,38 +656,69 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   const Item* items = static_cast<const Item*>(omf_plan_access::flat_items(plan, &n_items));
   const int64_t* d_sizes = omf_plan_access::d_sizes(plan);
   const int64_t* d_begins = omf_plan_access::d_begins(plan);
-
-  // hist, bin, cnt and cnt_all precede L.koff: zero them.
-  OMF_HIP(hipMemsetAsync(w, 0, L.koff, st));
-  hipLaunchKernelGGL(topk_offsets, dim3(1), dim3(64), 0, st, d_sizes, nt, ratio, kk, koff, d_begins, cnt,
-                     seg_b, seg_e, 0);
-  const float* tp = (residual_mode == 0) ? x : residual;
+  // t' lives in the residual (EF modes) or is alpha * x (mode 0)
+  const float* tp = residual_mode == 0 ? x : residual;
+  const float scale = residual_mode == 0 ? alpha : 1.0f;
+  float* rz = residual_mode ? residual : nullptr;  // selected slots to zero
   const dim3 grid((unsigned)n_items), blk(kThreads);
-  if (residual_mode == 0) hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, x, residual, items, hist);
-  else if (residual_mode == 1) hipLaunchKernelGGL((topk_prep_hist<1>), grid, blk, 0, st, x, residual, items, hist);
-  else hipLaunchKernelGGL((topk_prep_hist<2>), grid, blk, 0, st, x, residual, items, hist);
-  hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, bin);
+
+  OMF_HIP(hipMemsetAsync(w, 0, L.zero_end, st));
+  hipLaunchKernelGGL(topk_setup, dim3(1), blk, 0, st, d_sizes, nt, ratio, kk, koff, tfirst, tlast);
   const bool glob = global_path(plan);
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
-    hipLaunchKernelGGL((topk_collect<true>), grid, blk, 0, st, tp, items, d_begins, bin, cnt, item_cnt, cand);
-    size_t sb = L.tmp_bytes;
-    OMF_HIP(rocprim::exclusive_scan(w + L.tmp, sb, item_cnt, item_off, 0u, (size_t)n_items,
-                                    rocprim::plus<uint32_t>(), st, false));
-    hipLaunchKernelGGL(topk_tensor_ranges, dim3(64), blk, 0, st, items, n_items, item_cnt, item_off, cstart, cnt);
-    OMF_HIP(hipGetLastError());
-    uint32_t last[2];  // the sort needs the candidate count on the host
-    OMF_HIP(hipMemcpyAsync(&last[0], item_off + n_items - 1, 4, hipMemcpyDeviceToHost, st));
-    OMF_HIP(hipMemcpyAsync(&last[1], item_cnt + n_items - 1, 4, hipMemcpyDeviceToHost, st));
-    OMF_HIP(hipStreamSynchronize(st));
-    const uint64_t total = (uint64_t)last[0] + last[1];
+    const dim3 sgrid(kSBlocks, (unsigned)nt);
+    if (residual_mode == 1) {
+      hipLaunchKernelGGL((topk_sample<1>), sgrid, blk, 0, st, x, residual, alpha, d_begins, d_sizes, shist);
+      hipLaunchKernelGGL(topk_threshold, dim3((unsigned)nt), dim3(1024), 0, st, shist, kk, d_sizes, tbin);
+      hipLaunchKernelGGL((topk_fused<1>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt, cand);
+    } else {
+      hipLaunchKernelGGL((topk_sample<0>), sgrid, blk, 0, st, x, residual, alpha, d_begins, d_sizes, shist);
+      hipLaunchKernelGGL(topk_threshold, dim3((unsigned)nt), dim3(1024), 0, st, shist, kk, d_sizes, tbin);
+      if (residual_mode == 2)
+        hipLaunchKernelGGL((topk_fused<2>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt,
+                           cand);
+      else
+        hipLaunchKernelGGL((topk_fused<0>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt,
+                           cand);
+    }
+    uint32_t host_status[2] = {0, 0};
+    auto scan_and_check = [&]() -> int {
+      size_t sb = L.tmp_bytes;
+      OMF_HIP(rocprim::exclusive_scan(w + L.tmp, sb, item_cnt, item_off, 0u, (size_t)n_items,
+                                      rocprim::plus<uint32_t>(), st, false));
+      hipLaunchKernelGGL(topk_check, dim3(1), blk, 0, st, nt, kk, tfirst, tlast, item_cnt, item_off, n_items, cstart,
+                         cnt, flag, status);
+      OMF_HIP(hipGetLastError());
+      // the sort needs the candidate count on the host (and the redo decision)
+      OMF_HIP(hipMemcpyAsync(host_status, status, 8, hipMemcpyDeviceToHost, st));
+      OMF_HIP(hipStreamSynchronize(st));
+      return OMF_OK;
+    };
+    if (int rc = scan_and_check()) return rc;
+    if (host_status[1]) {  // a sample set the threshold too high for some tensor: redo it exactly
+      hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, tp, nullptr, scale, items, flag, hist);
+      hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, flag, bin);
+      hipLaunchKernelGGL((topk_collect<true>), grid, blk, 0, st, tp, scale, items, d_begins, bin, flag, cnt, item_cnt,
+                         cand);
+      if (int rc = scan_and_check()) return rc;
+    }
+    const uint64_t total = host_status[0];
     hipLaunchKernelGGL(topk_compact, grid, blk, 0, st, cand, items, item_cnt, item_off, sorted);
     // sort the packed keys back into `cand` (the per-item regions are no longer needed)
     OMF_HIP(rocprim::radix_sort_keys(w + L.tmp, tmp_bytes, sorted, cand, (size_t)total, 0, 64, st, false));
   } else {
-    hipLaunchKernelGGL((topk_collect<false>), grid, blk, 0, st, tp, items, d_begins, bin, cnt, item_cnt, cand);
-    hipLaunchKernelGGL(topk_offsets, dim3(1), dim3(64), 0, st, d_sizes, nt, ratio, kk, koff, d_begins, cnt,
-                       seg_b, seg_e, 1);
+    if (residual_mode == 0)
+      hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
+    else if (residual_mode == 1)
+      hipLaunchKernelGGL((topk_prep_hist<1>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
+    else
+      hipLaunchKernelGGL((topk_prep_hist<2>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
+    hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, nullptr, bin);
+    hipLaunchKernelGGL((topk_collect<false>), grid, blk, 0, st, tp, scale, items, d_begins, bin, nullptr, cnt, item_cnt,
+                       cand);
+    hipLaunchKernelGGL(topk_segments, dim3(((unsigned)nt + kThreads - 1) / kThreads), blk, 0, st, nt, d_begins, cnt,
+                       seg_b, seg_e);
     OMF_HIP(hipGetLastError());
     OMF_HIP(rocprim::segmented_radix_sort_keys_desc(w + L.tmp, tmp_bytes, cand, sorted,
                                                     (unsigned int)omf_plan_access::arena_end(plan), (unsigned int)nt,
@@ -453,11 +727,11 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   const uint64_t* sorted_keys = glob ? cand : sorted;
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((kmax + kThreads - 1) / kThreads, 1024));
   if (glob)
-    hipLaunchKernelGGL((topk_gather<true>), dim3(gx, (unsigned)nt), blk, 0, st, tp, residual_mode ? residual : nullptr,
-                       sorted_keys, d_begins, cstart, kk, koff, values, indices);
+    hipLaunchKernelGGL((topk_gather<true>), dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted_keys, d_begins,
+                       cstart, kk, koff, values, indices);
   else
-    hipLaunchKernelGGL((topk_gather<false>), dim3(gx, (unsigned)nt), blk, 0, st, tp,
-                       residual_mode ? residual : nullptr, sorted_keys, d_begins, cstart, kk, koff, values, indices);
+    hipLaunchKernelGGL((topk_gather<false>), dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted_keys, d_begins,
+                       cstart, kk, koff, values, indices);
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }

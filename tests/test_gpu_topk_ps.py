@@ -109,6 +109,78 @@ def test_topk_degenerate_ties(gpu):
     assert rest == sorted(set(range(n)) - set(nz.tolist()))[: k - len(nz)]
 
 
+def _fmix32(h):
+    h = h.astype(np.uint64)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    return h ^ (h >> np.uint64(16))
+
+
+def _sample_positions(n, t):
+    """The elements omf_topk.hip's topk_sample reads for tensor t (one per max(256, n/32Ki))."""
+    stride = max(256, -(-n // 32768))
+    lo = np.arange(0, n, stride, dtype=np.uint64)
+    key = lo ^ np.uint64((t * 0x9E3779B9) & 0xFFFFFFFF)
+    span = np.minimum(np.uint64(stride), np.uint64(n) - lo)
+    return (lo + _fmix32(key) % span).astype(np.int64)
+
+
+@pytest.mark.parametrize("alpha", [1.0, 3.0])
+def test_topk_sampled_threshold_error_feedback(gpu, alpha):
+    """Large tensors take the sampled-threshold single pass: over three error-feedback calls
+    the selection has the magnitudes of torch.topk's (ties aside), the order is descending,
+    and the residual is t' = residual + fl32(alpha x) with the selection zeroed, bit for bit."""
+    sizes = [1 << 20, 3 << 20, 5000, 1_000_003, 4096]
+    plan = codec.Plan(sizes, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(5)
+    res = torch.zeros(plan.arena_end, device=gpu)
+    ref_res = [torch.zeros(n, device=gpu) for n in sizes]
+    for call in range(3):
+        x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+        values, indices, ks = plan.topk_encode(x, 0.01, residual=res, residual_mode=2 if call == 0 else 1,
+                                               alpha=alpha)
+        K = 0
+        for t, (o, n) in enumerate(zip(plan.offsets, sizes)):
+            a = x[o:o + n] * torch.tensor(alpha, device=gpu)
+            tp = a if call == 0 else ref_res[t] + a
+            k = ks[t]
+            v, i = values[K:K + k], indices[K:K + k]
+            want, _ = torch.topk(tp.abs(), k, sorted=True)
+            assert torch.equal(v.abs(), want), (call, t)
+            assert torch.equal(v, tp[i]), (call, t)
+            r = tp.clone()
+            r[i] = 0.0
+            assert torch.equal(res[o:o + n], r), (call, t)
+            ref_res[t] = r
+            K += k
+
+
+def test_topk_sampled_threshold_redo(gpu):
+    """A tensor whose sampled elements are exactly its largest: the sample puts the threshold
+    above the k-th magnitude, the pass finds fewer than k candidates, and the tensor is redone
+    exactly — the k largest, ties by ascending index."""
+    n = 1 << 20
+    x = np.ones(n, np.float32)
+    sp = _sample_positions(n, 1)
+    x[sp] = 10.0
+    sizes = [40000, n]
+    plan = codec.Plan(sizes, device=gpu)
+    xa = torch.zeros(plan.arena_end)
+    xa[plan.offsets[1]:plan.offsets[1] + n] = torch.from_numpy(x)
+    xa[:40000] = torch.arange(40000, dtype=torch.float32)
+    values, indices, ks = plan.topk_encode(xa.to(gpu), 0.01)
+    k = ks[1]
+    assert k > len(sp)
+    ih = indices[ks[0]:].cpu().numpy()
+    vh = values[ks[0]:].cpu().numpy()
+    rest = np.setdiff1d(np.arange(n), sp)[: k - len(sp)]
+    assert ih.tolist() == sorted(sp.tolist()) + rest.tolist()
+    assert np.all(vh[: len(sp)] == 10.0) and np.all(vh[len(sp):] == 1.0)
+    assert indices[: ks[0]].cpu().tolist() == list(range(39999, 39999 - ks[0], -1))
+
+
 def test_layerwise_decompress(gpu):
     n = 1000
     vals = [torch.randn(10), torch.randn(10)]
