@@ -7,12 +7,13 @@
 // alpha = 1 leaves x's bits unchanged.
 //
 // Passes (all tensors of a plan per launch; <= 256 tensors of <= 2^25 elements):
-//   1. topk_sample      one t' per max(256, n/32Ki) elements (hashed offset) -> per-tensor
-//                       8192-bin histogram of the top 13 bits of |t'| (exponent + 5 mantissa
-//                       bits), aggregated in LDS.
-//   2. topk_threshold   per tensor: the bin whose suffix holds k*S/n + 5 sqrt(k*S/n) + 25 of
-//                       the S samples — a threshold below the k-th magnitude with ~5 sigma of
-//                       margin (tensors too small to sample keep every element).
+//   1. topk_sample_threshold, one block per tensor: one aligned 16-element run of t' per
+//                       max(256, n/4096) elements (hashed position; a random 64-byte sector
+//                       costs the same as one element) into an LDS 8192-bin histogram of the top 13 bits of
+//                       |t'| (exponent + 5 mantissa bits); the bin whose suffix holds
+//                       k*S/n + 6 sqrt(k*S/n) + 32 of the S samples is the threshold — below
+//                       the k-th magnitude with ~6 sigma of margin (tensors too small to
+//                       sample keep every element).
 //   3. topk_fused       ONE streaming pass: read x (+ residual), write t' into the residual,
 //                       and append every |t'| at or above the threshold (~1.1-1.8 k) as a
 //                       64-bit key (tensor << 56 | (2^31-1 - |t'|bits) << 25 | index) into the
@@ -48,9 +49,9 @@ constexpr int kShift = 21;  // key (31 bits) >> 21 -> 10-bit bin (exact path)
 constexpr int kSBits = 13;  // sample histogram: exponent + 5 mantissa bits
 constexpr int kSBins = 1 << kSBits;
 constexpr int kSShift = 31 - kSBits;
-constexpr int kSStride = 256;   // at least 256 elements per sample ...
-constexpr int kSMax = 32768;    // ... and at most 32 Ki samples per tensor
-constexpr int kSBlocks = 64;    // sampling blocks per tensor (<= 2 samples per thread)
+constexpr int kSRun = 16;       // a sample is a 64-byte run of 16 consecutive elements,
+constexpr int kSStride = 256;   // one run per >= 256 elements,
+constexpr int kSMaxRuns = 4096; // at most 4096 runs (64 Ki samples) per tensor
 constexpr int kV = 16;
 constexpr int64_t kSub = (int64_t)kV * kThreads * 4;
 
@@ -116,48 +117,62 @@ __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict
   }
 }
 
-// Pass 1: sample histograms.  grid (kSBlocks, nt); block b of tensor t takes samples
-// b*256 + j, stepping by kSBlocks*256; sample s reads element s*stride + hash(.) % span.
+// Passes 1+2, one 1024-thread block per tensor: R = ceil(n / stride) runs, stride =
+// max(256, n / 4096); run j covers 16 aligned elements at j*stride + 16 * (hash(.) % (span/16))
+// (a whole 64-byte sector: random sectors, not elements, are what the sample costs), so
+// S <= 16 R samples go into an LDS histogram of the top 13 bits of |t'|; then the bin whose
+// suffix holds k*S/n + 6 sqrt(k*S/n) + 32 samples (0 = every element, for tensors too small
+// to sample).  Four lanes read one run (float4 each).
 __device__ __forceinline__ int64_t sample_stride(int64_t n) {
-  return max((int64_t)kSStride, (n + kSMax - 1) / kSMax);
+  return max((int64_t)kSStride, (n + kSMaxRuns - 1) / kSMaxRuns);
 }
 template <int MODE>
-__global__ __launch_bounds__(kThreads) void topk_sample(const float* __restrict__ x, const float* __restrict__ r,
-                                                        float alpha, const int64_t* __restrict__ tbegin,
-                                                        const int64_t* __restrict__ tsize,
-                                                        uint32_t* __restrict__ shist) {
-  __shared__ uint32_t h[kSBins];
-  const int t = blockIdx.y;
-  const int64_t base = tbegin[t], n = tsize[t];
-  const int64_t stride = sample_stride(n), ns = (n + stride - 1) / stride;
-  if ((int64_t)blockIdx.x * kThreads >= ns) return;  // small tensors use few blocks
-  for (int b = threadIdx.x; b < kSBins; b += kThreads) h[b] = 0;
-  __syncthreads();
-  for (int64_t s = (int64_t)blockIdx.x * kThreads + threadIdx.x; s < ns; s += (int64_t)kSBlocks * kThreads) {
-    const int64_t lo = s * stride;
-    const uint32_t span = (uint32_t)min(stride, n - lo);
-    const int64_t e = base + lo + (int64_t)(hash32((uint32_t)lo ^ ((uint32_t)t * 0x9E3779B9u)) % span);
-    const float v = tprime<MODE>(x[e], MODE == 1 ? r[e] : 0.0f, alpha);
-    atomicAdd(&h[mag_key(v) >> kSShift], 1u);
-  }
-  __syncthreads();
-  uint32_t* ht = shist + (size_t)t * kSBins;
-  for (int b = threadIdx.x; b < kSBins; b += kThreads)
-    if (h[b]) atomicAdd(&ht[b], h[b]);
-}
-
-// Pass 2: per tensor, the sample-histogram bin of the threshold (0 = every element).
-__global__ __launch_bounds__(1024) void topk_threshold(const uint32_t* __restrict__ shist,
-                                                       const int64_t* __restrict__ kk,
-                                                       const int64_t* __restrict__ tsize, uint32_t* __restrict__ tbin) {
+__global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __restrict__ x, const float* __restrict__ r,
+                                                              float alpha, const int64_t* __restrict__ tbegin,
+                                                              const int64_t* __restrict__ tsize,
+                                                              const int64_t* __restrict__ kk,
+                                                              uint32_t* __restrict__ tbin) {
   constexpr int PER = kSBins / 1024;
+  constexpr int U = 4;  // runs in flight per lane group
+  __shared__ uint32_t h[kSBins];
   __shared__ uint32_t part[1024];
   const int t = blockIdx.x;
-  const uint32_t* ht = shist + (size_t)t * kSBins;
+  for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
+  __syncthreads();
+  const int64_t base = tbegin[t], n = tsize[t];
+  const int64_t stride = sample_stride(n), nr = (n + stride - 1) / stride;
+  const uint32_t salt = (uint32_t)t * 0x9E3779B9u;
+  const int q = threadIdx.x & 3;  // float4 of the run
+  for (int64_t j0 = threadIdx.x >> 2; j0 < nr; j0 += (int64_t)U * 256) {
+    float4 xv[U], rv[U];
+    int64_t rel[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {  // every load of the batch issued unconditionally (no branch
+      // around a load: hipcc would wait for each one in turn); past-the-end runs clamped
+      const int64_t j = min(j0 + (int64_t)u * 256, nr - 1);
+      const int64_t lo = j * stride;
+      const int64_t span = min(stride, n - lo);
+      const int64_t runs = max((int64_t)1, span / kSRun);
+      rel[u] = lo + kSRun * (int64_t)(hash32((uint32_t)lo ^ salt) % (uint32_t)runs) + 4 * q;
+      const int64_t e = base + min(rel[u], (n - 1) & ~(int64_t)3);  // 16-byte aligned, inside the arena
+      xv[u] = *reinterpret_cast<const float4*>(x + e);
+      rv[u] = MODE == 1 ? *reinterpret_cast<const float4*>(r + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (j0 + (int64_t)u * 256 >= nr) continue;
+      const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+      const float rs[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (rel[u] + c < n) atomicAdd(&h[mag_key(tprime<MODE>(xs[c], rs[c], alpha)) >> kSShift], 1u);
+    }
+  }
+  __syncthreads();
   uint32_t c[PER], loc = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
-    c[j] = ht[PER * threadIdx.x + j];
+    c[j] = h[PER * threadIdx.x + j];
     loc += c[j];
   }
   part[threadIdx.x] = loc;
@@ -169,8 +184,8 @@ __global__ __launch_bounds__(1024) void topk_threshold(const uint32_t* __restric
     __syncthreads();
   }
   const uint32_t S = part[0];
-  const double m = (double)kk[t] * (double)S / (double)max(tsize[t], (int64_t)1);
-  const double want = m + 5.0 * sqrt(m) + 25.0;
+  const double m = (double)kk[t] * (double)S / (double)max(n, (int64_t)1);
+  const double want = m + 6.0 * sqrt(m) + 32.0;
   if (m < 16.0 || want >= (double)S) {  // too few samples to trust: keep every element
     if (threadIdx.x == 0) tbin[t] = 0;
     return;
@@ -557,18 +572,16 @@ size_t sort_tmp_bytes(const omf_plan* p) {
 
 // Workspace: everything up to `zero_end` is cleared once per call.
 struct WsLayout {
-  size_t hist, shist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
+  size_t hist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
       item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes;
 };
 
 WsLayout layout(const omf_plan* p) {
   const int32_t nt = omf_plan_access::ntensors(p);
   const int64_t ae = omf_plan_access::arena_end(p);
-  const bool glob = global_path(p);
   WsLayout L;
   size_t o = 0;
   L.hist = o; o = align256(o + 4 * (size_t)nt * kBins);
-  L.shist = o; o = align256(o + (glob ? 4 * (size_t)nt * kSBins : 0));
   L.bin = o; o = align256(o + 4 * (size_t)nt);
   L.cnt = o; o = align256(o + 4 * (size_t)nt);
   L.flag = o; o = align256(o + 4 * (size_t)nt);
@@ -634,7 +647,6 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   hipStream_t st = (hipStream_t)stream;
   uint8_t* w = static_cast<uint8_t*>(ws);
   uint32_t* hist = reinterpret_cast<uint32_t*>(w + L.hist);
-  uint32_t* shist = reinterpret_cast<uint32_t*>(w + L.shist);
   uint32_t* bin = reinterpret_cast<uint32_t*>(w + L.bin);
   uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
   uint32_t* flag = reinterpret_cast<uint32_t*>(w + L.flag);
@@ -667,14 +679,14 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   const bool glob = global_path(plan);
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
-    const dim3 sgrid(kSBlocks, (unsigned)nt);
+    const dim3 sgrid((unsigned)nt), sblk(1024);
     if (residual_mode == 1) {
-      hipLaunchKernelGGL((topk_sample<1>), sgrid, blk, 0, st, x, residual, alpha, d_begins, d_sizes, shist);
-      hipLaunchKernelGGL(topk_threshold, dim3((unsigned)nt), dim3(1024), 0, st, shist, kk, d_sizes, tbin);
+      hipLaunchKernelGGL((topk_sample_threshold<1>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
+                         tbin);
       hipLaunchKernelGGL((topk_fused<1>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt, cand);
     } else {
-      hipLaunchKernelGGL((topk_sample<0>), sgrid, blk, 0, st, x, residual, alpha, d_begins, d_sizes, shist);
-      hipLaunchKernelGGL(topk_threshold, dim3((unsigned)nt), dim3(1024), 0, st, shist, kk, d_sizes, tbin);
+      hipLaunchKernelGGL((topk_sample_threshold<0>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
+                         tbin);
       if (residual_mode == 2)
         hipLaunchKernelGGL((topk_fused<2>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt,
                            cand);

@@ -119,12 +119,16 @@ def _fmix32(h):
 
 
 def _sample_positions(n, t):
-    """The elements omf_topk.hip's topk_sample reads for tensor t (one per max(256, n/32Ki))."""
-    stride = max(256, -(-n // 32768))
+    """The elements omf_topk.hip's topk_sample_threshold reads for tensor t: one aligned run
+    of 16 per max(256, n/4096) elements, at a hashed position."""
+    stride = max(256, -(-n // 4096))
     lo = np.arange(0, n, stride, dtype=np.uint64)
     key = lo ^ np.uint64((t * 0x9E3779B9) & 0xFFFFFFFF)
     span = np.minimum(np.uint64(stride), np.uint64(n) - lo)
-    return (lo + _fmix32(key) % span).astype(np.int64)
+    runs = np.maximum(np.uint64(1), span // np.uint64(16))
+    start = (lo + np.uint64(16) * (_fmix32(key) % runs)).astype(np.int64)
+    pos = (start[:, None] + np.arange(16)[None, :]).reshape(-1)
+    return pos[pos < n]
 
 
 @pytest.mark.parametrize("alpha", [1.0, 3.0])
@@ -161,7 +165,7 @@ def test_topk_sampled_threshold_redo(gpu):
     """A tensor whose sampled elements are exactly its largest: the sample puts the threshold
     above the k-th magnitude, the pass finds fewer than k candidates, and the tensor is redone
     exactly — the k largest, ties by ascending index."""
-    n = 1 << 20
+    n = 1 << 23  # 4096 runs of 16 = 64 Ki samples < k = 83886
     x = np.ones(n, np.float32)
     sp = _sample_positions(n, 1)
     x[sp] = 10.0
