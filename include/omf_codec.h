@@ -153,6 +153,24 @@ int omf_qsgd_decode(omf_plan* plan, const void* q, int32_t width, int32_t levels
 int omf_div_f32(float* y, int64_t n, float divisor, void* stream);
 
 /*
+ * Opt-in bit-packed QSGD wire (NOT reference-compatible, a new
+ * compression_type "QSGDBitPackedCompression" that replaces the int8/int32 values_data
+ * of _encode_qsgd_layer, global_grpc_compression.py:111-123, only when enabled).
+ * Level q in [-L, L] -> code q + L in b = omf_qsgd_packed_bits(L) = ceil(log2(2L+1))
+ * bits, LSB-first: element i of a tensor at bits [i*b, (i+1)*b) of its stream; tensor t's
+ * stream starts at 32-bit word offsets[t] * b / 32 of the packed arena, ceil(arena_end / 32) * b
+ * words (the plan's offsets are multiples of 64; 32 elements = b words, the last partial
+ * group of a tensor included, its padding packed as code 0).
+ * omf_qsgd_pack: payload (width 8 or 32, as omf_qsgd_encode wrote it) -> packed arena.
+ * omf_qsgd_decode_packed: y = fl32(fl32(norm * (code - L)) / L), bit-identical to
+ * omf_qsgd_decode of the unpacked payload (accumulate: y += that).
+ */
+int32_t omf_qsgd_packed_bits(int32_t levels);
+int omf_qsgd_pack(omf_plan* plan, const void* q, int32_t width, int32_t levels, uint32_t* packed, void* stream);
+int omf_qsgd_decode_packed(omf_plan* plan, const uint32_t* packed, int32_t levels, const float* norm, float* y,
+                           int32_t accumulate, void* stream);
+
+/*
  * Top-K sparsification with error feedback, all tensors of the plan in one call.
  * Replaces TopKCompression.compress (src/omnifed/hybrid/compression/topk.py:33-42)
  * with ResidualUpdates.compensate/update (src/omnifed/hybrid/compression/core.py:26-37)

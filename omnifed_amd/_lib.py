@@ -49,6 +49,9 @@ SIGNATURES = {
                                            _c_p]),
     "omf_qsgd_decode": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
     "omf_div_f32": (ctypes.c_int, [_c_p, _c_i64, _c_f32, _c_p]),
+    "omf_qsgd_packed_bits": (_c_i32, [_c_i32]),
+    "omf_qsgd_pack": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
+    "omf_qsgd_decode_packed": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
     "omf_topk_k": (_c_i64, [_c_i64, _c_f64]),
     "omf_topk_workspace_bytes": (_c_size, [_c_p, _c_f64]),
     "omf_topk_encode": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_f64, _c_f32, _c_p, _c_p, _c_p, _c_size, _c_p]),

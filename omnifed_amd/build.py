@@ -18,7 +18,7 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libomf_codec.so")
 
-SOURCES = ["omf_runtime.cpp", "omf_qsgd.hip", "omf_qsgd_ring.hip", "omf_topk.hip"]
+SOURCES = ["omf_runtime.cpp", "omf_qsgd.hip", "omf_qsgd_ring.hip", "omf_qsgd_pack.hip", "omf_topk.hip"]
 
 # Exact IEEE fp32 (no contraction, denormals kept, correctly rounded / and sqrt): the
 # payload must match the reference bit for bit.

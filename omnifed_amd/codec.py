@@ -37,6 +37,14 @@ def storage_width(levels: int) -> int:
     return 8 if levels <= 127 else 32
 
 
+def packed_bits(levels: int) -> int:
+    """Bits per element of the opt-in packed wire: ceil(log2(2 L + 1)) (omf_qsgd_packed_bits)."""
+    levels = int(levels)
+    if levels <= 0 or levels >= 2**31 - 1:
+        raise ValueError(f"invalid level={levels}")
+    return (2 * levels).bit_length()
+
+
 def _stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
@@ -277,6 +285,47 @@ class Plan:
         st = stream if stream is not None else _stream(dev)
         check(lib().omf_qsgd_decode(self._h, _ptr(q), width, levels, _ptr(norm), _ptr(y_out),
                                     1 if accumulate else 0, ctypes.c_void_p(st)), "omf_qsgd_decode")
+        return y_out
+
+    # ------------------------------------------------------------ bit-packed wire (opt-in)
+    def packed_words(self, levels: int) -> int:
+        """32-bit words of the packed arena: ceil(arena_end / 32) groups of 32 elements, b words
+        each (tensor t at word ``offsets[t] * b // 32``; the last tensor's partial group too)."""
+        return -(-self.arena_end // 32) * packed_bits(levels)
+
+    def qsgd_pack(self, q: torch.Tensor, width: int, levels: int, packed_out: Optional[torch.Tensor] = None,
+                  stream: Optional[int] = None) -> torch.Tensor:
+        """Levels (int8/int32 payload arena) -> codes ``q + L`` in ``packed_bits(L)`` bits (an int32
+        tensor holding the packed words)."""
+        width, levels = int(width), int(levels)
+        if width not in (8, 32):
+            raise ValueError(f"unsupported width={width}")
+        dev = self.device
+        _need(q, "q", torch.int8 if width == 8 else torch.int32, dev, self.arena_end, 16)
+        words = self.packed_words(levels)
+        if packed_out is None:
+            packed_out = torch.empty(max(words, 1), dtype=torch.int32, device=dev)
+        _need(packed_out, "packed_out", torch.int32, dev, words, 4)
+        st = stream if stream is not None else _stream(dev)
+        check(lib().omf_qsgd_pack(self._h, _ptr(q), width, levels, _ptr(packed_out), ctypes.c_void_p(st)),
+              "omf_qsgd_pack")
+        return packed_out
+
+    def qsgd_decode_packed(self, packed: torch.Tensor, levels: int, norm: torch.Tensor,
+                           y_out: Optional[torch.Tensor] = None, accumulate: bool = False,
+                           stream: Optional[int] = None) -> torch.Tensor:
+        levels = int(levels)
+        dev = self.device
+        _need(packed, "packed", torch.int32, dev, self.packed_words(levels), 4)
+        _need(norm, "norm", torch.float32, dev, self.nt, 4)
+        if y_out is None:
+            if accumulate:
+                raise ValueError("accumulate=True needs y_out")
+            y_out = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
+        _need(y_out, "y_out", torch.float32, dev, self.arena_end, 16)
+        st = stream if stream is not None else _stream(dev)
+        check(lib().omf_qsgd_decode_packed(self._h, _ptr(packed), levels, _ptr(norm), _ptr(y_out),
+                                           1 if accumulate else 0, ctypes.c_void_p(st)), "omf_qsgd_decode_packed")
         return y_out
 
     # ------------------------------------------------------------ Top-K

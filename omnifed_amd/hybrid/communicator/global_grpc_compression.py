@@ -28,6 +28,7 @@ import torch
 from . import global_grpc_pb2
 from ..compression.qsgd import (
     QSGD_COMPRESSION_NAME,
+    QSGD_PACKED_COMPRESSION_NAME,
     QSGDQuantCompression,
     choose_qsgd_storage_width,
     should_compress_tensor,
@@ -40,6 +41,7 @@ GlobalHybridCompressor = Union[TopKCompression, QSGDQuantCompression]
 
 _QSGD_NUMPY_DTYPES = {8: np.int8, 32: np.int32}
 _QSGD_TORCH_DTYPES = {8: torch.int8, 32: torch.int32}
+_QSGD_TYPES = (QSGD_COMPRESSION_NAME, QSGD_PACKED_COMPRESSION_NAME)
 
 
 class _PinnedStaging:
@@ -76,15 +78,16 @@ def compression_mode_name(compressor: Optional[GlobalHybridCompressor]) -> str:
 
 
 def build_global_compressor(*, enabled: bool, scheme: str = "topk", compress_ratio: float = 0.01,
-                            bit_width: int = 8, device="cpu") -> Optional[GlobalHybridCompressor]:
-    """global_grpc_compression.py:35-52."""
+                            bit_width: int = 8, device="cpu", packed_wire: bool = False) -> Optional[GlobalHybridCompressor]:
+    """global_grpc_compression.py:35-52.  ``packed_wire`` (QSGD only, default off): the opt-in
+    bit-packed wire (``QSGDBitPackedCompression``, not readable by the reference)."""
     if not enabled:
         return None
     scheme_norm = str(scheme).lower()
     if scheme_norm == "topk":
         return TopKCompression(device=device, compress_ratio=float(compress_ratio))
     if scheme_norm == "qsgd":
-        return QSGDQuantCompression(bit_width=int(bit_width), device=device)
+        return QSGDQuantCompression(bit_width=int(bit_width), device=device, packed_wire=bool(packed_wire))
     raise ValueError(f"Unsupported global_compression.scheme={scheme!r}; expected 'topk' or 'qsgd'")
 
 
@@ -118,8 +121,9 @@ def hybrid_global_compressor_from_cfg(cfg, device="cpu") -> Optional[GlobalHybri
     scheme = str(_select(cfg, "engine.hybrid.global_compression.scheme", "topk"))
     ratio = float(_select(cfg, "engine.hybrid.global_compression.compress_ratio", 0.01))
     bit_width = int(_select(cfg, "engine.hybrid.global_compression.bit_width", 8))
+    packed = bool(_select(cfg, "engine.hybrid.global_compression.packed_wire", False))  # opt-in, ours
     return build_global_compressor(enabled=enabled, scheme=scheme, compress_ratio=ratio, bit_width=bit_width,
-                                   device=device)
+                                   device=device, packed_wire=packed)
 
 
 # ---------------------------------------------------------------- layer builders (host)
@@ -147,6 +151,38 @@ def qsgd_layer_from_payload(name: str, shape, payload: bytes, norm: float, width
     return layer
 
 
+def qsgd_packed_layer_from_payload(name: str, shape, packed: bytes, norm: float, levels: int):
+    """The opt-in bit-packed QSGD ``LayerState``: the fields of the QSGD layer with
+    ``values_data`` = the codes q + L in ``width`` = ceil(log2(2L+1)) bits each, LSB first."""
+    layer = global_grpc_pb2.LayerState(layer_name=name)
+    layer.compression_type = QSGD_PACKED_COMPRESSION_NAME
+    layer.values_data = packed
+    bits = codec.packed_bits(levels)
+    layer.values_dtype = f"packed.u{bits}"
+    layer.original_shape.extend(list(shape))
+    layer.meta_tensor = np.array([float(norm)], dtype=np.float32).tobytes()
+    layer.meta_tensor_dtype = "torch.float32"
+    layer.width = bits
+    layer.level = int(levels)
+    return layer
+
+
+def _packed_host(plan, q: torch.Tensor, width: int, levels: int) -> np.ndarray:
+    """Pack a device payload arena and fetch it (one D2H through pinned staging); tensor t's
+    bytes start at ``plan.offsets[t] * b // 8``."""
+    packed = plan.qsgd_pack(q, width, levels)
+    staged = _STAGING.get("encode", packed.numel() * 4).view(torch.int32)
+    staged.copy_(packed, non_blocking=True)
+    torch.cuda.current_stream(q.device).synchronize()
+    return staged.numpy().view(np.uint8)
+
+
+def _packed_slice(host: np.ndarray, offset: int, n: int, levels: int) -> bytes:
+    b = codec.packed_bits(levels)
+    start = offset * b // 8
+    return host[start:start + (n * b + 7) // 8].tobytes()
+
+
 def topk_layer_from_payload(name: str, shape, values: np.ndarray, indices: np.ndarray):
     """The Top-K ``LayerState`` of global_grpc_compression.py:88-98."""
     layer = global_grpc_pb2.LayerState(layer_name=name)
@@ -169,6 +205,8 @@ def _encode_qsgd_layer(name: str, tensor: torch.Tensor, compressor: QSGDQuantCom
     """global_grpc_compression.py:101-123, payload produced on the GPU."""
     if not should_compress_tensor(tensor):
         return _encode_dense_layer(name, tensor)
+    if getattr(compressor, "packed_wire", False):
+        return encode_updates_dict({name: tensor}, compressor)[0]
     (q, norm, width, levels), = compressor.encode_flat([tensor.detach().reshape(-1)])
     if width == -1:
         return _encode_dense_layer(name, tensor)
@@ -245,8 +283,32 @@ def _check_qsgd_layer(layer):
         raise ValueError(f"cannot reshape QSGD payload of {len(layer.values_data)} bytes into {tuple(layer.original_shape)}")
 
 
+def _check_packed_layer(layer):
+    """The packed layer's fields, checked like _check_qsgd_layer checks the reference's."""
+    if not layer.values_data:
+        raise ValueError(f"QSGD layer {layer.layer_name!r} missing values_data")
+    if not layer.meta_tensor:
+        raise ValueError(f"QSGD layer {layer.layer_name!r} missing meta_tensor (norm)")
+    if layer.level <= 0:
+        raise ValueError(f"QSGD layer {layer.layer_name!r} has invalid level={layer.level}")
+    if layer.width != codec.packed_bits(layer.level):
+        raise ValueError(f"QSGD layer {layer.layer_name!r} has unsupported width={layer.width}")
+    n = int(np.prod(tuple(layer.original_shape)))
+    if len(layer.values_data) != (n * layer.width + 7) // 8:
+        raise ValueError(f"cannot reshape packed QSGD payload of {len(layer.values_data)} bytes into "
+                         f"{tuple(layer.original_shape)}")
+
+
 def _decode_qsgd_layer(layer, *, device=None) -> torch.Tensor:
     """global_grpc_compression.py:163-182, decoded on the GPU."""
+    if layer.compression_type == QSGD_PACKED_COMPRESSION_NAME:
+        _check_packed_layer(layer)
+        shape = tuple(layer.original_shape)
+        out_dev = _out_device(None, device)
+        if int(np.prod(shape)) == 0:
+            return torch.zeros(shape, dtype=torch.float32, device=out_dev)
+        y, plan = _decode_qsgd_batch([layer], _gpu_for(out_dev))
+        return y[:plan.sizes[0]].reshape(shape).to(out_dev)
     _check_qsgd_layer(layer)
     shape = tuple(layer.original_shape)
     n = int(np.prod(shape))
@@ -274,7 +336,7 @@ def decode_layer_tensor(layer, *, base_tensor: Optional[torch.Tensor] = None, de
         return out if device is None else out.to(device)
     if compression_type == TOPK_COMPRESSION_NAME:
         return _decode_topk_layer(layer, base_tensor=base_tensor, device=device)
-    if compression_type == QSGD_COMPRESSION_NAME:
+    if compression_type in _QSGD_TYPES:
         return _decode_qsgd_layer(layer, device=device)
     raise ValueError(f"Unsupported compression_type={compression_type!r}")
 
@@ -298,13 +360,20 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
         plan, q, norms = encode_many(flats, compressor.s, dev, compressor.rng, compressor._next_call())
         levels = 2**compressor.s
         width, _ = choose_qsgd_storage_width(levels)
-        staged = _STAGING.get("encode", q.numel() * q.element_size()).view(q.dtype)
-        staged.copy_(q, non_blocking=True)  # one D2H of the payload arena (w bytes per element)
-        host_norms = norms.cpu().tolist()  # synchronises the stream: the payload copy has landed
-        q_host = staged.numpy()
-        for i, o, n, nv in zip(comp_idx, plan.offsets, plan.sizes, host_norms):
-            if nv != 0:
-                results[i] = (q_host[o:o + n].tobytes(), nv)
+        if compressor.packed_wire:  # pack on the GPU; (b/8) bytes per element cross PCIe
+            p_host = _packed_host(plan, q, width, levels)
+            host_norms = norms.cpu().tolist()
+            for i, o, n, nv in zip(comp_idx, plan.offsets, plan.sizes, host_norms):
+                if nv != 0:
+                    results[i] = (_packed_slice(p_host, o, n, levels), nv)
+        else:
+            staged = _STAGING.get("encode", q.numel() * q.element_size()).view(q.dtype)
+            staged.copy_(q, non_blocking=True)  # one D2H of the payload arena (w bytes per element)
+            host_norms = norms.cpu().tolist()  # synchronises the stream: the payload copy has landed
+            q_host = staged.numpy()
+            for i, o, n, nv in zip(comp_idx, plan.offsets, plan.sizes, host_norms):
+                if nv != 0:
+                    results[i] = (q_host[o:o + n].tobytes(), nv)
     layers = []
     for i, name in enumerate(names):
         t = updates[name]
@@ -312,7 +381,10 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
             payload, nv = results[i]
             levels = 2**compressor.s
             width, _ = choose_qsgd_storage_width(levels)
-            layers.append(qsgd_layer_from_payload(name, tuple(t.shape), payload, nv, width, levels))
+            if compressor.packed_wire:
+                layers.append(qsgd_packed_layer_from_payload(name, tuple(t.shape), payload, nv, levels))
+            else:
+                layers.append(qsgd_layer_from_payload(name, tuple(t.shape), payload, nv, width, levels))
         else:
             layers.append(_encode_dense_layer(name, t))
     return layers
@@ -326,9 +398,23 @@ def _decode_qsgd_batch(layers, dev: torch.device):
     and the plan (layer i at ``[plan.offsets[i], + plan.sizes[i])``).
     """
     width, level = layers[0].width, layers[0].level
-    np_dt = _QSGD_NUMPY_DTYPES[width]
     sizes = [max(int(np.prod(tuple(L.original_shape))), 1) for L in layers]
     plan = codec.Plan.get(sizes, device=dev)
+    if layers[0].compression_type == QSGD_PACKED_COMPRESSION_NAME:  # tensor t at byte offsets[t] * b / 8
+        words = plan.packed_words(level)
+        hostb = _STAGING.get("decode", words * 4).numpy()
+        norms = np.zeros(plan.nt, dtype=np.float32)
+        for i, (L, o) in enumerate(zip(layers, plan.offsets)):
+            start = o * width // 8
+            hostb[start:start + len(L.values_data)] = np.frombuffer(L.values_data, dtype=np.uint8)
+            norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
+        pd = torch.empty(words, dtype=torch.int32, device=dev)
+        pd.copy_(torch.from_numpy(hostb).view(torch.int32), non_blocking=True)
+        nd = torch.from_numpy(norms).to(dev, non_blocking=False)
+        y = plan.qsgd_decode_packed(pd, level, nd)
+        torch.cuda.current_stream(dev).synchronize()
+        return y, plan
+    np_dt = _QSGD_NUMPY_DTYPES[width]
     itemsize = np.dtype(np_dt).itemsize
     host = _STAGING.get("decode", plan.arena_end * itemsize).numpy().view(np_dt)
     norms = np.zeros(plan.nt, dtype=np.float32)
@@ -357,17 +443,19 @@ def _validate_layer(layer):
             raise ValueError(f"Compressed layer {layer.layer_name!r} missing values/indices")
     elif ct == QSGD_COMPRESSION_NAME:
         _check_qsgd_layer(layer)
+    elif ct == QSGD_PACKED_COMPRESSION_NAME:
+        _check_packed_layer(layer)
     else:
         raise ValueError(f"Unsupported compression_type={ct!r}")
 
 
 def _qsgd_groups(proto_layers):
-    """Validate every layer in message order; QSGD layers grouped by (width, level)."""
+    """Validate every layer in message order; QSGD layers grouped by (type, width, level)."""
     groups: Dict[tuple, list] = {}
     for L in proto_layers:
         _validate_layer(L)
-        if L.compression_type == QSGD_COMPRESSION_NAME:
-            groups.setdefault((L.width, L.level), []).append(L)
+        if L.compression_type in _QSGD_TYPES:
+            groups.setdefault((L.compression_type, L.width, L.level), []).append(L)
     return groups
 
 
@@ -392,7 +480,7 @@ def decode_updates_dict(proto_layers, *, base_updates: Optional[Dict[str, torch.
                 decoded[L.layer_name] = y[o:o + n].view(tuple(L.original_shape))
     out: Dict[str, torch.Tensor] = {}
     for layer in proto_layers:
-        if layer.layer_name in decoded and layer.compression_type == QSGD_COMPRESSION_NAME:
+        if layer.layer_name in decoded and layer.compression_type in _QSGD_TYPES:
             out[layer.layer_name] = decoded[layer.layer_name]
             continue
         base = None if base_updates is None else base_updates.get(layer.layer_name)
@@ -417,7 +505,7 @@ def decode_updates_into(proto_layers, targets: Dict[str, torch.Tensor]) -> None:
             t = targets[L.layer_name]
             t.copy_(y[o:o + n].view(tuple(L.original_shape)).to(t.dtype))
     for L in proto_layers:
-        if L.compression_type == QSGD_COMPRESSION_NAME:
+        if L.compression_type in _QSGD_TYPES:
             continue
         t = targets[L.layer_name]
         dec = decode_layer_tensor(L, base_tensor=t, device=t.device)
@@ -435,5 +523,6 @@ __all__: List[str] = [
     "encode_updates_dict",
     "hybrid_global_compressor_from_cfg",
     "qsgd_layer_from_payload",
+    "qsgd_packed_layer_from_payload",
     "topk_layer_from_payload",
 ]

@@ -6,7 +6,7 @@ from .core import (
     ResidualUpdates,
     layerwise_decompress,
 )
-from .qsgd import QSGD_COMPRESSION_NAME, QSGDQuantCompression
+from .qsgd import QSGD_COMPRESSION_NAME, QSGD_PACKED_COMPRESSION_NAME, QSGDQuantCompression
 from .topk import TOPK_COMPRESSION_NAME, TopKCompression
 
 __all__ = [
@@ -17,5 +17,6 @@ __all__ = [
     "TOPK_COMPRESSION_NAME",
     "QSGDQuantCompression",
     "QSGD_COMPRESSION_NAME",
+    "QSGD_PACKED_COMPRESSION_NAME",
     "layerwise_decompress",
 ]

@@ -29,6 +29,9 @@ from ... import codec
 from .core import Compression, compute_device, to_arena
 
 QSGD_COMPRESSION_NAME = "QSGDQuantCompression"
+# Opt-in bit-packed wire (not reference-compatible): codes q + L in
+# ceil(log2(2L+1)) bits instead of int8/int32 levels (include/omf_codec.h omf_qsgd_pack).
+QSGD_PACKED_COMPRESSION_NAME = "QSGDBitPackedCompression"
 
 
 def should_compress_tensor(x: torch.Tensor) -> bool:
@@ -79,9 +82,10 @@ def encode_many(flats: Sequence[torch.Tensor], bit_width: int, dev: torch.device
 class QSGDQuantCompression(Compression):
     """QSGD (Alistarh et al., 2017), Algorithm 1 — on the GPU."""
 
-    def __init__(self, bit_width: int = 8, device="cpu", rng: str = "philox"):
+    def __init__(self, bit_width: int = 8, device="cpu", rng: str = "philox", packed_wire: bool = False):
         super().__init__()
         self.s = int(bit_width)
+        self.packed_wire = bool(packed_wire)  # encode_updates_dict / encode_layer_state emit packed layers
         self.device = torch.device(device)
         if rng not in ("philox", "mt19937"):
             raise ValueError(f"unknown rng={rng!r}; expected 'philox' or 'mt19937'")
