@@ -74,57 +74,69 @@ __global__ __launch_bounds__(kThreads) void qsgd_pack(const void* __restrict__ q
   }
 }
 
+// Decode: each thread unpacks its 32 elements (b words), then the workgroup transposes
+// through LDS (33-word rows: conflict-free both ways) so the fp32 stores are lane-contiguous
+// 16-byte non-temporal stores, like qsgd_decode_flat's.
 template <int B, bool ACC, bool POW2>
 __global__ __launch_bounds__(kThreads) void qsgd_decode_packed(const uint32_t* __restrict__ packed,
                                                                const Item* __restrict__ items,
                                                                const float* __restrict__ norm, float* __restrict__ y,
                                                                int32_t L, int32_t b_rt, float levels, float inv_levels) {
+  constexpr int G = 32 * kThreads;  // elements per pass
+  __shared__ float tile[kThreads * 33];
   const int b = B ? B : b_rt;
   const Item it = items[blockIdx.x];
   const float nrm = norm[it.tensor];
   const uint64_t mask = (1ull << b) - 1ull;
-  for (int64_t e0 = it.begin + 32 * (int64_t)threadIdx.x; e0 < it.end; e0 += 32 * (int64_t)kThreads) {
-    const int nv = (int)min((int64_t)32, it.end - e0);
-    const uint32_t* p = packed + (e0 >> 5) * (int64_t)b;
-    uint32_t wd[B ? B : 32];
-    if (B) {
+  for (int64_t base = it.begin; base < it.end; base += G) {
+    const int64_t e0 = base + 32 * (int64_t)threadIdx.x;
+    if (e0 < it.end) {
+      const uint32_t* p = packed + (e0 >> 5) * (int64_t)b;
+      uint32_t wd[B ? B : 32];
+      if (B) {
 #pragma unroll
-      for (int i = 0; i < (B ? B : 1); ++i) wd[i] = p[i];  // every word up front
-    } else {
-      for (int i = 0; i < b; ++i) wd[i] = p[i];
-    }
-    float yv[32];
-    uint64_t acc = 0;
-    int nb = 0, w = 0;
-#pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      if (nb < b) {
-        acc |= (uint64_t)wd[w++] << nb;
-        nb += 32;
+        for (int i = 0; i < (B ? B : 1); ++i) wd[i] = p[i];  // every word up front
+      } else {
+        for (int i = 0; i < b; ++i) wd[i] = p[i];
       }
-      const int32_t qi = (int32_t)(acc & mask) - L;
-      acc >>= b;
-      nb -= b;
-      const float nq = __fmul_rn(nrm, (float)qi);  // qsgd_decode_flat's arithmetic
-      yv[i] = POW2 ? __fmul_rn(nq, inv_levels) : nq / levels;
-    }
-    float* yo = y + e0;
-    if (nv == 32) {
+      uint64_t acc = 0;
+      int nb = 0, w = 0;
 #pragma unroll
-      for (int v = 0; v < 8; ++v) {
-        float4 o = make_float4(yv[4 * v], yv[4 * v + 1], yv[4 * v + 2], yv[4 * v + 3]);
+      for (int i = 0; i < 32; ++i) {
+        if (nb < b) {
+          acc |= (uint64_t)wd[w++] << nb;
+          nb += 32;
+        }
+        const int32_t qi = (int32_t)(acc & mask) - L;
+        acc >>= b;
+        nb -= b;
+        const float nq = __fmul_rn(nrm, (float)qi);  // qsgd_decode_flat's arithmetic
+        tile[threadIdx.x * 33 + i] = POW2 ? __fmul_rn(nq, inv_levels) : nq / levels;
+      }
+    }
+    __syncthreads();
+    const int64_t lim = min((int64_t)G, it.end - base);
+#pragma unroll
+    for (int v = 0; v < 8; ++v) {
+      const int e = 4 * (v * kThreads + (int)threadIdx.x);  // element of this pass
+      if (e >= lim) continue;
+      float f[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) f[c] = tile[((e + c) >> 5) * 33 + ((e + c) & 31)];
+      float* yo = y + base + e;
+      if (e + 4 <= lim) {
+        float4 o = make_float4(f[0], f[1], f[2], f[3]);
         if (ACC) {
-          const float4 prev = *reinterpret_cast<const float4*>(yo + 4 * v);
+          const float4 prev = *reinterpret_cast<const float4*>(yo);
           o.x = __fadd_rn(prev.x, o.x); o.y = __fadd_rn(prev.y, o.y);
           o.z = __fadd_rn(prev.z, o.z); o.w = __fadd_rn(prev.w, o.w);
         }
-        store_nt(yo + 4 * v, o);
+        store_nt(yo, o);
+      } else {
+        for (int c = 0; c < 4 && e + c < lim; ++c) yo[c] = ACC ? __fadd_rn(yo[c], f[c]) : f[c];
       }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 32; ++i)
-        if (i < nv) yo[i] = ACC ? __fadd_rn(yo[i], yv[i]) : yv[i];
     }
+    __syncthreads();  // the tile is rewritten by the next pass
   }
 }
 

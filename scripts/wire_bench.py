@@ -66,6 +66,18 @@ res["ps_fused_apply_encode_ms"] = tm(lambda: plan.ps_apply_encode(acc, 40.0, 4, 
 res["ps_divide_then_encode_ms"] = tm(separate, reps=10) * 1e3
 res["ps_fused_apply_encode_ms"] = round(res["ps_fused_apply_encode_ms"], 4)
 res["ps_divide_then_encode_ms"] = round(res["ps_divide_then_encode_ms"], 4)
+# opt-in bit-packed wire (s = 4: 6 bits per element instead of 8)
+pcomp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev, packed_wire=True)
+players = encode_updates_dict(upd, pcomp)
+res["packed_encode_updates_dict_ms"] = round(tm(lambda: encode_updates_dict(upd, pcomp)) * 1e3, 2)
+res["packed_decode_updates_dict_gpu_ms"] = round(tm(lambda: decode_updates_dict(players, device=dev)) * 1e3, 2)
+res["packed_wire_bytes"] = sum(len(L.values_data) for L in players)
+res["int8_wire_bytes"] = sum(len(L.values_data) for L in layers)
+qq, nn = plan.qsgd_encode(acc, 4, seed=1)
+pk = plan.qsgd_pack(qq, 8, 16)
+res["device_pack_ms"] = round(tm(lambda: plan.qsgd_pack(qq, 8, 16, packed_out=pk), reps=10) * 1e3, 4)
+res["device_decode_packed_ms"] = round(tm(lambda: plan.qsgd_decode_packed(pk, 16, nn, y_out=avg), reps=10) * 1e3, 4)
+res["device_decode_int8_ms"] = round(tm(lambda: plan.qsgd_decode(qq, 8, 16, nn, y_out=avg), reps=10) * 1e3, 4)
 for k in ("encode_updates_dict_ms", "decode_updates_dict_gpu_ms", "decode_updates_into_ms",
           "decode_updates_dict_cpu_ms"):
     res[k.replace("_ms", "_fp32_GBs")] = round(4 * N / (res[k] * 1e-3) / 1e9, 2)
