@@ -47,8 +47,10 @@ struct Divisor {
     const f32x2_t lo = div2_markstein((f32x2_t){x.x, x.y}, D, R);
     const f32x2_t hi = div2_markstein((f32x2_t){x.z, x.w}, D, R);
     float4 q = make_float4(lo.x, lo.y, hi.x, hi.y);
-    const int need = (int)div_tiny(x.x) | (int)div_tiny(x.y) | (int)div_tiny(x.z) | (int)div_tiny(x.w);
-    if (__any(need)) {  // wave-uniform branch: tiny inputs take the exact division
+    // Quad pre-test (v_min3 with |.| modifiers): min |x| < 2^-96 catches every tiny input
+    // (and zeros, which Markstein divides exactly anyway); only then the per-element test.
+    const float mn = fminf(fminf(fabsf(x.x), fabsf(x.y)), fminf(fabsf(x.z), fabsf(x.w)));
+    if (__any(mn < 0x1p-96f)) {  // wave-uniform branch: tiny inputs take the exact division
       if (div_tiny(x.x)) q.x = x.x / d;
       if (div_tiny(x.y)) q.y = x.y / d;
       if (div_tiny(x.z)) q.z = x.z / d;
