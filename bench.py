@@ -48,9 +48,11 @@ def parse():
 def init_dist(n):
     if n <= 1 and "RANK" not in os.environ:
         return 0, 1, 0
-    dist.init_process_group(backend="nccl")
+    # the rank's GPU first: RCCL binds its communicator (and barrier) to the current device
+    local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
+    torch.cuda.set_device(local)
+    dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
     rank, world = dist.get_rank(), dist.get_world_size()
-    local = int(os.environ.get("LOCAL_RANK", rank))
     return rank, world, local
 
 
@@ -276,7 +278,7 @@ def main():
             **extras,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
