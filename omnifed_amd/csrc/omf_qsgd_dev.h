@@ -79,7 +79,9 @@ __device__ __forceinline__ int32_t qsgd_level(float vn, float L, float u) {
 }
 
 // Four levels of x (already scaled by alpha) with uniforms u.  `zero`: norm == 0 (all-zero
-// payload; the Python layer sends the tensor dense, qsgd.py:47-48).
+// payload; the Python layer sends the tensor dense, qsgd.py:47-48).  CHECK_BIG = false only
+// where the norm is the encoder's own (|x| <= norm, so |vn| * L cannot reach 2^63).
+template <bool CHECK_BIG = true>
 __device__ __forceinline__ void qsgd_quad(float4 x, float4 u, const Divisor& dv, float L, bool zero,
                                           int32_t (&q)[4]) {
   if (zero) {
@@ -91,6 +93,7 @@ __device__ __forceinline__ void qsgd_quad(float4 x, float4 u, const Divisor& dv,
   q[1] = qsgd_level_fast(vn.y, L, u.y);
   q[2] = qsgd_level_fast(vn.z, L, u.z);
   q[3] = qsgd_level_fast(vn.w, L, u.w);
+  if (!CHECK_BIG) return;
   // |vn| * L >= 2^63 (only with a caller-supplied norm far below |x|): the reference's
   // int64 conversion overflows to INT64_MIN and clamps to 0.  One test per quad.
   const float big = fmaxf(fmaxf(fabsf(vn.x), fabsf(vn.y)), fmaxf(fabsf(vn.z), fabsf(vn.w)));

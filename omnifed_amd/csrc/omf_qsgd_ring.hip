@@ -83,14 +83,14 @@ __device__ __forceinline__ void philox_group(const Args& a, uint64_t G, int32_t 
   for (int sl = 0; sl < 4; ++sl) uu[sl] = u24x4(w[3 * sl], w[3 * sl + 1], w[3 * sl + 2]);
 }
 
-// Quantise and store rows 4rg .. 4rg+3 at lane position j (float4 j of each row) of the
-// chunk [cb, ce) of tensor `tensor` (chunk offset coff within it); w = those four float4,
-// already scaled by alpha.  Philox group G = (coff/4096 + rg)*256 + j (oracle/philox.py).
-template <int WIDTH, bool HAS_U>
-__device__ __forceinline__ void quant_group_at(const Args& a, const float4 (&w)[4], int rg, int j, int64_t cb,
-                                               int64_t ce, int64_t coff, int32_t tensor, float norm, bool full) {
+// Uniforms for rows 4rg .. 4rg+3 at lane position j of the chunk [cb, ce) of tensor
+// `tensor` (chunk offset coff within it): caller draws (parity mode) or Philox group
+// G = (coff/4096 + rg)*256 + j (oracle/philox.py).  Independent of the norm, so a claimer
+// draws them while the norm is still being resolved.
+template <bool HAS_U>
+__device__ __forceinline__ void draws_at(const Args& a, int rg, int j, int64_t cb, int64_t ce, int64_t coff,
+                                         int32_t tensor, bool full, float4 (&uu)[4]) {
   const int n = (int)(ce - cb);
-  float4 uu[4];
   if (HAS_U) {
     const float* __restrict__ ub = a.u + cb;
 #pragma unroll
@@ -111,36 +111,6 @@ __device__ __forceinline__ void quant_group_at(const Args& a, const float4 (&w)[
 #else
     philox_group(a, ((uint64_t)(coff >> 12) + (uint64_t)rg) * 256u + (uint64_t)j, tensor, uu);
 #endif
-  }
-  const bool zero = !(norm != 0.0f);  // norm == 0: all-zero payload (reference: dense passthrough)
-  const Divisor dv(norm);
-#pragma unroll
-  for (int sl = 0; sl < 4; ++sl) {
-    const int e = (4 * rg + sl) * 1024 + 4 * j;
-    if (!full && e >= n) continue;
-    int32_t qq[4];
-    qsgd_quad(w[sl], uu[sl], dv, a.levels, zero, qq);
-    const int32_t q0 = qq[0], q1 = qq[1], q2 = qq[2], q3 = qq[3];
-    if (WIDTH == 1) {
-      int8_t* q8 = reinterpret_cast<int8_t*>(a.q) + cb;
-      if (full || e + 4 <= n) {
-        const uint32_t pk = pack_i8x4(qq);
-        if (!(a.dbg & 8) || pk == 0x7f7f7f7fu) store_nt(reinterpret_cast<uint32_t*>(q8 + e), pk);
-      } else {
-        q8[e] = (int8_t)q0;
-        if (e + 1 < n) q8[e + 1] = (int8_t)q1;
-        if (e + 2 < n) q8[e + 2] = (int8_t)q2;
-      }
-    } else {
-      int32_t* q32 = reinterpret_cast<int32_t*>(a.q) + cb;
-      if (full || e + 4 <= n) {
-        store_nt(q32 + e, make_int4(q0, q1, q2, q3));
-      } else {
-        q32[e] = q0;
-        if (e + 1 < n) q32[e + 1] = q1;
-        if (e + 2 < n) q32[e + 2] = q2;
-      }
-    }
   }
 }
 
@@ -184,6 +154,31 @@ __device__ __forceinline__ void st_levels(__amdgpu_buffer_rsrc_t r, int eoff, in
 }
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t payload_rsrc(const Args& a, int width, int64_t begin, int64_t n) {
   return chunk_rsrc(static_cast<int8_t*>(a.q) + begin * width, width == 1 ? (n + 3) & ~int64_t(3) : 4 * n);
+}
+
+// Quantise and store rows 4rg .. 4rg+3 at lane position j of the chunk [cb, ce); w = those
+// four float4, already scaled by alpha; uu = their uniforms (draws_at).  The payload goes
+// through a range-checked chunk descriptor, so a tensor's partial last chunk needs no
+// per-row guard (its out-of-range elements were loaded as zeros and quantise to 0).  The
+// norm is always this launch's own (never caller-supplied): |x| <= norm, so |vn| * L stays
+// far below 2^63 and qsgd_quad's overflow test is skipped.
+template <int WIDTH>
+__device__ __forceinline__ void quant_group_at(const Args& a, const float4 (&w)[4], const float4 (&uu)[4], int rg,
+                                               int j, int64_t cb, int64_t ce, const Divisor& dv, bool zero) {
+  const __amdgpu_buffer_rsrc_t r = payload_rsrc(a, WIDTH, cb, ce - cb);
+  const int eoff = 4 * rg * 1024 + 4 * j;
+  if (zero) {  // tile-uniform: keeps the flag out of the per-row code
+    const int32_t qz[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int sl = 0; sl < 4; ++sl) st_levels<WIDTH>(r, eoff, sl, qz);
+    return;
+  }
+#pragma unroll
+  for (int sl = 0; sl < 4; ++sl) {
+    int32_t qq[4];
+    qsgd_quad<false>(w[sl], uu[sl], dv, a.levels, false, qq);
+    st_levels<WIDTH>(r, eoff, sl, qq);
+  }
 }
 
 // One Philox group of the register-resident kernel: rows 4rg .. 4rg+3 at float4 column j,
@@ -389,24 +384,28 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
     const bool full = it.end - it.begin == CH;
     const int64_t coff = it.begin - it.tbegin;
     float norm = 0.0f;
+    Divisor dv(1.0f);
     bool have_norm = false;
     for (;;) {
       const uint32_t c = (uint32_t)ufirst((int)(lane == 0 ? lds_add(&tclaim[s], 1u) : 0u)) - base;
       if (c >= (uint32_t)NTL) break;
+      const int rg = (int)(c >> 2), j = 64 * (int)(c & 3) + lane;
+      float4 uu[4];
+      if (!(a.dbg & 2)) draws_at<HAS_U>(a, rg, j, it.begin, it.end, coff, it.tensor, full, uu);
       if (!have_norm) {  // a tile is held, so the slot cannot be recycled under us
         const uint64_t c2 = __builtin_readcyclecounter();
         lds_wait_ge(&qready[s], (uint32_t)(k + 1));
         norm = ufirst(qnorm[s]);
+        dv = Divisor(norm);
         have_norm = true;
         prof.add(4, __builtin_readcyclecounter() - c2);
       }
       const uint64_t c3 = __builtin_readcyclecounter();
-      const int rg = (int)(c >> 2), j = 64 * (int)(c & 3) + lane;
       if (!(a.dbg & 2)) {
         float4 w4[4];
 #pragma unroll
         for (int sl = 0; sl < 4; ++sl) w4[sl] = slots[s][(4 * rg + sl) * 256 + j];
-        quant_group_at<WIDTH, HAS_U>(a, w4, rg, j, it.begin, it.end, coff, it.tensor, norm, full);
+        quant_group_at<WIDTH>(a, w4, uu, rg, j, it.begin, it.end, dv, !(norm != 0.0f));
       }
       lds_drain();
       const uint32_t d = ufirst((int)(lane == 0 ? lds_add(&tfin[s], 1u) : 0u));
@@ -643,7 +642,10 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
       for (int q = 0; q < S; ++q)
         if (q == s) use = uses[q]++;
       const uint64_t c0 = __builtin_readcyclecounter();
-      lds_wait_ge(&loaded[s], (uint32_t)(k + 1));
+      // Claim before the chunk has landed: the first tile's draws are computed while the
+      // slot fills and the norm resolves (the data is read only after qready, which the
+      // poller sets after `loaded`, which the loaders set after every tile of the slot's
+      // previous use is finished).
       lds_wait_ge(&tclaim[s], PER_USE * use);  // every claimer has left the slot's previous use
       prof.add(2, __builtin_readcyclecounter() - c0);
       claim_tiles(s, use, k, it);
