@@ -1,19 +1,25 @@
 #!/usr/bin/env python3
 """Benchmark: device-resident QSGD encode+decode of Llama-400M gradients (BASELINE.json metric).
 
-One step = encode (omf_qsgd_encode: norms + stochastic levels + int8 payload, one launch)
-+ decode (omf_qsgd_decode, one launch) of one client's full Llama-400M update arena
-(183 tensors, 401 122 304 fp32 elements, synthetic N(0,1)*1e-3, random-init shapes),
-bit_width 4 (16 levels, int8 wire — the presets' value), on-device Philox draws.
-Inputs are resident in HBM before timing starts.
+One step = encode (omf_qsgd_encode: norms + stochastic levels + int8 payload, one launch,
+the client weighting ``param * batch_samples`` fused as alpha) + decode (omf_qsgd_decode,
+one launch) of one client's full Llama-400M update arena (183 tensors, 401 122 304 fp32
+elements, synthetic N(0,1)*1e-3, random-init shapes), bit_width 4 (16 levels, int8 wire —
+the presets' value), on-device Philox draws.  Inputs are resident in HBM before timing.
 
 value = algorithmic bytes of all ranks / time, algorithmic bytes per step = (8 + 2w)·N
 (encode reads 4N, writes wN; decode reads wN, writes 4N).
 
+The same line carries a ``topk`` object: the Top-K codec (k = 1 % per tensor, error
+feedback, weighting fused) on the same arena, algorithmic bytes 16N + 24k per step
+(§8d), with its own roofline and CPU baseline.  ``--codec topk`` makes Top-K the line.
+
   python bench.py [--gpus N --steps K --warmup W --config llama400m --bits 4]
-  N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+  N > 1: either the driver's torchrun (RANK/WORLD_SIZE set) or ``python bench.py --gpus N``,
+  which spawns the N rank processes itself (before anything touches a GPU).
 Each rank is one synthetic client (weak scaling).  For N > 1 the PS weighted sum over
-RCCL is timed after the codec steps and reported beside the metric.
+RCCL (Σ decode(Q(w_i x_i)) / Σ w_i) and the Top-K sparse aggregate are timed after the
+codec steps and reported beside the metric.
 """
 
 from __future__ import annotations
@@ -21,13 +27,15 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
+import sys
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 METRIC = "GB/s device-resident QSGD encode+decode, Llama-400M grads, 1/2/4/8 GPUs"
+METRIC_TOPK = "GB/s device-resident Top-K k=1% encode+decode (error feedback), Llama-400M grads, 1/2/4/8 GPUs"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -39,82 +47,197 @@ def parse():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="llama400m")
     ap.add_argument("--bits", type=int, default=4)
+    ap.add_argument("--ratio", type=float, default=0.01)
+    ap.add_argument("--codec", choices=("qsgd", "topk"), default="qsgd")
     ap.add_argument("--chunk", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-topk", action="store_true", help="skip the Top-K object of the QSGD line")
     ap.add_argument("--no-extras", action="store_true", help="skip PCIe-inclusive and PS timings")
     return ap.parse_args()
 
 
-def init_dist(n):
-    if n <= 1 and "RANK" not in os.environ:
+# ---------------------------------------------------------------- launch
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script (one per GPU)
+    and return the first non-zero exit code.  Nothing here touches a GPU."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    codes = [p.wait() for p in procs]
+    return next((c for c in codes if c != 0), 0)
+
+
+def init_dist(torch, dist):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world <= 1:
         return 0, 1, 0
     # the rank's GPU first: RCCL binds its communicator (and barrier) to the current device
     local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
     torch.cuda.set_device(local)
     dist.init_process_group(backend="nccl", device_id=torch.device("cuda", local))
-    rank, world = dist.get_rank(), dist.get_world_size()
-    return rank, world, local
+    return dist.get_rank(), dist.get_world_size(), local
 
 
-def barrier(world):
-    if world > 1:
-        dist.barrier()
+# ---------------------------------------------------------------- CPU baseline
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
-def max_over_ranks(v, world, dev):
-    if world == 1:
-        return v
-    t = torch.tensor([v], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+def stratified_sample(named, budget):
+    """Every k-th tensor of the arena (a representative mix of shapes) up to ``budget`` elements."""
+    sizes = [int(np.prod(s)) for _, s in named]
+    stride = max(1, int(np.ceil(sum(sizes) / budget)))
+    picked = [i for i in range(0, len(sizes), stride)]
+    while sum(sizes[i] for i in picked) > budget and len(picked) > 1:
+        picked.pop(int(np.argmax([sizes[i] for i in picked])))
+    return picked, sizes
 
 
-def cpu_baseline(named, bits, budget_elems=100_000_000):
-    """Reference-equivalent CPU codec (oracle, kind 'port') on a bounded sample of the same workload."""
+def _median_time(fn, reps=5):
+    fn()  # warm-up
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def cpu_baseline(torch, named, bits, budget=40_000_000):
+    """The reference's op sequence (oracle, kind 'port') on a stratified sample of the arena, at 1 thread
+    and at all threads, median of 5 after 1 warm-up; extrapolated per element to the whole arena."""
     import oracle
 
+    picked, sizes = stratified_sample(named, budget)
     torch.manual_seed(0)
-    sample, tot = [], 0
-    for name, shape in named:
-        n = int(np.prod(shape))
-        sample.append(torch.randn(n) * 1e-3)
-        tot += n
-        if tot >= budget_elems:
-            break
-    threads = torch.get_num_threads()
+    sample = [torch.randn(sizes[i]) * 1e-3 for i in picked]
+    tot = sum(x.numel() for x in sample)
+    w = 1 if 2**bits <= 127 else 4
 
     def one():
         payloads = []
         for x in sample:  # encode: reference op sequence + tobytes (global_grpc_compression.py:105-116)
-            q, norm, w, lv = oracle.qsgd_quantize(x, bits)
-            payloads.append((q.numpy().astype(np.int8 if w == 8 else np.int32).tobytes(), norm, w, lv, x.numel()))
-        for b, norm, w, lv, n in payloads:  # decode: frombuffer + decompress_quantized (:173-182)
-            q = torch.from_numpy(np.frombuffer(b, dtype=np.int8 if w == 8 else np.int32).copy())
+            q, norm, wd, lv = oracle.qsgd_quantize(x, bits)
+            payloads.append((q.numpy().astype(np.int8 if wd == 8 else np.int32).tobytes(), norm, wd, lv, x.numel()))
+        for b, norm, wd, lv, n in payloads:  # decode: frombuffer + decompress_quantized (:173-182)
+            q = torch.from_numpy(np.frombuffer(b, dtype=np.int8 if wd == 8 else np.int32).copy())
             oracle.qsgd_dequantize(q, norm, lv, (n,))
 
-    one()  # warm-up
-    ts = []
-    for _ in range(3):
-        t0 = time.perf_counter()
-        one()
-        ts.append(time.perf_counter() - t0)
-    t = float(np.median(ts))
-    w = 1 if 2**bits <= 127 else 4
+    all_threads = torch.get_num_threads()
+    times = {}
+    for th in (1, all_threads):
+        torch.set_num_threads(th)
+        times[th] = _median_time(one)
+    torch.set_num_threads(all_threads)
+    N = sum(sizes)
+    per = (8 + 2 * w)
+    best = min(times, key=lambda k: times[k])
     return {
-        "value": round((8 + 2 * w) * tot / t / 1e9, 4),
+        "value": round(per * tot / times[best] / 1e9, 4),
         "unit": "GB/s",
-        "cores": threads,
+        "cores": best,
         "kind": "port",
-        "sample": f"first {len(sample)} tensors of the same Llama-400M arena ({tot} fp32 elements), "
-                  f"QSGD s={bits} encode+decode incl. tobytes/frombuffer, median of 3 after 1 warm-up; "
-                  f"fp32-gradient rate {4 * tot / t / 1e9:.4f} GB/s",
-        "seconds_per_pass": round(t, 4),
+        "cpu": cpu_model(),
+        "sample": f"{len(picked)} of {len(sizes)} tensors (every {max(1, int(np.ceil(N / budget)))}th; {tot} of {N} "
+                  f"fp32 elements) of the same arena, QSGD s={bits} encode+decode incl. tobytes/frombuffer, median of 5 "
+                  f"after 1 warm-up, per-element rate extrapolated to the arena",
+        "GBs_by_threads": {str(k): round(per * tot / v / 1e9, 4) for k, v in times.items()},
+        "seconds_full_arena_by_threads": {str(k): round(v * N / tot, 2) for k, v in times.items()},
     }
+
+
+def cpu_baseline_topk(torch, named, ratio, budget=12_000_000):
+    """The reference Top-K with error feedback (oracle TopKOracle: compensate -> topk -> residual) plus its
+    zero-fill decode, on a stratified sample, all threads and 1 thread, median of 5; extrapolated."""
+    import oracle
+
+    picked, sizes = stratified_sample(named, budget)
+    torch.manual_seed(0)
+    sample = [torch.randn(sizes[i]) * 1e-3 for i in picked]
+    tot = sum(x.numel() for x in sample)
+    ks = [oracle.topk_k(x.numel(), ratio) for x in sample]
+    comp = oracle.TopKOracle(ratio)
+
+    def one():
+        for j, x in enumerate(sample):
+            vals, idx = comp.compress(x, f"t{j}")
+            oracle.topk_desparse(vals, idx, x.numel())
+
+    all_threads = torch.get_num_threads()
+    times = {}
+    for th in (1, all_threads):
+        torch.set_num_threads(th)
+        times[th] = _median_time(one)
+    torch.set_num_threads(all_threads)
+    alg = 16 * tot + 24 * sum(ks)
+    best = min(times, key=lambda k: times[k])
+    return {"value": round(alg / times[best] / 1e9, 4), "unit": "GB/s", "cores": best, "kind": "port",
+            "cpu": cpu_model(),
+            "sample": f"{len(picked)} of {len(sizes)} tensors ({tot} fp32 elements), Top-K k={ratio:g} with error "
+                      f"feedback + zero-fill decode, median of 5 after 1 warm-up",
+            "GBs_by_threads": {str(k): round(alg / v / 1e9, 4) for k, v in times.items()}}
+
+
+# ---------------------------------------------------------------- measurement helpers
+
+def pmc_traffic(kernel, config, bits):
+    """Per-launch HBM bytes of ``kernel`` from profiles/pmc_traffic.json, if it was measured on these
+    exact kernel sources (its source digest); otherwise None."""
+    from omnifed_amd.build import source_digest
+
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            tj = json.load(f)
+    except (OSError, ValueError):
+        return None, "no PMC file"
+    if tj.get("config") != config or tj.get("bits") != bits:
+        return None, "PMC file is for another config"
+    if tj.get("source_sha") != source_digest():
+        return None, f"PMC file measured on other kernel sources (commit {tj.get('commit')}, {tj.get('date')})"
+    return tj.get("bytes_per_launch", {}).get(kernel), f"rocprofv3 PMC, commit {tj.get('commit')}, {tj.get('date')}"
+
+
+def event_ms(torch, st, fn, reps):
+    """Mean duration of ``fn`` (its launches on stream ``st``) from HIP events recorded on ``st``."""
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for i in range(reps):
+        ev[i][0].record(st)
+        fn(i)
+        ev[i][1].record(st)
+    torch.cuda.synchronize()
+    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
 
 def main():
     args = parse()
-    rank, world, local = init_dist(args.gpus)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
+
+    import torch
+    import torch.distributed as dist
+
+    rank, world, local = init_dist(torch, dist)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from omnifed_amd import codec, shapes
@@ -122,92 +245,135 @@ def main():
 
     if rank == 0:
         build()
-    barrier(world)
+    if world > 1:
+        dist.barrier()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def max_over_ranks(v):
+        if world == 1:
+            return v
+        t = torch.tensor([v], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def timed(step, k0, steps):
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(k0 + i)
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+        return max_over_ranks(time.perf_counter() - t0)
+
     named = shapes.model_shapes(args.config)
     sizes = [shapes.numel(s) for _, s in named]
     N = sum(sizes)
     plan = codec.Plan.get(sizes, device=dev, chunk=args.chunk)
+    weight = float(1 + rank)  # this client's batch_samples (the weighting fused as alpha)
+    g = torch.Generator(device=dev)
+    g.manual_seed(1000 + rank)
+    x = torch.randn(plan.arena_end, device=dev, generator=g) * 1e-3
+    st = torch.cuda.current_stream(dev)
+
+    # ------------------------------------------------------------ QSGD
     s = args.bits
     L = 2**s
     w = 1 if L <= 127 else 4
     width = 8 * w
-    g = torch.Generator(device=dev)
-    g.manual_seed(1000 + rank)
-    x = torch.randn(plan.arena_end, device=dev, generator=g) * 1e-3
-    q = torch.empty(plan.arena_end, dtype=torch.int8 if w == 1 else torch.int32, device=dev)
+    q = torch.empty(plan.payload_elems(width), dtype=torch.int8 if w == 1 else torch.int32, device=dev)
     norms = torch.empty(plan.nt, dtype=torch.float32, device=dev)
     y = torch.empty(plan.arena_end, dtype=torch.float32, device=dev)
     seed = 0x5EED + rank
 
-    def step(i):
-        plan.qsgd_encode(x, s, q_out=q, norm_out=norms, seed=seed, offset=i)
+    def q_step(i):
+        plan.qsgd_encode(x, s, q_out=q, norm_out=norms, alpha=weight, seed=seed, offset=i)
         plan.qsgd_decode(q, width, L, norms, y_out=y)
 
-    for i in range(args.warmup):
-        step(i)
-    plan.check()
-    torch.cuda.synchronize()
-    barrier(world)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    torch.cuda.synchronize()
-    barrier(world)
-    torch.cuda.synchronize()
-    dt = max_over_ranks(time.perf_counter() - t0, world, dev)
-    plan.check()
-    alg_bytes_step = (8 + 2 * w) * N
-    value = world * alg_bytes_step * args.steps / dt / 1e9
+    qsgd = None
+    if args.codec == "qsgd":
+        for i in range(args.warmup):
+            q_step(i)
+        plan.check()
+        dt = timed(q_step, args.warmup, args.steps)
+        plan.check()
+        alg_bytes_step = (8 + 2 * w) * N
+        reps = max(args.steps, 10)
+        enc_ms = event_ms(torch, st, lambda i: plan.qsgd_encode(x, s, q_out=q, norm_out=norms, alpha=weight, seed=seed,
+                                                                offset=10_000 + i), reps)
+        dec_ms = event_ms(torch, st, lambda i: plan.qsgd_decode(q, width, L, norms, y_out=y), reps)
+        plan.check()
+        enc_bytes = dec_bytes = (4 + w) * N
+        dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, plan.encoder_kernel) if enc_ms >= dec_ms else \
+            (dec_ms, dec_bytes, "qsgd_decode_flat")
+        achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+        traffic, tsrc = pmc_traffic(dom_name, args.config, s)
+        qsgd = {
+            "value": world * alg_bytes_step * args.steps / dt / 1e9, "ms_per_step": dt / args.steps * 1e3,
+            "alg_bytes_step": alg_bytes_step,
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": dom_name, "algorithmic_bytes_per_launch": dom_bytes,
+                         "avg_launch_ms": round(dom_ms, 4), "encode_ms": round(enc_ms, 4),
+                         "decode_ms": round(dec_ms, 4), "encode_GBs": round(enc_bytes / enc_ms / 1e6, 1),
+                         "decode_GBs": round(dec_bytes / dec_ms / 1e6, 1)},
+        }
 
-    # --- dominant-kernel roofline: HIP events on the launch stream around each launch
-    st = torch.cuda.current_stream(dev)
-    reps = max(args.steps, 10)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    evd = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for i in range(reps):
-        ev[i][0].record(st)
-        plan.qsgd_encode(x, s, q_out=q, norm_out=norms, seed=seed, offset=10_000 + i)
-        ev[i][1].record(st)
-        evd[i][0].record(st)
-        plan.qsgd_decode(q, width, L, norms, y_out=y)
-        evd[i][1].record(st)
-    torch.cuda.synchronize()
-    enc_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evd]))
-    enc_bytes = (4 + w) * N
-    dec_bytes = (w + 4) * N
-    dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, plan.encoder_kernel) if enc_ms >= dec_ms else \
-        (dec_ms, dec_bytes, "qsgd_decode_flat")
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
-    traffic = None
-    tpath = os.path.join(HERE, "profiles", "pmc_traffic.json")
-    if os.path.exists(tpath):
-        try:
-            with open(tpath) as f:
-                tj = json.load(f)
-            if tj.get("config") == args.config and tj.get("bits") == s:
-                traffic = tj.get("bytes_per_launch", {}).get(dom_name)
-        except (OSError, ValueError):
-            traffic = None
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": dom_name,
-                "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_ms": round(dom_ms, 4),
-                "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
-                "encode_GBs": round(enc_bytes / enc_ms / 1e6, 1), "decode_GBs": round(dec_bytes / dec_ms / 1e6, 1)}
+    # ------------------------------------------------------------ Top-K
+    topk = None
+    if args.codec == "topk" or not args.no_topk:
+        ratio = args.ratio
+        ks = plan.topk_ks(ratio)
+        K = sum(ks)
+        res = torch.zeros(plan.arena_end, dtype=torch.float32, device=dev)
+        vals = torch.empty(K, dtype=torch.float32, device=dev)
+        idx = torch.empty(K, dtype=torch.int64, device=dev)
+        yt = torch.empty(plan.arena_end, dtype=torch.float32, device=dev)
+
+        def t_enc(i):
+            plan.topk_encode(x, ratio, residual=res, residual_mode=1, values=vals, indices=idx, alpha=weight)
+
+        def t_step(i):
+            t_enc(i)
+            plan.topk_decode_arena(vals, idx, ratio, y=yt, mode=0)
+
+        for i in range(args.warmup):
+            t_step(i)
+        steps_t = args.steps if args.codec == "topk" else max(5, args.steps // 2)
+        dtt = timed(t_step, args.warmup, steps_t)
+        alg_t = 16 * N + 24 * K
+        reps = max(steps_t, 5)
+        tenc = event_ms(torch, st, t_enc, reps)
+        tdec = event_ms(torch, st, lambda i: plan.topk_decode_arena(vals, idx, ratio, y=yt, mode=0), reps)
+        enc_alg = 12 * N + 12 * K  # read x, read+write the residual, write values+indices
+        ach = enc_alg / (tenc * 1e-3) / 1e9
+        topk = {"metric": METRIC_TOPK, "value": round(world * alg_t * steps_t / dtt / 1e9, 2), "unit": "GB/s",
+                "ms_per_step": round(dtt / steps_t * 1e3, 4), "steps": steps_t, "ratio": ratio, "k_total": K,
+                "algorithmic_bytes_per_step_per_client": alg_t,
+                "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                             "kernel": "omf_topk_encode (all launches of one call, host sync included)",
+                             "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(tenc, 4),
+                             "decode_ms": round(tdec, 4)}}
+        del res, yt
 
     extras = {}
-    if not args.no_extras and world == 1:
+    if not args.no_extras and world == 1 and qsgd is not None:
         # PCIe-inclusive rate: host fp32 in -> device encode -> host payload; host payload -> decode -> host fp32
         xh = torch.empty(plan.arena_end, dtype=torch.float32, pin_memory=True)
         xh.copy_(x, non_blocking=False)
-        qh = torch.empty(plan.arena_end, dtype=q.dtype, pin_memory=True)
+        qh = torch.empty(q.numel(), dtype=q.dtype, pin_memory=True)
         yh = torch.empty(plan.arena_end, dtype=torch.float32, pin_memory=True)
         xd = torch.empty_like(x)
 
         def pcie_step(i):
             xd.copy_(xh, non_blocking=True)
-            plan.qsgd_encode(xd, s, q_out=q, norm_out=norms, seed=seed, offset=20_000 + i)
+            plan.qsgd_encode(xd, s, q_out=q, norm_out=norms, alpha=weight, seed=seed, offset=20_000 + i)
             qh.copy_(q, non_blocking=True)
             q.copy_(qh, non_blocking=True)
             plan.qsgd_decode(q, width, L, norms, y_out=y)
@@ -221,62 +387,72 @@ def main():
         torch.cuda.synchronize()
         pt = (time.perf_counter() - t1) / 5
         extras["pcie_inclusive"] = {"ms_per_step": round(pt * 1e3, 3),
-                                    "algorithmic_GBs": round(alg_bytes_step / pt / 1e9, 2),
+                                    "algorithmic_GBs": round((8 + 2 * w) * N / pt / 1e9, 2),
                                     "fp32_gradient_GBs": round(4 * N / pt / 1e9, 2)}
         del xh, qh, yh, xd
     if not args.no_extras and world > 1:
-        from omnifed_amd.ps import GpuOps, weighted_sum_gather, weighted_sum_reduce
+        from omnifed_amd.ps import GpuOps, qsgd_weighted_round, topk_sparse_aggregate, total_weight
 
-        ops = GpuOps(plan)
-        wgt = float(world * (world + 1) / 2)
+        ops = GpuOps(plan, seed=seed)
+        total = total_weight(weight, dev)
         acc = torch.empty_like(y)
         bufs = [(torch.empty_like(q), torch.empty_like(norms)) for _ in range(world)] if rank == 0 else None
+        ps = {"clients": world, "total_weight": total, "fp32_bytes_per_rank": 4 * N, "payload_bytes_per_rank": w * N}
+        for mode in ("gather", "reduce"):
+            def ps_step(i, mode=mode):
+                qsgd_weighted_round(x, weight, total, ops, s, 30_000 + i, mode=mode, y=y, acc=acc, q=q, norms=norms,
+                                    bufs=bufs)
+            ps_step(0)
+            ps[f"{mode}_ms"] = round(timed(ps_step, 1, 5) / 5 * 1e3, 3)
+        extras["ps_weighted_sum"] = ps
+        if topk is not None:
+            K = topk["k_total"]
+            vals = torch.empty(K, dtype=torch.float32, device=dev)
+            idx = torch.empty(K, dtype=torch.int64, device=dev)
+            plan.topk_encode(x, args.ratio, values=vals, indices=idx, alpha=weight)
+            tb = [(torch.empty_like(vals), torch.empty_like(idx)) for _ in range(world)]
+            agg = {}
+            for name, dst in (("allgather", None), ("gather_root", 0)):
+                def tk_step(i, dst=dst):
+                    topk_sparse_aggregate(vals, idx, args.ratio, acc, ops, dst=dst, bufs=tb)
+                tk_step(0)
+                agg[f"{name}_ms"] = round(timed(tk_step, 1, 5) / 5 * 1e3, 3)
+            agg["bytes_per_rank"] = 12 * K
+            extras["topk_sparse_aggregate"] = agg
 
-        def t_op(fn, reps=5):
-            fn()
-            torch.cuda.synchronize()
-            barrier(world)
-            ta = time.perf_counter()
-            for _ in range(reps):
-                fn()
-            torch.cuda.synchronize()
-            barrier(world)
-            return max_over_ranks((time.perf_counter() - ta) / reps, world, dev)
-
-        t_red = t_op(lambda: weighted_sum_reduce(y, wgt, ops))
-        t_gat = t_op(lambda: weighted_sum_gather(q, norms, width, L, acc, wgt, ops, bufs=bufs))
-        extras["ps_weighted_sum"] = {"reduce_fp32_ms": round(t_red * 1e3, 3),
-                                     "gather_payload_decode_ms": round(t_gat * 1e3, 3),
-                                     "fp32_bytes_per_rank": 4 * N, "payload_bytes_per_rank": w * N}
-
-    cpu = None
+    cpu = cpu_t = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(named, s)
+        if qsgd is not None:
+            cpu = cpu_baseline(torch, named, s)
+        if topk is not None:
+            cpu_t = cpu_baseline_topk(torch, named, args.ratio)
+    if topk is not None:
+        topk["cpu_baseline"] = cpu_t
 
     if rank == 0:
-        line = {
-            "metric": METRIC,
-            "value": round(value, 2),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic N(0,1)*1e-3 gradients of the named shapes (no checkpoints)",
-            "config": {"workload": f"{args.config} QSGD encode+decode, bit_width {s} ({L} levels, int{8 * w} wire), "
-                                   f"philox draws, one client per GPU",
-                       "tensors": len(sizes), "elements_per_client": N, "bit_width": s,
-                       "algorithmic_bytes_per_step_per_client": alg_bytes_step,
-                       "fp32_gradient_GBs": round(world * 4 * N * args.steps / dt / 1e9, 2),
-                       "parallelism": f"clients{world}"},
-            "roofline": roofline,
-            "cpu_baseline": cpu,
-            **extras,
-        }
+        common = {"n_gpus": world, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+                  "vs_baseline": None, "dtype": "f32",
+                  "data": "synthetic N(0,1)*1e-3 gradients of the named shapes (no checkpoints)"}
+        if qsgd is not None:
+            line = {"metric": METRIC, "value": round(qsgd["value"], 2), "unit": "GB/s", "steps": args.steps,
+                    "ms_per_step": round(qsgd["ms_per_step"], 4), **common,
+                    "config": {"workload": f"{args.config} QSGD encode+decode, bit_width {s} ({L} levels, int{8 * w} "
+                                           f"wire), philox draws, client weighting fused (alpha = batch_samples = "
+                                           f"rank + 1), one client per GPU",
+                               "tensors": len(sizes), "elements_per_client": N, "bit_width": s,
+                               "algorithmic_bytes_per_step_per_client": qsgd["alg_bytes_step"],
+                               "fp32_gradient_GBs": round(qsgd["value"] * 4 / (8 + 2 * w), 2),
+                               "parallelism": f"clients{world}"},
+                    "roofline": qsgd["roofline"], "cpu_baseline": cpu, "topk": topk, **extras}
+        else:
+            line = {"metric": METRIC_TOPK, "value": topk["value"], "unit": "GB/s", "steps": topk["steps"],
+                    "ms_per_step": topk["ms_per_step"], **common,
+                    "config": {"workload": f"{args.config} Top-K k={args.ratio:g} per tensor, error feedback, "
+                                           f"client weighting fused, arena decode, one client per GPU",
+                               "tensors": len(sizes), "elements_per_client": N, "k_total": topk["k_total"],
+                               "algorithmic_bytes_per_step_per_client": topk["algorithmic_bytes_per_step_per_client"],
+                               "parallelism": f"clients{world}"},
+                    "roofline": topk["roofline"], "cpu_baseline": cpu_t, **extras}
         print(json.dumps(line), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

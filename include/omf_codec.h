@@ -17,8 +17,10 @@
  *    asynchronous on that stream; results are ready when the stream is.
  *  - Return value: 0 (OMF_OK) or a negative OMF_E* code; the message for the
  *    calling thread is in omf_last_error().  No C++ exception crosses the ABI.
- *  - Reentrant: no global mutable state.  A plan's workspace is used by one
- *    call at a time (one plan per stream/thread in flight).
+ *  - Reentrant: no global mutable state.  A plan is driven by one host thread at
+ *    a time; its stateful launches (encode, norms, fused PS step) may go to any
+ *    stream: a launch on a different stream than the plan's previous one is
+ *    ordered after it on the device (hipStreamWaitEvent), never run concurrently.
  *
  * Data layout ("update arena"): the named tensors of one client, flattened in
  * named_parameters() order into one fp32 buffer, tensor t occupying elements
@@ -26,7 +28,10 @@
  * (16-byte aligned starts; gaps between tensors are padding that is never
  * read as data).  Payload arenas (int8 / int32 QSGD levels, fp32 decoded
  * values) use the SAME element offsets.  Base pointers: fp32 and int32 buffers
- * 16-byte aligned, int8 buffers 4-byte aligned.
+ * 16-byte aligned, int8 buffers 4-byte aligned.  An int8 payload is written in
+ * whole dwords: the bytes from the end of a tensor up to the next multiple of 4
+ * (padding, inside the next tensor's aligned start) may be written as zero, so an
+ * int8 payload buffer must hold round_up(arena_end, 4) elements.
  */
 #ifndef OMF_CODEC_H
 #define OMF_CODEC_H
@@ -66,8 +71,10 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
 int omf_plan_destroy(omf_plan* plan);
 /* Number of workgroups one encode launch uses (diagnostics / roofline bookkeeping). */
 int64_t omf_plan_encode_items(const omf_plan* plan);
-/* Synchronise `stream` and report an in-kernel wait timeout (OMF_ETIMEOUT) if one occurred;
- * returns 1 (results still exact) when the resident encoder had to recompute a norm. */
+/* Synchronise `stream` and report what the plan's launches since the previous check hit:
+ * OMF_ETIMEOUT when an on-chip hand-off wait of the ring encoder exceeded its bound (that
+ * workgroup aborted and drained: the payload is invalid); 1 (results still exact) when an
+ * encoder recomputed a norm after a bounded wait; 0 otherwise.  Clears what it reports. */
 int omf_plan_check(omf_plan* plan, void* stream);
 /* Encoder strategy: 0 = register-resident items for tensors of at most
  * omf_plan_resident_capacity() items (x read once; the workgroup holds its 16 Ki elements
@@ -123,12 +130,33 @@ int omf_qsgd_encode(omf_plan* plan, const float* x, float alpha, int32_t bit_wid
 int omf_qsgd_norms(omf_plan* plan, const float* x, float alpha, float* norm_out, void* stream);
 
 /*
+ * omf_qsgd_encode / omf_qsgd_norms for tensors whose dtype is bf16 or fp16.  The reference
+ * quantises in the tensor's own dtype (qsgd.py:46-58 on a bf16/fp16 tensor; the weighting
+ * torch.mul(param, batch_samples) of global_grpc.py:104/121 too).  x still holds fp32 (the
+ * exact upcast of the tensor); value_format 0 = fp32 (= omf_qsgd_encode), 1 = bf16,
+ * 2 = fp16, and the encoder rounds (to nearest even) where torch's CPU ops round:
+ *   xs   = round(fl32(x * alpha))                (exact when alpha = 1)
+ *   norm = round(fp32 L2 norm of xs)             (norm_out receives it; the wire's float32)
+ *   vn   = round(fl32(xs / norm))
+ * and an fp16 |vn| * L of 65520 or more (inf in fp16) gives level 0, as the reference's
+ * int64 conversion of inf does.  The rest of the chain is exact in fp32.
+ */
+int omf_qsgd_encode_ex(omf_plan* plan, const float* x, float alpha, int32_t bit_width, int32_t value_format,
+                       const float* u, uint64_t seed, uint64_t offset, const float* norm_in, void* q_out,
+                       float* norm_out, void* stream);
+int omf_qsgd_norms_ex(omf_plan* plan, const float* x, float alpha, int32_t value_format, float* norm_out,
+                      void* stream);
+
+/*
  * Fused PS step: avg_out = acc / divisor (IEEE fp32 division, as the reference's
  * `acc / total_samples` in CentralServerServicer._apply_model_updates,
  * src/omnifed/hybrid/communicator/global_grpc_server.py:155-171) and the QSGD encode of avg
  * for the downlink (_send_current_model, :213-234 -> encode_layer_state) in ONE launch
  * with the ring encoder (acc read once); other strategies run divide + encode.
- * Arguments after avg_out as omf_qsgd_encode (no alpha, no norm_in).  avg_out may equal acc.
+ * Arguments after avg_out as omf_qsgd_encode (no alpha, no norm_in).  avg_out must be
+ * disjoint from acc for the one-launch path (the launch re-reads acc for tensors larger
+ * than the on-chip ring); avg_out == acc is accepted and runs as divide (in place) +
+ * encode; a partial overlap is OMF_EINVAL.
  */
 int omf_ps_apply_encode(omf_plan* plan, const float* acc, float divisor, float* avg_out, int32_t bit_width,
                         const float* u, uint64_t seed, uint64_t offset, void* q_out, float* norm_out, void* stream);
@@ -206,6 +234,18 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
  */
 int omf_topk_decode(const float* values, const int64_t* indices, int64_t k, float* y,
                     int64_t n, int32_t mode, void* stream);
+
+/*
+ * Top-K decode of ONE client's whole selection (omf_topk_encode's packed layout for the
+ * plan's tensors at `ratio`) into an arena y, one launch: the per-layer _decode_topk_layer
+ * loop of decode_updates_dict (global_grpc_compression.py:140-160, 214-223) and, with
+ * mode 2, one client's term of layerwise_decompress's scatter-add (core.py:62-71) as
+ * torch_mpi.sparse_aggregate applies it to every parameter (torch_mpi.py:302-359).
+ * mode 0: y := 0 then set; 1: set over y (overlay); 2: y += v.  Index -1 (padding) and
+ * indices outside a tensor are skipped.  Plans of at most 4096 tensors.
+ */
+int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
+                          int32_t mode, void* stream);
 
 #ifdef __cplusplus
 }

@@ -45,6 +45,9 @@ SIGNATURES = {
     "omf_plan_ring_profile": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64)]),
     "omf_qsgd_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p, _c_p, _c_p]),
     "omf_qsgd_norms": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_p]),
+    "omf_qsgd_encode_ex": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_i32, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p, _c_p,
+                                          _c_p]),
+    "omf_qsgd_norms_ex": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_i32, _c_p, _c_p]),
     "omf_ps_apply_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p,
                                            _c_p]),
     "omf_qsgd_decode": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
@@ -56,6 +59,7 @@ SIGNATURES = {
     "omf_topk_workspace_bytes": (_c_size, [_c_p, _c_f64]),
     "omf_topk_encode": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_f64, _c_f32, _c_p, _c_p, _c_p, _c_size, _c_p]),
     "omf_topk_decode": (ctypes.c_int, [_c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i32, _c_p]),
+    "omf_topk_decode_arena": (ctypes.c_int, [_c_p, _c_f64, _c_p, _c_p, _c_p, _c_i32, _c_p]),
 }
 
 _lock = threading.Lock()

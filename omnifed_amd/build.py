@@ -46,6 +46,21 @@ def _sources():
     return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
 
 
+def source_digest() -> str:
+    """SHA-256 over the library's sources and headers (stamps measurements taken with a build)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(f for f in os.listdir(CSRC) if f.endswith((".hip", ".h", ".cpp")))
+    for f in files:
+        with open(os.path.join(CSRC, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    for f in sorted(os.listdir(INCLUDE)):
+        with open(os.path.join(INCLUDE, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()
+
+
 def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True

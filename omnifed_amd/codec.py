@@ -101,7 +101,7 @@ class Plan:
         check(L.omf_plan_create(szs, ofs, n, self.chunk, device.index, ctypes.byref(h)), "omf_plan_create")
         self._h = h
         self._lock = threading.Lock()
-        self._topk_ws: Optional[torch.Tensor] = None
+        self._topk_ws: Dict[int, torch.Tensor] = {}  # per stream: launches on two streams never share one
         # the library's default (omf_qsgd.hip), unless an experiment overrides it
         self.strategy = {"0": "resident", "1": "ordered"}.get(os.environ.get("OMF_ENCODE_STRATEGY", ""), "ring")
 
@@ -125,6 +125,12 @@ class Plan:
     @property
     def handle(self):
         return self._h
+
+    def payload_elems(self, width: int) -> int:
+        """Elements a payload arena must hold: an int8 payload is stored in whole dwords, so the
+        last tensor's partial dword may be written (as zero levels) up to ``arena_end`` rounded
+        up to 4 (include/omf_codec.h, data layout)."""
+        return self.arena_end if int(width) == 32 else (self.arena_end + 3) & ~3
 
     @property
     def encode_items(self) -> int:
@@ -189,8 +195,11 @@ class Plan:
     def qsgd_encode(self, x: torch.Tensor, bit_width: int, q_out: Optional[torch.Tensor] = None,
                     norm_out: Optional[torch.Tensor] = None, alpha: float = 1.0,
                     u: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
-                    norm_in: Optional[torch.Tensor] = None, stream: Optional[int] = None):
-        """Encode the whole arena ``x``; returns ``(q, norms)`` (device tensors)."""
+                    norm_in: Optional[torch.Tensor] = None, stream: Optional[int] = None, value_format: int = 0):
+        """Encode the whole arena ``x``; returns ``(q, norms)`` (device tensors).
+
+        ``value_format``: 0 fp32, 1 bf16, 2 fp16 — the dtype the tensors had (x holds their exact
+        fp32 upcast; omf_qsgd_encode_ex rounds where the reference's reduced-precision ops do)."""
         s = int(bit_width)
         if not 0 <= s <= 30:
             raise ValueError("bit_width must be in [0, 30]")
@@ -199,8 +208,8 @@ class Plan:
         dev = self.device
         _need(x, "x", torch.float32, dev, self.arena_end, 16)
         if q_out is None:
-            q_out = torch.empty(self.arena_end, dtype=qdt, device=dev)
-        _need(q_out, "q_out", qdt, dev, self.arena_end, 4 if width == 8 else 16)
+            q_out = torch.empty(self.payload_elems(width), dtype=qdt, device=dev)
+        _need(q_out, "q_out", qdt, dev, self.payload_elems(width), 4 if width == 8 else 16)
         if norm_out is None:
             norm_out = torch.empty(self.nt, dtype=torch.float32, device=dev)
         _need(norm_out, "norm_out", torch.float32, dev, self.nt, 4)
@@ -210,10 +219,10 @@ class Plan:
             _need(norm_in, "norm_in", torch.float32, dev, self.nt, 4)
         st = stream if stream is not None else _stream(dev)
         with self._lock:
-            check(lib().omf_qsgd_encode(self._h, _ptr(x), float(alpha), s, _ptr(u),
-                                        int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset) & 0xFFFFFFFFFFFFFFFF,
-                                        _ptr(norm_in), _ptr(q_out), _ptr(norm_out), ctypes.c_void_p(st)),
-                  "omf_qsgd_encode")
+            check(lib().omf_qsgd_encode_ex(self._h, _ptr(x), float(alpha), s, int(value_format), _ptr(u),
+                                           int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset) & 0xFFFFFFFFFFFFFFFF,
+                                           _ptr(norm_in), _ptr(q_out), _ptr(norm_out), ctypes.c_void_p(st)),
+                  "omf_qsgd_encode_ex")
         return q_out, norm_out
 
     def ps_apply_encode(self, acc: torch.Tensor, divisor: float, bit_width: int,
@@ -237,8 +246,8 @@ class Plan:
             avg_out = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
         _need(avg_out, "avg_out", torch.float32, dev, self.arena_end, 16)
         if q_out is None:
-            q_out = torch.empty(self.arena_end, dtype=qdt, device=dev)
-        _need(q_out, "q_out", qdt, dev, self.arena_end, 4 if width == 8 else 16)
+            q_out = torch.empty(self.payload_elems(width), dtype=qdt, device=dev)
+        _need(q_out, "q_out", qdt, dev, self.payload_elems(width), 4 if width == 8 else 16)
         if norm_out is None:
             norm_out = torch.empty(self.nt, dtype=torch.float32, device=dev)
         _need(norm_out, "norm_out", torch.float32, dev, self.nt, 4)
@@ -253,7 +262,7 @@ class Plan:
         return avg_out, q_out, norm_out
 
     def qsgd_norms(self, x: torch.Tensor, alpha: float = 1.0, norm_out: Optional[torch.Tensor] = None,
-                   stream: Optional[int] = None) -> torch.Tensor:
+                   stream: Optional[int] = None, value_format: int = 0) -> torch.Tensor:
         dev = self.device
         _need(x, "x", torch.float32, dev, self.arena_end, 16)
         if norm_out is None:
@@ -261,8 +270,8 @@ class Plan:
         _need(norm_out, "norm_out", torch.float32, dev, self.nt, 4)
         st = stream if stream is not None else _stream(dev)
         with self._lock:
-            check(lib().omf_qsgd_norms(self._h, _ptr(x), float(alpha), _ptr(norm_out), ctypes.c_void_p(st)),
-                  "omf_qsgd_norms")
+            check(lib().omf_qsgd_norms_ex(self._h, _ptr(x), float(alpha), int(value_format), _ptr(norm_out),
+                                          ctypes.c_void_p(st)), "omf_qsgd_norms_ex")
         return norm_out
 
     def qsgd_decode(self, q: torch.Tensor, width: int, levels: int, norm: torch.Tensor,
@@ -362,13 +371,36 @@ class Plan:
         need = int(L.omf_topk_workspace_bytes(self._h, float(ratio)))
         st = stream if stream is not None else _stream(dev)
         with self._lock:
-            if self._topk_ws is None or self._topk_ws.numel() < need:
-                self._topk_ws = torch.empty(need, dtype=torch.uint8, device=dev)
+            ws = self._topk_ws.get(st)
+            if ws is None or ws.numel() < need:
+                ws = torch.empty(need, dtype=torch.uint8, device=dev)
+                self._topk_ws[st] = ws
             check(L.omf_topk_encode(self._h, _ptr(x), _ptr(residual) if residual_mode else None, int(residual_mode),
-                                    float(ratio), float(alpha), _ptr(values), _ptr(indices), _ptr(self._topk_ws),
-                                    ctypes.c_size_t(self._topk_ws.numel()), ctypes.c_void_p(st)),
+                                    float(ratio), float(alpha), _ptr(values), _ptr(indices), _ptr(ws),
+                                    ctypes.c_size_t(ws.numel()), ctypes.c_void_p(st)),
                   "omf_topk_encode")
         return values, indices, ks
+
+
+    def topk_decode_arena(self, values: torch.Tensor, indices: torch.Tensor, ratio: float,
+                          y: Optional[torch.Tensor] = None, mode: int = 0, stream: Optional[int] = None) -> torch.Tensor:
+        """Decode one client's whole Top-K selection (topk_encode's packed layout at ``ratio``)
+        into the arena ``y``: mode 0 zeros + set, 1 overlay, 2 scatter-add (one launch)."""
+        dev = self.device
+        K = sum(self.topk_ks(ratio))
+        _need(values, "values", torch.float32, dev, K, 4)
+        _need(indices, "indices", torch.int64, dev, K, 8)
+        if mode not in (0, 1, 2):
+            raise ValueError("mode must be 0, 1 or 2")
+        if y is None:
+            if mode != 0:
+                raise ValueError("mode 1/2 need y")
+            y = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
+        _need(y, "y", torch.float32, dev, self.arena_end, 4)
+        st = stream if stream is not None else _stream(dev)
+        check(lib().omf_topk_decode_arena(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), int(mode),
+                                          ctypes.c_void_p(st)), "omf_topk_decode_arena")
+        return y
 
 
 def div_(y: torch.Tensor, divisor: float, stream: Optional[int] = None) -> torch.Tensor:

@@ -66,6 +66,7 @@ struct EncArgs {
   uint32_t* counters;
   uint64_t* gran;
   float alpha;
+  uint32_t fmt;  // value format (omf_qsgd_dev.h kFmt*)
   float levels;  // 2^s as float (exact)
   uint32_t seed_lo, seed_hi, offset;
   uint64_t wait_ticks;  // bounded norm wait (100 MHz ticks)
@@ -99,8 +100,11 @@ __device__ __forceinline__ void load_f4(const float* __restrict__ p, int64_t b, 
   }
 }
 
-template <int V>
-__device__ __forceinline__ void scale_f4(float4 (&v)[V], float alpha) {
+// x * alpha (the client weighting), rounded to the value format for bf16/fp16 tensors
+// (torch.mul on a reduced-precision tensor rounds its product; with alpha = 1 it is exact).
+template <int V, class A>
+__device__ __forceinline__ void scale_f4(float4 (&v)[V], const A& a) {
+  const float alpha = a.alpha;
   if (alpha == 1.0f) return;
 #pragma unroll
   for (int k = 0; k < V; ++k) {
@@ -108,6 +112,7 @@ __device__ __forceinline__ void scale_f4(float4 (&v)[V], float alpha) {
     v[k].y = __fmul_rn(v[k].y, alpha);
     v[k].z = __fmul_rn(v[k].z, alpha);
     v[k].w = __fmul_rn(v[k].w, alpha);
+    if (a.fmt) v[k] = round_fmt4(v[k], a.fmt);
   }
 }
 
@@ -147,7 +152,7 @@ __device__ __forceinline__ void quant_store(const float4 (&v)[V], const EncArgs&
                                             int64_t tbegin, int32_t tensor, float norm) {
   static_assert(V % 4 == 0, "rows come in groups of 4 (RNG slots)");
   const bool zero = !(norm != 0.0f);  // norm == 0: all-zero payload (reference: dense passthrough)
-  const Divisor dv(norm);
+  const Divisor dv(norm, a.fmt);
 #pragma unroll
   for (int g = 0; g < V / 4; ++g) {
     float4 uu[4];
@@ -209,11 +214,11 @@ __device__ __forceinline__ void quant_sub(const EncArgs& a, int64_t b, int64_t e
   float4 v[V];
   if (e - b == (int64_t)V * 1024) {
     load_f4<V, true>(a.x, b, e, v);
-    scale_f4<V>(v, a.alpha);
+    scale_f4<V>(v, a);
     quant_store<WIDTH, HAS_U, true, V>(v, a, b, e, tbegin, tensor, norm);
   } else {
     load_f4<V, false>(a.x, b, e, v);
-    scale_f4<V>(v, a.alpha);
+    scale_f4<V>(v, a);
     quant_store<WIDTH, HAS_U, false, V>(v, a, b, e, tbegin, tensor, norm);
   }
 }
@@ -231,7 +236,7 @@ __device__ __forceinline__ float chunk_sumsq(const EncArgs& a, int64_t b, int64_
     float4 v[V];
     if (se - sb == S) load_f4<V, true>(a.x, sb, se, v);
     else load_f4<V, false>(a.x, sb, se, v);
-    scale_f4<V>(v, a.alpha);
+    scale_f4<V>(v, a);
     acc = sumsq_f4<V>(v, acc);
   }
   return acc;
@@ -265,7 +270,7 @@ __device__ __forceinline__ void publish_partial(const EncArgs& a, const TensorIn
       p += __longlong_as_double((long long)ld_agent(&a.partials[ti.pbase + j]));
     const double tot = block_sum_f64(p, sh.red);
     if (threadIdx.x == 0) {
-      const float norm = sqrtf((float)tot);
+      const float norm = finish_norm(tot, a.fmt);
       a.norm_out[t] = norm;
       st_agent(&a.gran[t], ((uint64_t)a.epoch << 32) | (uint64_t)__float_as_uint(norm));
     }
@@ -308,7 +313,7 @@ __device__ __forceinline__ float norm_wait_or_recompute(const EncArgs& a, const 
   }
   const double tot = block_sum_f64(p, sh.red);
   if (threadIdx.x == 0) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return sqrtf((float)tot);
+  return finish_norm(tot, a.fmt);
 }
 
 // ---------------------------------------------------------------- kernels
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(kThreads) void qsgd_encode_ordered(EncArgs a) {
     float4 v[EV];
     if (full) load_f4<EV, true>(a.x, it.begin, it.end, v);
     else load_f4<EV, false>(a.x, it.begin, it.end, v);
-    scale_f4<EV>(v, a.alpha);
+    scale_f4<EV>(v, a);
     publish_partial(a, ti, it.tensor, it.chunk, sumsq_f4<EV>(v, 0.0f), sh);
     if (NORM_ONLY) return;
     const float norm = norm_wait_or_recompute<EV>(a, ti, it.tensor, sh);
@@ -495,7 +500,25 @@ struct omf_plan {
   omf::ring::Tensor* d_ring_t = nullptr;
   uint64_t* d_ring_gran = nullptr;
   unsigned long long* d_ring_prof = nullptr;  // 16 phase counters (OMF_RING_DBG & 4)
+  // Launches that use the sync block / granules are ordered across streams: a launch on a
+  // stream other than the previous one first waits for the previous launch's event.
+  hipEvent_t last_ev = nullptr;
+  hipStream_t last_stream = nullptr;
+  bool last_valid = false;
 };
+
+// Order this launch after the plan's previous stateful launch when the stream changes.
+static int plan_enter(omf_plan* p, hipStream_t st) {
+  if (p->last_valid && p->last_stream != st) OMF_HIP(hipStreamWaitEvent(st, p->last_ev, 0));
+  return OMF_OK;
+}
+static int plan_leave(omf_plan* p, hipStream_t st) {
+  if (!p->last_ev) OMF_HIP(hipEventCreateWithFlags(&p->last_ev, hipEventDisableTiming));
+  OMF_HIP(hipEventRecord(p->last_ev, st));
+  p->last_stream = st;
+  p->last_valid = true;
+  return OMF_OK;
+}
 
 // Plan internals shared with omf_topk.hip.
 namespace omf_plan_access {
@@ -840,6 +863,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
 int omf_plan_destroy(omf_plan* plan) {
   if (!plan) return OMF_OK;
   DeviceGuard g(plan->device);
+  if (plan->last_ev) (void)hipEventDestroy(plan->last_ev);
   if (plan->d_block) (void)hipFree(plan->d_block);
   delete plan;
   return OMF_OK;
@@ -913,6 +937,10 @@ int omf_plan_check(omf_plan* plan, void* stream) {
   OMF_HIP(hipStreamSynchronize((hipStream_t)stream));
   uint32_t err = 0;
   OMF_HIP(hipMemcpy(&err, plan->d_sync + 4, 4, hipMemcpyDeviceToHost));
+  if (err) OMF_HIP(hipMemset(plan->d_sync + 4, 0, 4));  // report each event once
+  if (err & 4u)
+    return fail(OMF_ETIMEOUT, "ring encoder: an on-chip hand-off wait exceeded its bound and the workgroup "
+                              "aborted; the payload of that launch is invalid");
   if (err & 2u) {
     set_error("encoder recomputed a norm after a bounded wait (items not co-resident); results are exact");
     return 1;
@@ -926,9 +954,27 @@ static int check_bits(int32_t s) {
   return OMF_OK;
 }
 
+static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, const float* u, uint64_t seed,
+                         uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream,
+                         float divisor, float* xout, uint32_t fmt);
+
 static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, const float* u, uint64_t seed,
                        uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream,
-                       float divisor = 0.0f, float* xout = nullptr) {
+                       float divisor = 0.0f, float* xout = nullptr, int32_t fmt = 0) {
+  if (!p) return fail(OMF_EINVAL, "plan is NULL");
+  if (fmt < 0 || fmt > 2) return fail(OMF_EINVAL, "value_format must be 0 (fp32), 1 (bf16) or 2 (fp16)");
+  DeviceGuard g(p->device);
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  if (int r = plan_enter(p, (hipStream_t)stream)) return r;
+  if (int r = encode_launch(p, x, alpha, s, u, seed, offset, norm_in, q, norm_out, norm_only, stream, divisor, xout,
+                            (uint32_t)fmt))
+    return r;
+  return plan_leave(p, (hipStream_t)stream);
+}
+
+static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, const float* u, uint64_t seed,
+                         uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream,
+                         float divisor, float* xout, uint32_t fmt) {
   if (!p) return fail(OMF_EINVAL, "plan is NULL");
   if (int r = check_bits(s)) return r;
   const int width = (1 << s) <= 127 ? 1 : 4;
@@ -946,6 +992,7 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
   a.counters = reinterpret_cast<uint32_t*>(p->d_sync + p->off_counters);
   a.gran = reinterpret_cast<uint64_t*>(p->d_sync + p->off_gran);
   a.alpha = alpha;
+  a.fmt = fmt;
   a.levels = (float)(1u << s);
   a.seed_lo = (uint32_t)seed; a.seed_hi = (uint32_t)(seed >> 32); a.offset = (uint32_t)offset;
   a.wait_ticks = p->wait_ticks;
@@ -971,6 +1018,8 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
     r.err = reinterpret_cast<uint32_t*>(p->d_sync + 4);
     r.n_items = p->n_ring;
     r.alpha = alpha;
+    r.fmt = fmt;
+    r.round_in = (fmt != 0 && alpha != 1.0f) ? 1u : 0u;
     r.divisor = divisor;
     r.divide = divisor != 0.0f ? 1u : 0u;
     r.xout = xout;
@@ -979,6 +1028,7 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
     if (++p->ring_epoch == 0) ++p->ring_epoch;
     r.epoch = p->ring_epoch;
     r.wait_ticks = p->wait_ticks;
+    r.lds_wait_ticks = kWaitTicks;
     r.dbg = p->ring_dbg;
     r.prof = p->d_ring_prof;
     const int grid = (int)std::min<int64_t>(p->ring_grid, std::max<int64_t>(p->n_ring, 1));
@@ -1020,13 +1070,34 @@ int omf_qsgd_encode(omf_plan* plan, const float* x, float alpha, int32_t bit_wid
   return encode_impl(plan, x, alpha, bit_width, u, seed, offset, norm_in, q_out, norm_out, false, stream);
 }
 
+int omf_qsgd_encode_ex(omf_plan* plan, const float* x, float alpha, int32_t bit_width, int32_t value_format,
+                       const float* u, uint64_t seed, uint64_t offset, const float* norm_in, void* q_out,
+                       float* norm_out, void* stream) {
+  return encode_impl(plan, x, alpha, bit_width, u, seed, offset, norm_in, q_out, norm_out, false, stream, 0.0f,
+                     nullptr, value_format);
+}
+
+int omf_qsgd_norms_ex(omf_plan* plan, const float* x, float alpha, int32_t value_format, float* norm_out,
+                      void* stream) {
+  return encode_impl(plan, x, alpha, 0, nullptr, 0, 0, nullptr, nullptr, norm_out, true, stream, 0.0f, nullptr,
+                     value_format);
+}
+
 int omf_ps_apply_encode(omf_plan* p, const float* acc, float divisor, float* avg_out, int32_t bit_width,
                         const float* u, uint64_t seed, uint64_t offset, void* q_out, float* norm_out, void* stream) {
   if (!p) return fail(OMF_EINVAL, "plan is NULL");
   if (!acc || !avg_out) return fail(OMF_EINVAL, "omf_ps_apply_encode: acc and avg_out must be non-NULL");
   if (!(divisor != 0.0f)) return fail(OMF_EINVAL, "omf_ps_apply_encode: divisor must be non-zero");
   if (!aligned(avg_out, 16)) return fail(OMF_EINVAL, "omf_ps_apply_encode: avg_out must be 16-byte aligned");
-  if (p->strategy == 2)  // one launch: read acc once, write avg and the payload
+  const size_t bytes = 4 * (size_t)p->arena_end;
+  const uintptr_t a0 = (uintptr_t)acc, o0 = (uintptr_t)avg_out;
+  const bool alias = avg_out == acc;
+  if (!alias && a0 < o0 + bytes && o0 < a0 + bytes)
+    return fail(OMF_EINVAL, "omf_ps_apply_encode: avg_out partially overlaps acc (pass the same pointer or disjoint buffers)");
+  // The fused launch reads acc while it writes avg (second-pass chunks of large tensors
+  // re-read acc, the bounded-wait fallback recomputes partials from it), so it needs
+  // avg_out disjoint from acc; in place it runs as divide + encode.
+  if (p->strategy == 2 && !alias)  // one launch: read acc once, write avg and the payload
     return encode_impl(p, acc, 1.0f, bit_width, u, seed, offset, nullptr, q_out, norm_out, false, stream, divisor,
                        avg_out);
   // other strategies: the same results in two passes

@@ -19,6 +19,30 @@ namespace omf {
 
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
+// Value formats: the dtype the reference computes in (qsgd.py:46-58 runs in the tensor's own
+// dtype).  The arena always holds fp32 (a bf16/fp16 tensor upcast exactly); in a reduced
+// format the encoder rounds where torch's bf16/fp16 CPU ops round: the weighted input
+// (torch.mul(param, batch_samples)), the norm (torch.norm(v).item()) and v / norm.  The
+// rest of the chain is exact (|vn| * 2^s, floor, the fp32 fraction: prob_round_up is
+// promoted to fp32 by `- lower.float()`).
+enum : uint32_t { kFmtF32 = 0, kFmtBF16 = 1, kFmtF16 = 2 };
+
+// Round to nearest even, as c10::BFloat16(float) / c10::Half(float) do (NaN stays NaN).
+__device__ __forceinline__ float round_bf16(float f) {
+  if (f != f) return f;
+  const uint32_t u = __float_as_uint(f);
+  return __uint_as_float((u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u);
+}
+__device__ __forceinline__ float round_f16(float f) { return (float)(_Float16)f; }
+__device__ __forceinline__ float round_fmt(float f, uint32_t fmt) {
+  return fmt == kFmtBF16 ? round_bf16(f) : (fmt == kFmtF16 ? round_f16(f) : f);
+}
+__device__ __forceinline__ float4 round_fmt4(float4 v, uint32_t fmt) {
+  return make_float4(round_fmt(v.x, fmt), round_fmt(v.y, fmt), round_fmt(v.z, fmt), round_fmt(v.w, fmt));
+}
+// The tensor norm from its sum of squares: fp32 sqrt (torch.norm's result), then the format.
+__device__ __forceinline__ float finish_norm(double sumsq, uint32_t fmt) { return round_fmt(sqrtf((float)sumsq), fmt); }
+
 __device__ __forceinline__ f32x2_t fma2(f32x2_t a, f32x2_t b, f32x2_t c) { return __builtin_elementwise_fma(a, b, c); }
 
 // Correctly rounded x / d from r = RN(1/d) on a pair (see div_markstein in omf_common.h).
@@ -37,11 +61,16 @@ __device__ __forceinline__ bool div_tiny(float x) { return __builtin_amdgcn_frex
 struct Divisor {
   float d, r;
   bool fast;
-  __device__ __forceinline__ explicit Divisor(float norm) : d(norm), r(1.0f / norm) {
+  uint32_t fmt;  // value format of the quotient (v / norm is rounded to it)
+  __device__ __forceinline__ explicit Divisor(float norm, uint32_t fmt_ = kFmtF32) : d(norm), r(1.0f / norm), fmt(fmt_) {
     const float a = fabsf(norm);
     fast = a >= 0x1p-100f && a <= 0x1p100f;
   }
   __device__ __forceinline__ float4 div4(float4 x) const {
+    const float4 q = div4_f32(x);
+    return fmt ? round_fmt4(q, fmt) : q;  // uniform branch
+  }
+  __device__ __forceinline__ float4 div4_f32(float4 x) const {
     if (!fast) return make_float4(x.x / d, x.y / d, x.z / d, x.w / d);
     const f32x2_t D = {d, d}, R = {r, r};
     const f32x2_t lo = div2_markstein((f32x2_t){x.x, x.y}, D, R);
@@ -93,6 +122,12 @@ __device__ __forceinline__ void qsgd_quad(float4 x, float4 u, const Divisor& dv,
   q[1] = qsgd_level_fast(vn.y, L, u.y);
   q[2] = qsgd_level_fast(vn.z, L, u.z);
   q[3] = qsgd_level_fast(vn.w, L, u.w);
+  if (dv.fmt == kFmtF16) {  // fp16 |vn| * L >= 65520 is inf in the reference: level 0
+    if (!(fabsf(__fmul_rn(vn.x, L)) < 65520.0f)) q[0] = 0;
+    if (!(fabsf(__fmul_rn(vn.y, L)) < 65520.0f)) q[1] = 0;
+    if (!(fabsf(__fmul_rn(vn.z, L)) < 65520.0f)) q[2] = 0;
+    if (!(fabsf(__fmul_rn(vn.w, L)) < 65520.0f)) q[3] = 0;
+  }
   if (!CHECK_BIG) return;
   // |vn| * L >= 2^63 (only with a caller-supplied norm far below |x|): the reference's
   // int64 conversion overflows to INT64_MIN and clamps to 0.  One test per quad.

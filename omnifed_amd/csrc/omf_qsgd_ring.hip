@@ -59,7 +59,8 @@ __device__ __forceinline__ float4 scale4(float4 v, float alpha) {
 // or the PS average x / total_samples (global_grpc_server.py:155-171), bit-exact.
 __device__ __forceinline__ float4 prologue4(const Args& a, float4 v) {
   if (a.divide) return Divisor(a.divisor).div4(v);
-  return scale4(v, a.alpha);
+  v = scale4(v, a.alpha);
+  return a.round_in ? round_fmt4(v, a.fmt) : v;  // bf16/fp16 torch.mul rounds its product
 }
 
 __device__ __forceinline__ float sumsq4(float4 v, float acc) {
@@ -191,7 +192,7 @@ __device__ __forceinline__ void quant_group_rr(const Args& a, const float4 (&w)[
                                                int32_t tensor, float norm, __amdgpu_buffer_rsrc_t rq,
                                                __amdgpu_buffer_rsrc_t ru, int voff) {
   const bool zero = !(norm != 0.0f);
-  const Divisor dv(norm);
+  const Divisor dv(norm, a.fmt);
   auto row = [&](int sl, float4 u) {
     int32_t qq[4];
     qsgd_quad(w[sl], u, dv, a.levels, zero, qq);
@@ -251,8 +252,37 @@ __device__ __forceinline__ uint32_t lds_add(uint32_t* p, uint32_t v) {
 }
 // This wave's LDS writes have landed (LDS only; in-flight global loads stay in flight).
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
-__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t v) {
-  while (ufirst((int)lds_ld(p)) < (int)v) __builtin_amdgcn_s_sleep(1);
+// Per-workgroup abort word (every kernel below zeroes it before its first barrier): set
+// when an LDS wait exceeds its bound.  Every later wait of the workgroup then returns at
+// once, so each wave runs its loops (all bounded by the item count) to the end and the
+// grid drains; err bit 4 makes omf_plan_check report OMF_ETIMEOUT (payload invalid).
+__shared__ uint32_t g_wg_abort;
+
+__device__ __forceinline__ bool wg_aborted() { return ufirst((int)lds_ld(&g_wg_abort)) != 0; }
+
+// Wait until the LDS word *p >= v.  Bounded: the clock is read only every 64 sleeps, so
+// the common short wait costs one LDS load per poll; past a.wait_ticks (20 ms) the
+// workgroup aborts instead of hanging the GPU (a hand-off logic error, never expected).
+// a.lds_wait_ticks is fixed (20 ms); the tunable a.wait_ticks bounds only norm waits.
+__device__ __forceinline__ void lds_wait_ge(const Args& a, const uint32_t* p, uint32_t v) {
+  if (ufirst((int)lds_ld(p)) < (int)v) {
+    uint64_t t0 = 0;
+    for (uint32_t i = 1;; ++i) {
+      __builtin_amdgcn_s_sleep(1);
+      if (ufirst((int)lds_ld(p)) >= (int)v) break;
+      if ((i & 63) == 0) {
+        if (wg_aborted()) break;
+        const uint64_t now = wall_clock64();
+        if (t0 == 0) {
+          t0 = now;
+        } else if (now - t0 > a.lds_wait_ticks) {
+          lds_st(&g_wg_abort, 1u);
+          if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(a.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+  }
   asm volatile("" ::: "memory");
 }
 
@@ -300,7 +330,7 @@ __device__ __forceinline__ bool poll_norm_wave(const Args& a, const Tensor& ti, 
     p += (double)__uint_as_float((uint32_t)g);
   }
   if (!__all(ok)) return false;
-  norm = ufirst(sqrtf((float)wave_sum_f64(p)));
+  norm = ufirst(finish_norm(wave_sum_f64(p), a.fmt));
   return true;
 }
 
@@ -313,6 +343,7 @@ __device__ __forceinline__ float wait_norm_poll(const Args& a, const Tensor& ti,
   float norm;
   for (;;) {
     if (poll_norm_wave(a, ti, lane, norm)) return norm;
+    if (wg_aborted()) return 1.0f;  // the payload is already invalid: just drain
     if (ufirst((int)(wall_clock64() - t0 > a.wait_ticks))) break;
     __builtin_amdgcn_s_sleep(2);
   }
@@ -324,7 +355,7 @@ __device__ __forceinline__ float wait_norm_poll(const Args& a, const Tensor& ti,
     if ((c & 63) == lane) p += (double)part;
   }
   if (lane == 0) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return ufirst(sqrtf((float)wave_sum_f64(p)));
+  return ufirst(finish_norm(wave_sum_f64(p), a.fmt));
 }
 
 // The LDS ring's chunk partial: LW loader-wave partials folded in order.
@@ -371,6 +402,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
     rarrive[t] = 0;
     rgen[t] = (uint32_t)t;  // record r first serves chunk r
   }
+  if (t == 0) g_wg_abort = 0;
   __syncthreads();
   const int64_t G = gridDim.x, n_items = a.n_items;
   const uint64_t t_start = __builtin_readcyclecounter();
@@ -394,9 +426,9 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
       if (!(a.dbg & 2)) draws_at<HAS_U>(a, rg, j, it.begin, it.end, coff, it.tensor, full, uu);
       if (!have_norm) {  // a tile is held, so the slot cannot be recycled under us
         const uint64_t c2 = __builtin_readcyclecounter();
-        lds_wait_ge(&qready[s], (uint32_t)(k + 1));
+        lds_wait_ge(a, &qready[s], (uint32_t)(k + 1));
         norm = ufirst(qnorm[s]);
-        dv = Divisor(norm);
+        dv = Divisor(norm, a.fmt);
         have_norm = true;
         prof.add(4, __builtin_readcyclecounter() - c2);
       }
@@ -477,7 +509,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
       const int r = (int)(k % PR);
       if (it.flags & kPublish) {
         const double wp = wave_sum_f64((double)acc);
-        lds_wait_ge(&rgen[r], (uint32_t)k);  // record free (chunk k-PR folded)
+        lds_wait_ge(a, &rgen[r], (uint32_t)k);  // record free (chunk k-PR folded)
         if (lane == 0) lpart[r][w] = wp;
         lds_drain();
         const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&rarrive[r], 1u) : 0u));
@@ -493,7 +525,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
           }
         }
       } else if (w == 0) {  // QUANT chunk: no partial, retire the record
-        lds_wait_ge(&rgen[r], (uint32_t)k);
+        lds_wait_ge(a, &rgen[r], (uint32_t)k);
         if (lane == 0) lds_st(&rgen[r], (uint32_t)(k + PR));
       }
       prof.add(1, __builtin_readcyclecounter() - c1);
@@ -519,14 +551,14 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
           // Like every claimer: not before all claimers have left the slot's previous use.
           // (freed only says its tiles are done; a late claimer's failing ticket may still
           // be outstanding, and a ticket taken before it would steal this use's tile 0.)
-          lds_wait_ge(&tclaim[s], PER_USE * use);
+          lds_wait_ge(a, &tclaim[s], PER_USE * use);
           claim_tiles(s, use, k - S, prev);  // help quantise it (takes this wave's failing ticket)
         }
         if (ufirst((int)lds_ld(&freed[s])) < (int)(k - S + 1) && DB && idxo < n_items && !pubo) {
           publish(vo, ito, ko);  // never hold an unpublished chunk while waiting
           pubo = true;
         }
-        lds_wait_ge(&freed[s], (uint32_t)(k - S + 1));
+        lds_wait_ge(a, &freed[s], (uint32_t)(k - S + 1));
       }
       prof.add(0, __builtin_readcyclecounter() - c0);
       if (it.flags & kQuant) {
@@ -619,7 +651,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
       }
       const uint64_t c1 = __builtin_readcyclecounter();
       prof.add(3, c1 - c0);
-      lds_wait_ge(&loaded[s], (uint32_t)(k + 1));  // the slot's previous chunk is finished
+      lds_wait_ge(a, &loaded[s], (uint32_t)(k + 1));  // the slot's previous chunk is finished
       prof.add(2, __builtin_readcyclecounter() - c1);
       if (lane == 0) {
         qnorm[s] = norm;
@@ -646,7 +678,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
       // slot fills and the norm resolves (the data is read only after qready, which the
       // poller sets after `loaded`, which the loaders set after every tile of the slot's
       // previous use is finished).
-      lds_wait_ge(&tclaim[s], PER_USE * use);  // every claimer has left the slot's previous use
+      lds_wait_ge(a, &tclaim[s], PER_USE * use);  // every claimer has left the slot's previous use
       prof.add(2, __builtin_readcyclecounter() - c0);
       claim_tiles(s, use, k, it);
     }
@@ -715,6 +747,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr(Args a, const Item* __
     qdone[t] = 0;
     qnorm[t] = 0.0f;
   }
+  if (t == 0) g_wg_abort = 0;
   __syncthreads();
   const int64_t G = gridDim.x, n_items = a.n_items;
   const int64_t npos = (n_items - (int64_t)blockIdx.x + G - 1) / G;
@@ -755,7 +788,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr(Args a, const Item* __
       for (int sl = 0; sl < 4; ++sl) acc = sumsq4(v[sl], acc);
       const double wp = wave_sum_f64((double)acc);
       const int r = (int)(npub % PR);
-      lds_wait_ge(&rgen[r], npub);  // record free (publish npub - PR folded)
+      lds_wait_ge(a, &rgen[r], npub);  // record free (publish npub - PR folded)
       if (lane == 0) lpart[r][wave] = wp;
       lds_drain();
       const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&rarrive[r], 1u) : 0u));
@@ -794,7 +827,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr(Args a, const Item* __
       }
     }
     if (!__all(ok)) return false;
-    norm = ufirst(sqrtf((float)wave_sum_f64(sum)));
+    norm = ufirst(finish_norm(wave_sum_f64(sum), a.fmt));
     return true;
   };
   auto resolve = [&](const Item& it) __attribute__((always_inline)) -> float {
@@ -809,14 +842,14 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr(Args a, const Item* __
       if (!ok)
         norm = wait_norm_poll(a, tensor_of(it), lane, CH,
                               [&](int64_t cb, int n) { return rr_chunk_partial(a, cb, n, lane); });
-      lds_wait_ge(&qdone[s], (uint32_t)(NW - 1) * use);
+      lds_wait_ge(a, &qdone[s], (uint32_t)(NW - 1) * use);
       if (lane == 0) {
         qnorm[s] = norm;
         lds_drain();
         lds_st(&qflag[s], use + 1);
       }
     } else {
-      lds_wait_ge(&qflag[s], use + 1);
+      lds_wait_ge(a, &qflag[s], use + 1);
       norm = ufirst(qnorm[s]);
       if (lane == 0) lds_add(&qdone[s], 1u);
     }
@@ -906,6 +939,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr2(Args a, const Item* _
     qdone[t] = 0;
     qnorm[t] = 0.0f;
   }
+  if (t == 0) g_wg_abort = 0;
   __syncthreads();
   const int64_t G = gridDim.x, n_items = a.n_items;
   const int64_t npos = (n_items - (int64_t)blockIdx.x + G - 1) / G;
@@ -946,7 +980,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr2(Args a, const Item* _
       for (int sl = 0; sl < 4; ++sl) acc = sumsq4(v[sl], acc);
       const double wp = wave_sum_f64((double)acc);
       const int r = (int)(npub % PR);
-      lds_wait_ge(&rgen[r], npub);  // record free (publish npub - PR folded)
+      lds_wait_ge(a, &rgen[r], npub);  // record free (publish npub - PR folded)
       if (lane == 0) lpart[r][wave] = wp;
       lds_drain();
       const uint32_t old = ufirst((int)(lane == 0 ? lds_add(&rarrive[r], 1u) : 0u));
@@ -989,7 +1023,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr2(Args a, const Item* _
       }
     }
     if (!__all(ok)) return false;
-    norm = ufirst(sqrtf((float)wave_sum_f64(sum)));
+    norm = ufirst(finish_norm(wave_sum_f64(sum), a.fmt));
     return true;
   };
   auto resolve_early = [&](int64_t p) __attribute__((always_inline)) {
@@ -1006,7 +1040,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr2(Args a, const Item* _
       if (!ok)
         norm = wait_norm_poll(a, tensor_of(it), lane, CH,
                               [&](int64_t cb, int n) { return rr_chunk_partial(a, cb, n, lane); });
-      lds_wait_ge(&qdone[s], (uint32_t)(NW - 1) * use);
+      lds_wait_ge(a, &qdone[s], (uint32_t)(NW - 1) * use);
       if (lane == 0) {
         qnorm[s] = norm;
         lds_drain();
@@ -1023,7 +1057,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_rr2(Args a, const Item* _
     const int64_t n = it.end - it.begin;
     if (it.flags & kQuant) {
       if (rd_slot >= 0) {
-        lds_wait_ge(&qflag[rd_slot], rd_use + 1);
+        lds_wait_ge(a, &qflag[rd_slot], rd_use + 1);
         cached_norm = ufirst(qnorm[rd_slot]);
         if (lane == 0) lds_add(&qdone[rd_slot], 1u);
         rd_slot = -1;

@@ -48,8 +48,11 @@ struct Args {
   uint32_t divide;
   float* xout;
   uint32_t seed_lo, seed_hi, offset;
+  uint32_t fmt;       // value format (omf_qsgd_dev.h kFmt*): rounding of norm and v / norm
+  uint32_t round_in;  // fmt != F32 and alpha != 1: the weighted input is rounded to fmt
   uint32_t epoch;  // per-launch granule tag (never 0)
-  uint64_t wait_ticks;
+  uint64_t wait_ticks;      // bound of a norm wait (tunable: tests force the recompute fallback)
+  uint64_t lds_wait_ticks;  // bound of an on-chip LDS hand-off wait (fixed 20 ms; expiry aborts)
   uint32_t dbg;  // experiment switches: 1 = no norm wait (norm := 1), 2 = no quantisation, 4 = time phases
   unsigned long long* prof;  // dbg & 4: per-phase cycle totals (omf_plan_ring_profile)
 };

@@ -523,6 +523,41 @@ __global__ __launch_bounds__(kThreads) void topk_scatter(const float* __restrict
   }
 }
 
+// Whole-arena decode of one client's selection (values/indices packed per tensor at
+// K_t = sum_{u<t} k_u, tensor-local indices): y[begin_t + idx] = v (mode 0/1) or += v (2).
+// Indices are unique within a client, so the read-modify-write needs no atomics.
+constexpr int kArenaMaxTensors = 4096;
+__global__ __launch_bounds__(kThreads) void topk_scatter_arena(const float* __restrict__ values,
+                                                               const int64_t* __restrict__ indices,
+                                                               const int64_t* __restrict__ sizes,
+                                                               const int64_t* __restrict__ begins, int nt,
+                                                               double ratio, int64_t ktot, float* __restrict__ y,
+                                                               int add) {
+  __shared__ int64_t koff[kArenaMaxTensors + 1];
+  if (threadIdx.x == 0) {  // k_t exactly as omf_topk_k, prefix-summed (nt is small)
+    int64_t acc = 0;
+    for (int t = 0; t < nt; ++t) {
+      koff[t] = acc;
+      const int64_t k = (int64_t)((double)sizes[t] * ratio);
+      acc += k < 1 ? 1 : k;
+    }
+    koff[nt] = acc;
+  }
+  __syncthreads();
+  for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < ktot; j += (int64_t)gridDim.x * kThreads) {
+    int lo = 0, hi = nt - 1;  // the tensor t with koff[t] <= j < koff[t + 1]
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (koff[mid] <= j) lo = mid;
+      else hi = mid - 1;
+    }
+    const int64_t i = indices[j];
+    if (i < 0 || i >= sizes[lo]) continue;  // padding (-1) or out of range: skipped
+    float* p = y + begins[lo] + i;
+    *p = add ? __fadd_rn(*p, values[j]) : values[j];
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- host side
@@ -744,6 +779,32 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   else
     hipLaunchKernelGGL((topk_gather<false>), dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted_keys, d_begins,
                        cstart, kk, koff, values, indices);
+  OMF_HIP(hipGetLastError());
+  return OMF_OK;
+}
+
+int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
+                          int32_t mode, void* stream) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (mode < 0 || mode > 2) return fail(OMF_EINVAL, "omf_topk_decode_arena: mode must be 0, 1 or 2");
+  if (!(ratio == ratio)) return fail(OMF_EINVAL, "ratio is NaN");
+  if (!values || !indices || !y) return fail(OMF_EINVAL, "omf_topk_decode_arena: NULL buffer");
+  const int32_t nt = omf_plan_access::ntensors(plan);
+  if (nt > kArenaMaxTensors) return fail(OMF_EINVAL, "omf_topk_decode_arena: too many tensors (decode per tensor)");
+  int64_t ktot = 0;
+  for (int64_t n : omf_plan_access::sizes(plan)) {
+    const int64_t k = omf_topk_k(n, ratio);
+    if (k > n) return fail(OMF_EINVAL, "selected index k out of range (k > numel): compress_ratio too large");
+    ktot += k;
+  }
+  DeviceGuard g(omf_plan_access::device(plan));
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  hipStream_t st = (hipStream_t)stream;
+  if (mode == 0) OMF_HIP(hipMemsetAsync(y, 0, 4 * (size_t)omf_plan_access::arena_end(plan), st));
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ktot + kThreads - 1) / kThreads, 4096));
+  hipLaunchKernelGGL(topk_scatter_arena, dim3(gx), dim3(kThreads), 0, st, values, indices,
+                     omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (int)nt, ratio, ktot, y,
+                     mode == 2 ? 1 : 0);
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }

@@ -130,7 +130,7 @@ def hybrid_global_compressor_from_cfg(cfg, device="cpu") -> Optional[GlobalHybri
 
 def _encode_dense_layer(name: str, tensor: torch.Tensor):
     """global_grpc_compression.py:76-81."""
-    layer = global_grpc_pb2.LayerState(layer_name=name)
+    layer = global_grpc_pb2.layer_state(layer_name=name)
     t = tensor.detach().cpu()
     layer.param_shape.extend(list(t.shape))
     layer.param_update.extend(t.flatten().tolist())
@@ -139,7 +139,7 @@ def _encode_dense_layer(name: str, tensor: torch.Tensor):
 
 def qsgd_layer_from_payload(name: str, shape, payload: bytes, norm: float, width: int, levels: int):
     """The QSGD ``LayerState`` of global_grpc_compression.py:111-123 from an encoded payload."""
-    layer = global_grpc_pb2.LayerState(layer_name=name)
+    layer = global_grpc_pb2.layer_state(layer_name=name)
     layer.compression_type = QSGD_COMPRESSION_NAME
     layer.values_data = payload
     layer.values_dtype = f"torch.int{width}"
@@ -154,7 +154,7 @@ def qsgd_layer_from_payload(name: str, shape, payload: bytes, norm: float, width
 def qsgd_packed_layer_from_payload(name: str, shape, packed: bytes, norm: float, levels: int):
     """The opt-in bit-packed QSGD ``LayerState``: the fields of the QSGD layer with
     ``values_data`` = the codes q + L in ``width`` = ceil(log2(2L+1)) bits each, LSB first."""
-    layer = global_grpc_pb2.LayerState(layer_name=name)
+    layer = global_grpc_pb2.layer_state(layer_name=name)
     layer.compression_type = QSGD_PACKED_COMPRESSION_NAME
     layer.values_data = packed
     bits = codec.packed_bits(levels)
@@ -185,7 +185,7 @@ def _packed_slice(host: np.ndarray, offset: int, n: int, levels: int) -> bytes:
 
 def topk_layer_from_payload(name: str, shape, values: np.ndarray, indices: np.ndarray):
     """The Top-K ``LayerState`` of global_grpc_compression.py:88-98."""
-    layer = global_grpc_pb2.LayerState(layer_name=name)
+    layer = global_grpc_pb2.layer_state(layer_name=name)
     layer.compression_type = TOPK_COMPRESSION_NAME
     layer.values_data = np.ascontiguousarray(values, dtype=np.float32).tobytes()
     layer.indices_data = np.ascontiguousarray(indices, dtype=np.int64).tobytes()
@@ -195,33 +195,47 @@ def topk_layer_from_payload(name: str, shape, values: np.ndarray, indices: np.nd
     return layer
 
 
-def _encode_topk_layer(name: str, tensor: torch.Tensor, compressor: TopKCompression):
-    (values, indices), _ctx = compressor.compress(tensor.detach(), name=name)
+def _weighted(tensor: torch.Tensor, weight) -> torch.Tensor:
+    """``torch.mul(tensor, batch_samples)`` of GrpcCommunicator.aggregate (global_grpc.py:104, 121)."""
+    return tensor if weight is None else torch.mul(tensor.detach(), weight)
+
+
+def _alpha(weight) -> float:
+    return 1.0 if weight is None else float(weight)
+
+
+def _encode_topk_layer(name: str, tensor: torch.Tensor, compressor: TopKCompression, weight=None):
+    (values, indices), _ctx = compressor.compress_weighted(tensor.detach(), name, _alpha(weight))
     return topk_layer_from_payload(name, tuple(tensor.shape), values.detach().cpu().numpy(),
                                    indices.detach().cpu().numpy())
 
 
-def _encode_qsgd_layer(name: str, tensor: torch.Tensor, compressor: QSGDQuantCompression):
+def _encode_qsgd_layer(name: str, tensor: torch.Tensor, compressor: QSGDQuantCompression, weight=None):
     """global_grpc_compression.py:101-123, payload produced on the GPU."""
     if not should_compress_tensor(tensor):
-        return _encode_dense_layer(name, tensor)
-    if getattr(compressor, "packed_wire", False):
-        return encode_updates_dict({name: tensor}, compressor)[0]
-    (q, norm, width, levels), = compressor.encode_flat([tensor.detach().reshape(-1)])
+        return _encode_dense_layer(name, _weighted(tensor, weight))
+    if getattr(compressor, "packed_wire", False) or tensor.dtype != torch.float32:
+        return encode_updates_dict({name: tensor}, compressor, weight=weight)[0]
+    (q, norm, width, levels), = compressor.encode_flat([tensor.detach().reshape(-1)], alpha=_alpha(weight))
     if width == -1:
-        return _encode_dense_layer(name, tensor)
+        return _encode_dense_layer(name, _weighted(tensor, weight))
     payload = q.cpu().numpy().tobytes()
     return qsgd_layer_from_payload(name, tuple(tensor.shape), payload, norm, width, levels)
 
 
-def encode_layer_state(name: str, tensor: torch.Tensor, compressor: Optional[GlobalHybridCompressor]):
-    """global_grpc_compression.py:126-137."""
+def encode_layer_state(name: str, tensor: torch.Tensor, compressor: Optional[GlobalHybridCompressor], *,
+                       weight=None):
+    """global_grpc_compression.py:126-137.
+
+    ``weight`` (optional, ours): encode ``torch.mul(tensor, weight)`` — the client weighting
+    ``param * batch_samples`` of GrpcCommunicator.aggregate (global_grpc.py:101-123) — with the
+    multiply fused into the GPU encoder (same bits as multiplying first)."""
     if compressor is None:
-        return _encode_dense_layer(name, tensor)
+        return _encode_dense_layer(name, _weighted(tensor, weight))
     if isinstance(compressor, TopKCompression):
-        return _encode_topk_layer(name, tensor, compressor)
+        return _encode_topk_layer(name, tensor, compressor, weight)
     if isinstance(compressor, QSGDQuantCompression):
-        return _encode_qsgd_layer(name, tensor, compressor)
+        return _encode_qsgd_layer(name, tensor, compressor, weight)
     raise TypeError(f"Unsupported compressor type: {type(compressor)!r}")
 
 
@@ -343,10 +357,13 @@ def decode_layer_tensor(layer, *, base_tensor: Optional[torch.Tensor] = None, de
 
 # ---------------------------------------------------------------- dict helpers (batched)
 
-def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[GlobalHybridCompressor]) -> list:
-    """global_grpc_compression.py:207-211; QSGD tensors go through ONE batched launch."""
+def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[GlobalHybridCompressor], *,
+                        weight=None) -> list:
+    """global_grpc_compression.py:207-211; QSGD tensors go through ONE batched launch.
+
+    ``weight``: as encode_layer_state (the client's ``batch_samples``, fused into the encoder)."""
     if not isinstance(compressor, QSGDQuantCompression):
-        return [encode_layer_state(name, tensor, compressor) for name, tensor in updates.items()]
+        return [encode_layer_state(name, tensor, compressor, weight=weight) for name, tensor in updates.items()]
     names = list(updates.keys())
     comp_idx = [i for i, n in enumerate(names) if should_compress_tensor(updates[n])]
     results = {}
@@ -355,25 +372,28 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
             raise ValueError(f"QSGD bit_width={compressor.s} out of range [0, 30]")
         flats = [updates[names[i]].detach().reshape(-1) for i in comp_idx]
         dev = compute_device(flats[0], compressor.device)
-        from ..compression.qsgd import encode_many
+        from ..compression.qsgd import encode_groups
 
-        plan, q, norms = encode_many(flats, compressor.s, dev, compressor.rng, compressor._next_call())
+        groups = encode_groups(flats, compressor.s, dev, compressor.rng, compressor._next_call(),
+                               alpha=_alpha(weight), key=compressor.philox_key())
         levels = 2**compressor.s
         width, _ = choose_qsgd_storage_width(levels)
-        if compressor.packed_wire:  # pack on the GPU; (b/8) bytes per element cross PCIe
-            p_host = _packed_host(plan, q, width, levels)
-            host_norms = norms.cpu().tolist()
-            for i, o, n, nv in zip(comp_idx, plan.offsets, plan.sizes, host_norms):
-                if nv != 0:
-                    results[i] = (_packed_slice(p_host, o, n, levels), nv)
-        else:
-            staged = _STAGING.get("encode", q.numel() * q.element_size()).view(q.dtype)
-            staged.copy_(q, non_blocking=True)  # one D2H of the payload arena (w bytes per element)
-            host_norms = norms.cpu().tolist()  # synchronises the stream: the payload copy has landed
-            q_host = staged.numpy()
-            for i, o, n, nv in zip(comp_idx, plan.offsets, plan.sizes, host_norms):
-                if nv != 0:
-                    results[i] = (q_host[o:o + n].tobytes(), nv)
+        for plan, q, norms, members in groups:  # one group per dtype (normally one)
+            idx = [comp_idx[m] for m in members]
+            if compressor.packed_wire:  # pack on the GPU; (b/8) bytes per element cross PCIe
+                p_host = _packed_host(plan, q, width, levels)
+                host_norms = norms.cpu().tolist()
+                for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, host_norms):
+                    if nv != 0:
+                        results[i] = (_packed_slice(p_host, o, n, levels), nv)
+            else:
+                staged = _STAGING.get("encode", q.numel() * q.element_size()).view(q.dtype)
+                staged.copy_(q, non_blocking=True)  # one D2H of the payload arena (w bytes per element)
+                host_norms = norms.cpu().tolist()  # synchronises the stream: the payload copy has landed
+                q_host = staged.numpy()
+                for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, host_norms):
+                    if nv != 0:
+                        results[i] = (q_host[o:o + n].tobytes(), nv)  # bytes are copies: staging reusable
     layers = []
     for i, name in enumerate(names):
         t = updates[name]
@@ -386,7 +406,7 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
             else:
                 layers.append(qsgd_layer_from_payload(name, tuple(t.shape), payload, nv, width, levels))
         else:
-            layers.append(_encode_dense_layer(name, t))
+            layers.append(_encode_dense_layer(name, _weighted(t, weight)))
     return layers
 
 

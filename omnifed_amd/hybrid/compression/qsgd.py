@@ -8,20 +8,28 @@ GPU and its payload returned on the CPU, as ``_do_compress`` returns it on
 ``tensor.device``, qsgd.py:69).
 
 Random draws (``rng``):
-  * ``"philox"`` (default): on-device Philox4x32-10 keyed by a 63-bit seed drawn
-    from torch's default CPU generator per call — so ``torch.manual_seed`` makes
-    runs reproducible, as in the reference — plus a per-compressor call counter.
+  * ``"philox"`` (default): on-device Philox4x32-10 keyed by (``torch.initial_seed()``,
+    the compressor's creation index) with the per-compressor call counter as the
+    stream offset — so ``torch.manual_seed`` makes runs reproducible, as in the
+    reference, and the caller's CPU generator is never advanced (the reference's
+    ``rand_like`` consumes n of its draws per tensor; this codec consumes none, so
+    data shuffling or CPU dropout after a swap sees a different generator state).
     Statistically the reference's ``rand_like`` (24-bit uniforms), not the same bits.
   * ``"mt19937"``: the reference's own stream: ``torch.rand`` on the default CPU
     generator, consumed tensor by tensor and skipped for zero-norm tensors
     (qsgd.py:47-48, 58), handed to the kernel as an input buffer.  Bit-identical
     payloads follow whenever the norm equals the reference's (its fp32
     ``torch.norm`` is ISA dependent).
+
+Dtypes: the reference quantises in the tensor's own dtype.  float32, bfloat16 and
+float16 tensors are encoded with that dtype's rounding (``omf_qsgd_encode_ex``
+value formats); float64 tensors raise ``ValueError`` (no fp64 encoder).
 """
 
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+import itertools
+from typing import Dict, List, Sequence, Tuple
 
 import torch
 
@@ -46,37 +54,90 @@ def choose_qsgd_storage_width(levels: int) -> tuple:
     return 32, torch.int32
 
 
-def encode_many(flats: Sequence[torch.Tensor], bit_width: int, dev: torch.device, rng: str = "philox",
-                call_index: int = 0, alpha: float = 1.0, chunk: int = 0):
-    """Encode several flat tensors in ONE launch.
+_VALUE_FORMATS = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
 
-    Returns ``(plan, q_arena, norms_dev)``: tensor i's levels are
-    ``q_arena[plan.offsets[i] : plan.offsets[i] + plan.sizes[i]]``.
-    """
-    sizes = [int(f.numel()) for f in flats]
-    plan = codec.Plan.get(sizes, device=dev, chunk=chunk)
+
+def value_format(dtype: torch.dtype) -> int:
+    """The encoder's value format for a tensor dtype (omf_qsgd_encode_ex): 0 fp32, 1 bf16, 2 fp16."""
+    fmt = _VALUE_FORMATS.get(dtype)
+    if fmt is None:
+        raise ValueError(f"QSGD on the MI355X codec encodes float32, bfloat16 and float16 tensors, not {dtype}")
+    return fmt
+
+
+def _arena(flats: Sequence[torch.Tensor], dev: torch.device, plan) -> torch.Tensor:
     if len(flats) == 1:
-        x = to_arena(flats[0], dev, plan)
-    else:
-        x = torch.empty(plan.arena_end, dtype=torch.float32, device=dev)
-        for f, o, n in zip(flats, plan.offsets, sizes):
-            x[o:o + n].copy_(f.detach().reshape(-1))
-    s = int(bit_width)
-    if rng == "mt19937":
-        norms = plan.qsgd_norms(x, alpha=alpha)
-        host_norms = norms.cpu().tolist()
-        u_host = torch.zeros(plan.arena_end, dtype=torch.float32)
-        for o, n, nv in zip(plan.offsets, sizes, host_norms):
-            if nv != 0:
-                u_host[o:o + n] = torch.rand(n)
-        u = u_host.to(dev)
-        q, norms = plan.qsgd_encode(x, s, alpha=alpha, u=u, norm_in=norms)
-    elif rng == "philox":
-        seed = int(torch.randint(0, 2**62, (1,)).item())
-        q, norms = plan.qsgd_encode(x, s, alpha=alpha, seed=seed, offset=call_index)
-    else:
+        return to_arena(flats[0], dev, plan)
+    x = torch.empty(plan.arena_end, dtype=torch.float32, device=dev)
+    for f, o, n in zip(flats, plan.offsets, plan.sizes):
+        x[o:o + n].copy_(f.detach().reshape(-1))  # bf16/fp16 -> fp32 is exact
+    return x
+
+
+def encode_groups(flats: Sequence[torch.Tensor], bit_width: int, dev: torch.device, rng: str = "philox",
+                  call_index: int = 0, alpha: float = 1.0, chunk: int = 0, key: int = 0):
+    """Encode flat tensors, ONE launch per dtype present (normally one).
+
+    Returns ``[(plan, q_arena, norms_dev, members)]`` in order of first appearance:
+    ``members[k]`` is the index into ``flats`` of the plan's tensor k (levels at
+    ``q_arena[plan.offsets[k] : + plan.sizes[k]]``).  ``mt19937``: the uniforms are drawn
+    tensor by tensor in ``flats`` order across the groups, skipping zero norms.
+    ``philox``: key = ``key`` (+ the group's index), stream offset = ``call_index``.
+    """
+    if rng not in ("philox", "mt19937"):
         raise ValueError(f"unknown rng={rng!r}; expected 'philox' or 'mt19937'")
+    members: Dict[torch.dtype, List[int]] = {}
+    for i, f in enumerate(flats):
+        value_format(f.dtype)
+        members.setdefault(f.dtype, []).append(i)
+    groups = []
+    for dt, idx in members.items():
+        plan = codec.Plan.get([int(flats[i].numel()) for i in idx], device=dev, chunk=chunk)
+        groups.append((plan, _arena([flats[i] for i in idx], dev, plan), value_format(dt), idx))
+    s = int(bit_width)
+    out = []
+    if rng == "mt19937":
+        norms = [plan.qsgd_norms(x, alpha=alpha, value_format=fmt) for plan, x, fmt, _ in groups]
+        host = [n.cpu().tolist() for n in norms]
+        where = {i: (g, k) for g, (_, _, _, idx) in enumerate(groups) for k, i in enumerate(idx)}
+        u_host = [torch.zeros(plan.arena_end, dtype=torch.float32) for plan, _, _, _ in groups]
+        for i in range(len(flats)):  # the reference's draw order: tensor by tensor
+            g, k = where[i]
+            plan = groups[g][0]
+            if host[g][k] != 0:
+                o, n = plan.offsets[k], plan.sizes[k]
+                u_host[g][o:o + n] = torch.rand(n)
+        for (plan, x, fmt, idx), nd, uh in zip(groups, norms, u_host):
+            q, nd = plan.qsgd_encode(x, s, alpha=alpha, u=uh.to(dev), norm_in=nd, value_format=fmt)
+            out.append((plan, q, nd, idx))
+    else:
+        for g, (plan, x, fmt, idx) in enumerate(groups):
+            q, nd = plan.qsgd_encode(x, s, alpha=alpha, seed=(int(key) + g) & (2**64 - 1), offset=call_index,
+                                     value_format=fmt)
+            out.append((plan, q, nd, idx))
+    return out
+
+
+def encode_many(flats: Sequence[torch.Tensor], bit_width: int, dev: torch.device, rng: str = "philox",
+                call_index: int = 0, alpha: float = 1.0, chunk: int = 0, key: int = 0):
+    """Encode flat tensors of ONE dtype in one launch: ``(plan, q_arena, norms_dev)``."""
+    groups = encode_groups(flats, bit_width, dev, rng, call_index, alpha, chunk, key)
+    if len(groups) != 1:
+        raise ValueError("encode_many: the tensors must share one dtype (use encode_groups)")
+    plan, q, norms, _ = groups[0]
     return plan, q, norms
+
+
+_INSTANCES = itertools.count()
+
+
+def philox_key(instance: int) -> int:
+    """64-bit Philox key of a compressor: splitmix64 of (torch.initial_seed(), creation index)."""
+    z = (int(torch.initial_seed()) * 0x9E3779B97F4A7C15 + int(instance) * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB)
+    z &= 2**64 - 1
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+    return z ^ (z >> 31)
 
 
 class QSGDQuantCompression(Compression):
@@ -91,6 +152,11 @@ class QSGDQuantCompression(Compression):
             raise ValueError(f"unknown rng={rng!r}; expected 'philox' or 'mt19937'")
         self.rng = rng
         self._calls = 0
+        self._instance = next(_INSTANCES)
+
+    def philox_key(self) -> int:
+        """The Philox key of this compressor (see the module docstring)."""
+        return philox_key(self._instance)
 
     def _next_call(self) -> int:
         c = self._calls
@@ -107,9 +173,11 @@ class QSGDQuantCompression(Compression):
             return torch.zeros_like(v), -1, -1, -1
         return q.to(v.device), norm, width, levels
 
-    def encode_flat(self, flats: List[torch.Tensor]) -> List[Tuple]:
+    def encode_flat(self, flats: List[torch.Tensor], alpha: float = 1.0) -> List[Tuple]:
         """Batched ``quantize_vector``: one launch for every tensor (all must be non-empty floats).
 
+        ``alpha``: the client weighting ``param * batch_samples`` of GrpcCommunicator.aggregate
+        (global_grpc.py:101-123), fused into the encoder: the levels are those of fl32(alpha * x).
         Returns a ``(q_device_view, norm, width, levels)`` per tensor, or
         ``(None, -1, -1, -1)`` for a zero norm.
         """
@@ -117,16 +185,13 @@ class QSGDQuantCompression(Compression):
             # levels = 2**s must fit LayerState.level (int32); the reference fails there too.
             raise ValueError(f"QSGD bit_width={self.s} out of range [0, 30]")
         dev = compute_device(flats[0], self.device)
-        plan, q, norms = encode_many(flats, self.s, dev, self.rng, self._next_call())
+        groups = encode_groups(flats, self.s, dev, self.rng, self._next_call(), alpha=alpha, key=self.philox_key())
         levels = 2**self.s
         width, _ = choose_qsgd_storage_width(levels)
-        host_norms = norms.cpu().tolist()
-        out = []
-        for o, n, nv in zip(plan.offsets, plan.sizes, host_norms):
-            if nv == 0:
-                out.append((None, -1, -1, -1))
-            else:
-                out.append((q[o:o + n], float(nv), width, levels))
+        out: List[Tuple] = [None] * len(flats)
+        for plan, q, norms, idx in groups:
+            for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, norms.cpu().tolist()):
+                out[i] = (None, -1, -1, -1) if nv == 0 else (q[o:o + n], float(nv), width, levels)
         return out
 
     def _do_compress(self, tensor: torch.Tensor):

@@ -48,6 +48,18 @@ class TopKCompression(Compression):
         self.compress_ratio = float(compress_ratio)
 
     def compress(self, tensor: torch.Tensor, name: str):
+        """topk.py:33-42: ``((values, indices), (numel, shape))``; mutates the residual of ``name``."""
+        return self.compress_weighted(tensor, name, 1.0)
+
+    def compress_weighted(self, tensor: torch.Tensor, name: str, alpha: float):
+        """``compress(fl32(alpha * tensor), name)`` with the weighting fused into the encoder (the
+        client weighting param * batch_samples, global_grpc.py:101-123)."""
+        if tensor.is_floating_point() and tensor.dtype != torch.float32:
+            # The reference selects and keeps its residual in the tensor's dtype; this codec's Top-K
+            # is fp32 (integer tensors are selected on their exact fp32 values, as the wire's
+            # astype(float32) sends them; a bf16 tensor fails in the reference's wire encode anyway:
+            # numpy has no bfloat16).
+            raise ValueError(f"Top-K on the MI355X codec encodes float32 (or integer) tensors, not {tensor.dtype}")
         dev = compute_device(tensor, self.device)
         numel = tensor.numel()
         shape = tensor.size()
@@ -61,7 +73,8 @@ class TopKCompression(Compression):
         mode = 1 if res is not None else 2
         if res is None:
             res = torch.empty(numel, dtype=torch.float32, device=dev)
-        values, indices, _ = plan.topk_encode(x, self.compress_ratio, residual=res, residual_mode=mode)
+        values, indices, _ = plan.topk_encode(x, self.compress_ratio, residual=res, residual_mode=mode,
+                                              alpha=float(alpha))
         self.residual.residuals[name] = res
         ctx = (numel, shape)
         return (values.to(self.device), indices.to(self.device)), ctx

@@ -10,12 +10,20 @@ total sample count.  Clients are summed in call (= arrival) order, as the refere
 
 Several GPUs of one node (one synthetic client per rank) — the
 weighted sum Σ_i decode(Q(w_i·x_i)) / Σ_i w_i is the path's only exchange step:
+* ``qsgd_weighted_round``: each rank encodes its client with the weighting fused
+  (alpha = w_i, global_grpc.py:101-123), then one of
 * ``weighted_sum_reduce``: each rank decodes its own payload, then one RCCL
   ``reduce(SUM)`` of the fp32 arena to the root, which divides by Σw;
 * ``weighted_sum_gather``: RCCL ``gather`` of the int8/int32 payloads + norms to
   the root (w/4 of the fp32 bytes over xGMI), which decode-accumulates them in
   rank order (deterministic) and divides.
-Both take an ``ops`` object so the orchestration is testable with gloo on CPU.
+Top-K across GPUs (``topk_sparse_aggregate``): the reference's sparse aggregate
+(torch_mpi.py:302-359 → core.layerwise_decompress, core.py:62-71): every rank's
+(values, indices) all-gathered (or gathered to one root), scatter-added in rank order
+and divided by the client count.  Every rank selects k = max(1, int(n·ratio)) per
+tensor of the same plan, so no padding is needed (the reference pads to the largest
+k with index 0 / value 0, which is a no-op whenever the k agree).
+All of them take an ``ops`` object so the orchestration is testable with gloo on CPU.
 """
 
 from __future__ import annotations
@@ -33,14 +41,27 @@ from .shapes import numel
 class GpuOps:
     """The device operations the PS steps use (HIP C ABI)."""
 
-    def __init__(self, plan: "codec.Plan"):
+    def __init__(self, plan: "codec.Plan", seed: int = 0):
         self.plan = plan
+        self.seed = int(seed)
+
+    def encode(self, x, bit_width, alpha, call, q=None, norms=None):
+        """Q(fl32(alpha·x)) of the whole arena (Philox keyed by ``seed``, stream ``call``)."""
+        return self.plan.qsgd_encode(x, bit_width, q_out=q, norm_out=norms, alpha=alpha, seed=self.seed, offset=call)
 
     def decode(self, q, width, levels, norms, y, accumulate):
         return self.plan.qsgd_decode(q, width, levels, norms, y_out=y, accumulate=accumulate)
 
     def div_(self, y, d):
         return codec.div_(y, d)
+
+    def topk_encode(self, x, ratio, residual, residual_mode, alpha, values=None, indices=None):
+        values, indices, _ = self.plan.topk_encode(x, ratio, residual=residual, residual_mode=residual_mode,
+                                                   values=values, indices=indices, alpha=alpha)
+        return values, indices
+
+    def topk_decode(self, values, indices, ratio, y, mode):
+        return self.plan.topk_decode_arena(values, indices, ratio, y=y, mode=mode)
 
 
 class DeviceAggregator:
@@ -55,10 +76,9 @@ class DeviceAggregator:
         self.index = {n: i for i, n in enumerate(self.names)}
         self.compute_mean = compute_mean
         self.acc = torch.zeros(self.plan.arena_end, dtype=torch.float32, device=self.device)
+        self.avg: Optional[torch.Tensor] = None  # the fused step's output arena (disjoint from acc)
         self.update_count = 0
         self.total_samples = 0
-        self._q8 = None
-        self._q32 = None
 
     def reset(self):
         """_initialize_accumulated_updates (global_grpc_server.py:58-62)."""
@@ -70,6 +90,11 @@ class DeviceAggregator:
         i = self.index[name]
         o, n = self.plan.offsets[i], self.plan.sizes[i]
         return self.acc[o:o + n]
+
+    def _avg_slice(self, name):
+        i = self.index[name]
+        o, n = self.plan.offsets[i], self.plan.sizes[i]
+        return self.avg[o:o + n]
 
     def accumulate_layers(self, layers, number_samples: int = 0):
         """Decode one client's update into the accumulator (global_grpc_server.py:108-111, 147-153)."""
@@ -111,6 +136,47 @@ class DeviceAggregator:
         self.update_count += 1
         self.total_samples += int(number_samples)
 
+    def accumulate_updates(self, updates: Dict[str, torch.Tensor], compressor, number_samples: int = 0,
+                           weight=None):
+        """One in-process client's whole round trip into the accumulator, without the wire:
+        ``encode_updates_dict(updates, compressor, weight=weight)`` then ``accumulate_layers`` —
+        for a QSGD compressor as ONE weighted encode launch (alpha = weight) and ONE
+        decode-accumulate launch on the device (no host copy).  Bit-identical to the wire path
+        for the same draws (same kernels, same payload and norms)."""
+        from .hybrid.compression.qsgd import QSGDQuantCompression, encode_groups, should_compress_tensor
+
+        names = [n for n in self.names if n in updates]
+        if (not isinstance(compressor, QSGDQuantCompression) or compressor.packed_wire
+                or not all(should_compress_tensor(updates[n]) and updates[n].dtype == torch.float32 for n in names)
+                or [n for n in updates if n not in self.index]):
+            from .hybrid.communicator.global_grpc_compression import encode_updates_dict
+            return self.accumulate_layers(encode_updates_dict(updates, compressor, weight=weight), number_samples)
+        x = torch.zeros(self.plan.arena_end, dtype=torch.float32, device=self.device)
+        for n in names:
+            i = self.index[n]
+            x[self.plan.offsets[i]:self.plan.offsets[i] + self.plan.sizes[i]].copy_(updates[n].detach().reshape(-1))
+        alpha = 1.0 if weight is None else float(weight)
+        if compressor.rng == "philox":
+            q, norms = self.plan.qsgd_encode(x, compressor.s, alpha=alpha, seed=compressor.philox_key(),
+                                             offset=compressor._next_call())
+        else:  # the reference's MT19937 stream over the named tensors present, in order
+            flats = [updates[n].detach().reshape(-1) for n in names]
+            (plan, qg, ng, _), = encode_groups(flats, compressor.s, self.device, "mt19937", compressor._next_call(),
+                                              alpha=alpha)
+            q = torch.zeros(self.plan.payload_elems(8 if 2**compressor.s <= 127 else 32), dtype=qg.dtype,
+                            device=self.device)
+            norms = torch.zeros(self.plan.nt, dtype=torch.float32, device=self.device)
+            for k, n in enumerate(names):
+                i = self.index[n]
+                o, m = self.plan.offsets[i], self.plan.sizes[i]
+                q[o:o + m].copy_(qg[plan.offsets[k]:plan.offsets[k] + m])
+                norms[i] = ng[k]
+        levels = 2**compressor.s
+        # absent tensors have q = 0 (x was zero there): acc += +0, as accumulate_layers
+        self.plan.qsgd_decode(q, 8 if levels <= 127 else 32, levels, norms, y_out=self.acc, accumulate=True)
+        self.update_count += 1
+        self.total_samples += int(number_samples)
+
     def apply_and_encode(self, compressor, total_samples: Optional[int] = None):
         """Fused ``_apply_model_updates`` + the first downlink ``_send_current_model``
         (global_grpc_server.py:155-171, 213-234): one launch divides the accumulator by the
@@ -128,14 +194,16 @@ class DeviceAggregator:
             return avg, encode_updates_dict(avg, compressor)
         total = self.total_samples if total_samples is None else int(total_samples)
         s = compressor.s
-        seed = int(torch.randint(0, 2**62, (1,)).item())
-        _, q, norms = self.plan.ps_apply_encode(self.acc, float(total), s, avg_out=self.acc, seed=seed,
-                                                offset=compressor._next_call())
+        if self.avg is None:
+            self.avg = torch.empty_like(self.acc)
+        # avg_out disjoint from acc: the one-launch path (omf_ps_apply_encode)
+        _, q, norms = self.plan.ps_apply_encode(self.acc, float(total), s, avg_out=self.avg,
+                                                seed=compressor.philox_key(), offset=compressor._next_call())
         levels = 2**s
         width, _ = choose_qsgd_storage_width(levels)
         qh = q.cpu().numpy()
         nh = norms.cpu().tolist()
-        avg = {n: self._slice(n).view(self.shapes[n]) for n in self.names}
+        avg = {n: self._avg_slice(n).view(self.shapes[n]) for n in self.names}
         layers = []
         for i, n in enumerate(self.names):
             o, k = self.plan.offsets[i], self.plan.sizes[i]
@@ -179,4 +247,67 @@ def weighted_sum_gather(q: torch.Tensor, norms: torch.Tensor, width: int, levels
     else:
         dist.gather(q, dst=dst, group=group)
         dist.gather(norms, dst=dst, group=group)
+    return acc
+
+
+def total_weight(weight: float, device, group=None) -> float:
+    """Σ_i w_i over the ranks (the PS's total_samples, global_grpc_server.py:107)."""
+    t = torch.tensor([float(weight)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+    return float(t.item())
+
+
+def qsgd_weighted_round(x: torch.Tensor, weight: float, total: float, ops, bit_width: int, call: int,
+                        mode: str = "gather", y: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
+                        q: Optional[torch.Tensor] = None, norms: Optional[torch.Tensor] = None, group=None,
+                        dst: int = 0, bufs=None) -> torch.Tensor:
+    """One round of the 8-GPU PS weighted sum: this rank's client update ``x`` is encoded as
+    Q(fl32(weight·x)) (the weighting fused into the encoder) and the root ends with
+    Σ_i decode(Q(w_i x_i)) / total (``total`` = Σ_i w_i, e.g. from ``total_weight``).
+    ``mode``: "gather" (payloads to the root, rank-order decode-accumulate: deterministic)
+    or "reduce" (decode locally, RCCL reduce of fp32).  Returns the root's result arena."""
+    levels = 2**int(bit_width)
+    width = 8 if levels <= 127 else 32
+    q, norms = ops.encode(x, bit_width, float(weight), call, q, norms)
+    if mode == "reduce":
+        y = ops.decode(q, width, levels, norms, y, False)
+        return weighted_sum_reduce(y, total, ops, group=group, dst=dst)
+    if mode != "gather":
+        raise ValueError("mode must be 'gather' or 'reduce'")
+    if acc is None:
+        acc = torch.empty(x.numel(), dtype=torch.float32, device=x.device)
+    return weighted_sum_gather(q, norms, width, levels, acc, total, ops, group=group, dst=dst, bufs=bufs)
+
+
+def topk_sparse_aggregate(values: torch.Tensor, indices: torch.Tensor, ratio: float, acc: torch.Tensor, ops,
+                          client_count: Optional[int] = None, group=None, dst: Optional[int] = None,
+                          bufs: Optional[List[Tuple[torch.Tensor, torch.Tensor]]] = None) -> torch.Tensor:
+    """Multi-GPU Top-K aggregate (torch_mpi.py:302-359 + core.py:62-71) over whole arenas.
+
+    ``values``/``indices``: this rank's packed selection (``Plan.topk_encode`` at ``ratio``;
+    tensor-local indices).  ``dst=None``: all-gather, every rank ends with the aggregate
+    (the reference's form); ``dst=r``: gather to rank r only (half the xGMI traffic).  The
+    receiving ranks scatter-add the selections in rank order into ``acc`` (zeroed first) and
+    divide by ``client_count`` (default: the world size, as sparse_aggregate)."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    count = world if client_count is None else int(client_count)
+    receive = dst is None or rank == dst
+    if receive and bufs is None:
+        bufs = [(torch.empty_like(values), torch.empty_like(indices)) for _ in range(world)]
+    if dst is None:
+        dist.all_gather([b[0] for b in bufs], values, group=group)
+        dist.all_gather([b[1] for b in bufs], indices, group=group)
+    elif rank == dst:
+        dist.gather(values, gather_list=[b[0] for b in bufs], dst=dst, group=group)
+        dist.gather(indices, gather_list=[b[1] for b in bufs], dst=dst, group=group)
+    else:
+        dist.gather(values, dst=dst, group=group)
+        dist.gather(indices, dst=dst, group=group)
+    if not receive:
+        return acc
+    acc.zero_()
+    for v, ix in bufs:  # rank order: tensor.data[ix] += vals per client, as layerwise_decompress
+        ops.topk_decode(v, ix, ratio, acc, 2)
+    ops.div_(acc, float(count))
     return acc

@@ -27,8 +27,8 @@ def load(d, counter):
 
 
 def short(name):
-    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_decode_flat", "qsgd_quant_flat", "topk_prep_hist",
-              "topk_collect"):
+    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_decode_flat", "qsgd_quant_flat",
+              "topk_fused", "topk_prep_hist", "topk_collect", "topk_gather", "topk_scatter_arena"):
         if k in name:
             return k
     return None
@@ -47,7 +47,17 @@ def main():
         f = 2 * 1024 * sum(vals) / len(vals)
         w = 1024 * sum(write[name]) / len(write[name])
         res[k] = {"fetch_bytes_corrected": f, "write_bytes": w, "launches": len(vals)}
-    j = {"config": cfg, "bits": bits, "note": "FETCH_SIZE x2 (gfx950 wide-load correction) + WRITE_SIZE, KiB->B, "
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from omnifed_amd.build import source_digest
+    import datetime
+    import subprocess
+
+    try:
+        commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
+    except OSError:
+        commit = ""
+    j = {"config": cfg, "bits": bits, "source_sha": source_digest(), "commit": commit or None,
+         "date": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%d"), "note": "FETCH_SIZE x2 (gfx950 wide-load correction) + WRITE_SIZE, KiB->B, "
          "average per launch; Infinity-Cache hits are counted as fetches",
          "bytes_per_launch": {k: round(v["fetch_bytes_corrected"] + v["write_bytes"]) for k, v in res.items()},
          "detail": res}

@@ -43,7 +43,7 @@ def test_golden_cases_injected(gpu, golden, golden_index):
         u = _dev(oracle.mt19937_uniforms(c["seed"], n), gpu)
         nin = torch.tensor([c["norm"]], dtype=torch.float32, device=gpu)
         q, norms = plan.qsgd_encode(x, s, u=u, norm_in=nin)
-        assert q.cpu().numpy().tobytes() == golden[key + "/q"].tobytes(), key
+        assert q[:n].cpu().numpy().tobytes() == golden[key + "/q"].tobytes(), key
         y = plan.qsgd_decode(q, c["width"], c["level"], norms)
         assert y.cpu().numpy().tobytes() == golden[key + "/y"].tobytes(), key
 
@@ -57,7 +57,7 @@ def test_golden_hashed_cases(gpu, golden_index):
         u = _dev(oracle.mt19937_uniforms(c["seed"], n), gpu)
         nin = torch.tensor([c["norm"]], dtype=torch.float32, device=gpu)
         q, norms = plan.qsgd_encode(_dev(x_np, gpu), s, u=u, norm_in=nin)
-        assert hashlib.sha256(q.cpu().numpy().tobytes()).hexdigest() == c["q_sha"], c
+        assert hashlib.sha256(q[:n].cpu().numpy().tobytes()).hexdigest() == c["q_sha"], c
         y = plan.qsgd_decode(q, c["width"], 2**s, norms)
         assert sha(y.cpu().numpy()) == c["y_sha"], c
 
@@ -78,7 +78,7 @@ def test_golden_edge_cases(gpu, golden, golden_index):
         u = _dev(oracle.mt19937_uniforms(c["seed"], n), gpu)
         q, norms = plan.qsgd_encode(_dev(x_np.astype(np.float32), gpu), c["s"], u=u,
                                     norm_in=torch.tensor([norm], device=gpu))
-        assert q.cpu().numpy().tobytes() == L.values_data, key
+        assert q[:n].cpu().numpy().tobytes() == L.values_data, key
         y = plan.qsgd_decode(q, L.width, L.level, norms)
         assert y.cpu().numpy().tobytes() == golden[key + "/y"].tobytes(), key
 
@@ -261,8 +261,11 @@ def test_bad_arguments_raise(gpu):
 
 
 @pytest.mark.parametrize("cfg", ["resnet18"])
-def test_full_config_parity_mt_stream(gpu, cfg):
-    """Whole R18 update arena, reference MT19937 stream, GPU norms: bit-exact vs the oracle per tensor."""
+@pytest.mark.parametrize("bits", [3, 4, 8])
+def test_full_config_parity_mt_stream(gpu, cfg, bits):
+    """Whole R18 update arena (BASELINE config 2: "8-level" = s=3, the presets' s=4, the base
+    default s=8 with an int32 wire), reference MT19937 stream, GPU norms: payload and decoded
+    floats bit-exact vs the oracle per tensor."""
     named = shapes.model_shapes(cfg)
     sizes = [shapes.numel(s) for _, s in named]
     plan = codec.Plan.get(sizes, device=gpu)
@@ -278,14 +281,19 @@ def test_full_config_parity_mt_stream(gpu, cfg):
     for t, (o, n) in enumerate(zip(plan.offsets, sizes)):
         if nh[t] != 0:
             u_host[o:o + n] = stream.draw(n)
-    q, _ = plan.qsgd_encode(x, 4, u=_dev(u_host, gpu), norm_in=norms)
+    q, _ = plan.qsgd_encode(x, bits, u=_dev(u_host, gpu), norm_in=norms)
+    L = 2**bits
+    y = plan.qsgd_decode(q, 8 if L <= 127 else 32, L, norms)
     qh = q.cpu().numpy()
+    yh = y.cpu().numpy()
     xh = x_host.numpy()
     for t, (o, n) in enumerate(zip(plan.offsets, sizes)):
         ref = float(np.sqrt(np.sum(xh[o:o + n].astype(np.float64) ** 2)))
         assert nh[t] == pytest.approx(ref, rel=NORM_RTOL)
-        want = _oracle_q(xh[o:o + n], 4, float(nh[t]), u_host[o:o + n])
+        want = _oracle_q(xh[o:o + n], bits, float(nh[t]), u_host[o:o + n])
         assert qh[o:o + n].tobytes() == want.tobytes(), t
+        want_y = oracle.qsgd_dequantize(torch.from_numpy(want), float(nh[t]), L, (n,)).numpy()
+        assert yh[o:o + n].tobytes() == want_y.tobytes(), t
 
 
 @pytest.mark.parametrize("cfg,s", [("llama400m", 4), ("llama150m", 8)])

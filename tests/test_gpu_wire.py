@@ -93,15 +93,20 @@ def test_batched_decode_errors_in_message_order(gpu):
         decode_updates_dict([odd])
 
 
-@pytest.mark.parametrize("strategy", ["ring", "ordered"])
-def test_fused_ps_apply_encode(gpu, strategy):
+@pytest.mark.parametrize("strategy,hold", [("ring", 0), ("ring", 1), ("ordered", 0)])
+def test_fused_ps_apply_encode(gpu, strategy, hold):
     """avg = acc / total (numpy fp32 division, bit for bit) and its payload = encode(avg) with the
-    same draws — in one launch (ring) or divide + encode (other strategies)."""
+    same draws — in one launch (ring) or divide + encode (other strategies).  hold=1: every
+    tensor of more than one ring chunk takes two passes (the second re-reads acc).  In place
+    (avg_out is acc) the same average and payload come out of divide + encode."""
     from omnifed_amd import codec
 
     sizes = [5, 16384, 70001, 1 << 20, 3000]
     plan = codec.Plan(sizes, device=gpu)
     plan.set_encode_strategy(strategy)
+    if hold:
+        plan.set_ring(hold_max=hold)
+        assert plan.ring_info["two_pass_tensors"] >= 2
     g = torch.Generator(device=gpu).manual_seed(9)
     acc = torch.randn(plan.arena_end, device=gpu, generator=g) * 3.0
     total = 7
@@ -115,11 +120,18 @@ def test_fused_ps_apply_encode(gpu, strategy):
     assert torch.equal(norms, n2)
     for o, n in zip(plan.offsets, plan.sizes):
         assert torch.equal(q[o:o + n], q2[o:o + n])
-    # in place (the PS's accumulator becomes the averaged model)
+    # in place (the PS's accumulator becomes the averaged model): same average, same payload
     acc2 = acc.clone()
-    plan.ps_apply_encode(acc2, float(total), 4, avg_out=acc2, seed=21, offset=4)
+    _, q3, n3 = plan.ps_apply_encode(acc2, float(total), 4, avg_out=acc2, seed=21, offset=4)
+    assert plan.check()
+    assert torch.equal(n3, n2)
     for o, n in zip(plan.offsets, plan.sizes):
         assert torch.equal(acc2[o:o + n], avg[o:o + n])
+        assert torch.equal(q3[o:o + n], q2[o:o + n])
+    # a partial overlap of avg_out and acc is refused
+    big = torch.zeros(plan.arena_end + 64, device=gpu)
+    with pytest.raises(ValueError, match="overlap"):
+        plan.ps_apply_encode(big[:plan.arena_end], float(total), 4, avg_out=big[32:32 + plan.arena_end])
 
 
 def test_device_aggregator_apply_and_encode(gpu):
