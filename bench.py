@@ -180,7 +180,7 @@ def cpu_baseline_topk(torch, named, ratio, budget=12_000_000):
 
     def one():
         for j, x in enumerate(sample):
-            vals, idx = comp.compress(x, f"t{j}")
+            (vals, idx), _ = comp.compress(x, f"t{j}")
             oracle.topk_desparse(vals, idx, x.numel())
 
     all_threads = torch.get_num_threads()

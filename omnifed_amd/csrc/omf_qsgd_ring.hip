@@ -379,10 +379,8 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
   constexpr int QW = 16 - LW;               // quantiser waves
   constexpr int RPW = ROWS / LW;            // rows per loader wave
   constexpr int VL = RPW * 4;               // float4 per loader lane
-  constexpr int GPT = (ROWS / 4) * 256 / (QW * 64);  // Philox groups per quantiser thread
   constexpr int CH = ROWS * 1024;           // chunk elements
   static_assert(ROWS % 4 == 0 && ROWS % LW == 0 && S >= 2, "configuration");
-  static_assert(GPT >= 1 && GPT * QW * 64 == (ROWS / 4) * 256, "quantiser threads must tile the groups");
   constexpr int PR = 4;  // partial records (per chunk, decoupled from LDS slots)
   constexpr int NTL = ROWS;   // quantisation tiles per chunk (4 rows x 64 float4 positions each)
   constexpr int QC = QW - 1;  // claiming quantiser waves (quantiser wave 0 polls norms)
@@ -1138,6 +1136,9 @@ constexpr Config kConfigs[] = {
     {16, 4, 0, 0, 1},  // register-resident: 64 KiB chunks, 4 register buffers per thread, lookahead 1
     {16, 3, 0, 0, 1},  // register streams + 2 LDS slots for published chunks: lookahead 2
 };
+// Measured and dropped (Llama-400M, round 2): 48 KiB x 3 slots with 4 / 6 / 12 loader waves
+// 0.84 / 0.63 / 0.78 ms, 32 KiB x 4 slots with 8 / 4 loader waves 0.78 / 0.71 ms, 64 KiB x 2
+// with 4 loader waves 0.85 ms, against cfg 0's 0.63 ms: more, smaller slots do not help.
 
 template <int ROWS, int S, int LW, bool DB>
 const void* kernel_ptr(int width, bool has_u) {

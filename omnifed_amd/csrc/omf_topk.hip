@@ -16,7 +16,7 @@
 //                       sample keep every element).
 //   3. topk_fused       ONE streaming pass: read x (+ residual), write t' into the residual,
 //                       and append every |t'| at or above the threshold (~1.1-1.8 k) as a
-//                       64-bit key (tensor << 56 | (2^31-1 - |t'|bits) << 25 | index) into the
+//                       64-bit key (index << 39 | tensor << 31 | (2^31-1 - |t'|bits)) into the
 //                       item's own region (one block scan per 8 Ki elements, no contended
 //                       atomics).
 //   4. topk_check       candidates per tensor from the item scan; a tensor whose sample put
@@ -30,6 +30,7 @@
 // descending sort of (|t'|bits << 32 | ~index) per tensor).
 // Decode is a scatter (mode 0 zero-fill, 1 overlay, 2 scatter-add).
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include <rocprim/rocprim.hpp>
@@ -54,6 +55,10 @@ constexpr int kSStride = 256;   // one run per >= 256 elements,
 constexpr int kSMaxRuns = 4096; // at most 4096 runs (64 Ki samples) per tensor
 constexpr int kV = 16;
 constexpr int64_t kSub = (int64_t)kV * kThreads * 4;
+// Composite candidate key: index << 39 | tensor << 31 | (2^31 - 1 - |t'|bits).  Candidates are
+// emitted in index order within each tensor, so a stable radix sort of the low 39 bits alone
+// gives (tensor ascending, |t'| descending, index ascending): 5 digit passes instead of 8.
+constexpr int kSortBits = 39;
 
 // Mirrors the QSGD plan's item / tensor tables (omf_qsgd.hip); only the fields used here.
 struct Item {
@@ -131,13 +136,15 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
                                                               float alpha, const int64_t* __restrict__ tbegin,
                                                               const int64_t* __restrict__ tsize,
                                                               const int64_t* __restrict__ kk,
-                                                              uint32_t* __restrict__ tbin) {
+                                                              uint32_t* __restrict__ tbin,
+                                                              uint32_t* __restrict__ hist) {
   constexpr int PER = kSBins / 1024;
   constexpr int U = 4;  // runs in flight per lane group
   __shared__ uint32_t h[kSBins];
   __shared__ uint32_t part[1024];
   const int t = blockIdx.x;
   for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
+  for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;  // this call's redo histogram
   __syncthreads();
   const int64_t base = tbegin[t], n = tsize[t];
   const int64_t stride = sample_stride(n), nr = (n + stride - 1) / stride;
@@ -198,45 +205,71 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
   }
 }
 
-// Append the selected elements of one 8 Ki-element pass of an item to the item's region
-// (block scan of the per-lane counts; coalesced per (row, component)).
+// Append the selected elements of one 8 Ki-element pass of an item to the item's region in
+// ascending element order (element idx0 + 1024 k + c of thread t is the pass's element
+// 1024 k + 4 t + c): the 8 per-row counts of every thread are block-scanned as 16-bit
+// fields, so a stable sort on the key bits above the index keeps index order for equal
+// magnitudes (torch's tie order) without sorting the index bits.
 struct PassCollector {
-  uint32_t* s_wsum;  // kWaves
+  uint32_t* s_wsum;  // 4 x kWaves packed row counts
   __device__ __forceinline__ uint32_t append(const float4 (&v)[8], uint32_t selm, uint64_t* dst, uint32_t idx0,
                                              uint64_t tag) const {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t nsel = (uint32_t)__popc(selm);
-    uint32_t wtot = nsel;
+    uint32_t pk[4], mine[4];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) wtot += __shfl_xor(wtot, o, 64);
-    if (lane == 0) s_wsum[wave] = wtot;
+    for (int i = 0; i < 4; ++i) {  // rows 2i, 2i+1: counts 0..4 in 16-bit fields
+      pk[i] = (uint32_t)__popc((selm >> (8 * i)) & 0xFu) | ((uint32_t)__popc((selm >> (8 * i + 4)) & 0xFu) << 16);
+      mine[i] = pk[i];
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {  // wave inclusive scan (fields never carry: <= 256)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t u = __shfl_up(pk[i], o, 64);
+        if (lane >= o) pk[i] += u;
+      }
+    }
+    if (lane == 63) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s_wsum[4 * wave + i] = pk[i];
+    }
     __syncthreads();
-    uint32_t wpre = 0, tot = 0;
+    uint32_t wpre[4] = {0, 0, 0, 0}, tot[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int w2 = 0; w2 < kWaves; ++w2) {
-      if (w2 < wave) wpre += s_wsum[w2];
-      tot += s_wsum[w2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t ws = s_wsum[4 * w2 + i];
+        if (w2 < wave) wpre[i] += ws;
+        tot[i] += ws;  // fields <= 1024: no carry
+      }
     }
     __syncthreads();  // s_wsum reuse by the next pass
-    dst += wpre;
-    const uint64_t lt = (1ull << lane) - 1ull;
-    if (wtot) {
+    uint32_t rowbase = 0, total = 0;
+    uint32_t base[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = k >> 1, sh = 16 * (k & 1);
+      const uint32_t ex = ((pk[i] - mine[i]) >> sh) & 0xFFFFu;  // threads before me in my wave
+      base[k] = rowbase + ((wpre[i] >> sh) & 0xFFFFu) + ex;
+      rowbase += (tot[i] >> sh) & 0xFFFFu;
+    }
+    total = rowbase;
+    if (selm) {
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const float vv[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+        uint32_t r = base[k];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-          const bool sel = (selm >> (4 * k + c)) & 1u;
-          const uint64_t m = __ballot(sel);
-          if (sel) {
+          if ((selm >> (4 * k + c)) & 1u) {
             const uint32_t idx = idx0 + 1024u * k + c;
-            dst[__popcll(m & lt)] = tag | ((uint64_t)(0x7fffffffu - mag_key(vv[c])) << 25) | (uint64_t)idx;
+            dst[r++] = ((uint64_t)idx << 39) | tag | (uint64_t)(0x7fffffffu - mag_key(vv[c]));
           }
-          dst += __popcll(m);
         }
       }
     }
-    return tot;
+    return total;
   }
 };
 
@@ -249,13 +282,13 @@ __global__ __launch_bounds__(kThreads, MODE == 0 ? 4 : 6) void topk_fused(const 
                                                        const int64_t* __restrict__ tbegin,
                                                        const uint32_t* __restrict__ tbin,
                                                        uint32_t* __restrict__ item_cnt, uint64_t* __restrict__ cand) {
-  __shared__ uint32_t s_wsum[kWaves];
+  __shared__ uint32_t s_wsum[4 * kWaves];
   const Item it = items[blockIdx.x];
   const uint32_t thr = tbin[it.tensor];
   const int64_t base = tbegin[it.tensor];
   constexpr int64_t CS = 8 * kThreads * 4;  // 8192 elements per pass
   const PassCollector col{s_wsum};
-  const uint64_t tag = (uint64_t)it.tensor << 56;
+  const uint64_t tag = (uint64_t)it.tensor << 31;
   uint32_t item_total = 0;
   for (int64_t b = it.begin; b < it.end; b += CS) {
     const uint32_t lim = (uint32_t)(min(b + CS, it.end) - b);
@@ -291,24 +324,60 @@ __global__ __launch_bounds__(kThreads, MODE == 0 ? 4 : 6) void topk_fused(const 
   if (threadIdx.x == 0) item_cnt[blockIdx.x] = item_total;
 }
 
-// Candidates per tensor from the item scan; flag the tensors whose threshold was too high.
-__global__ __launch_bounds__(kThreads) void topk_check(int32_t nt, const int64_t* __restrict__ kk,
-                                                       const uint32_t* __restrict__ tfirst,
-                                                       const uint32_t* __restrict__ tlast,
-                                                       const uint32_t* __restrict__ item_cnt,
-                                                       const uint32_t* __restrict__ item_off, int64_t n_items,
-                                                       int64_t* __restrict__ cstart, uint32_t* __restrict__ cnt,
-                                                       uint32_t* __restrict__ flag, uint32_t* __restrict__ status) {
-  for (int32_t t = threadIdx.x; t < nt; t += kThreads) {
-    const uint32_t f = tfirst[t], l = tlast[t];
-    const uint32_t c = item_off[l] + item_cnt[l] - item_off[f];
-    cstart[t] = item_off[f];
-    cnt[t] = c;
-    const uint32_t redo = (int64_t)c < kk[t] ? 1u : 0u;
-    flag[t] = redo;
-    if (redo) atomicOr(&status[1], 1u);
+// One block: exclusive scan of the per-item candidate counts (items in tensor order), then
+// per tensor its candidate count and start; flag the tensors whose threshold was too high.
+// status[0] = all candidates, status[1] = any flagged.  (Replaces a library scan: no
+// workspace clears, one launch.)
+__global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_t* __restrict__ kk,
+                                                        const uint32_t* __restrict__ tfirst,
+                                                        const uint32_t* __restrict__ tlast,
+                                                        const uint32_t* __restrict__ item_cnt,
+                                                        uint32_t* __restrict__ item_off, int64_t n_items,
+                                                        int64_t* __restrict__ cstart, uint32_t* __restrict__ cnt,
+                                                        uint32_t* __restrict__ flag, uint32_t* __restrict__ status) {
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t s_any;
+  const int t = threadIdx.x;
+  const int64_t per = (n_items + 1023) / 1024;
+  const int64_t b = min((int64_t)t * per, n_items), e = min(b + per, n_items);
+  uint32_t loc = 0;
+  for (int64_t i = b; i < e; ++i) loc += item_cnt[i];
+  part[t] = loc;
+  if (t == 0) s_any = 0;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan
+    const uint32_t add = t >= o ? part[t - o] : 0u;
+    __syncthreads();
+    part[t] += add;
+    __syncthreads();
   }
-  if (threadIdx.x == 0) status[0] = item_off[n_items - 1] + item_cnt[n_items - 1];
+  uint32_t run = part[t] - loc;
+  for (int64_t i = b; i < e; ++i) {
+    item_off[i] = run;
+    run += item_cnt[i];
+  }
+  // exclusive prefix of item i from the thread prefixes (no read-back of item_off)
+  auto prefix = [&](int64_t i) -> uint32_t {
+    const int64_t owner = i / per;
+    uint32_t v = owner > 0 ? part[owner - 1] : 0u;
+    for (int64_t j = owner * per; j < i; ++j) v += item_cnt[j];
+    return v;
+  };
+  for (int32_t q = t; q < nt; q += 1024) {
+    const uint32_t f = tfirst[q], l = tlast[q];
+    const uint32_t of = prefix(f);
+    const uint32_t c = prefix(l) + item_cnt[l] - of;
+    cstart[q] = of;
+    cnt[q] = c;
+    const uint32_t redo = (int64_t)c < kk[q] ? 1u : 0u;
+    flag[q] = redo;
+    if (redo) s_any = 1u;
+  }
+  __syncthreads();
+  if (t == 0) {
+    status[0] = part[1023];
+    status[1] = s_any;
+  }
 }
 
 // Exact path, pass 1 (and the per-tensor redo): t' and its 1024-bin histogram per tensor.
@@ -406,7 +475,7 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
                                                          const uint32_t* __restrict__ bin,
                                                          const uint32_t* __restrict__ flag, uint32_t* __restrict__ cnt,
                                                          uint32_t* __restrict__ item_cnt, uint64_t* __restrict__ cand) {
-  __shared__ uint32_t s_wsum[kWaves];
+  __shared__ uint32_t s_wsum[4 * kWaves];
   __shared__ uint32_t s_base;
   const Item it = items[blockIdx.x];
   if (flag && !flag[it.tensor]) return;  // block-uniform
@@ -416,7 +485,7 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
   constexpr int CV = 8;
   constexpr int64_t CS = (int64_t)CV * kThreads * 4;
   const PassCollector col{s_wsum};
-  const uint64_t tag = (uint64_t)it.tensor << 56;
+  const uint64_t tag = (uint64_t)it.tensor << 31;
   uint32_t item_total = 0;
   for (int64_t b = it.begin; b < it.end; b += CS) {
     const uint32_t lim = (uint32_t)(min(b + CS, it.end) - b);
@@ -497,15 +566,21 @@ template <bool GLOBAL>
 __global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict__ tp, float scale,
                                                         float* __restrict__ r, const uint64_t* __restrict__ sorted,
                                                         const int64_t* __restrict__ tbegin,
+                                                        const int64_t* __restrict__ tsize,
                                                         const int64_t* __restrict__ cstart,
                                                         const int64_t* __restrict__ kk, const int64_t* __restrict__ koff,
                                                         float* __restrict__ values, int64_t* __restrict__ indices) {
   const int t = blockIdx.y;
-  const int64_t k = kk[t], base = tbegin[t], o = koff[t];
+  const int64_t k = kk[t], base = tbegin[t], o = koff[t], n = tsize[t];
   const int64_t s0 = GLOBAL ? cstart[t] : base;
   for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < k; j += (int64_t)gridDim.x * kThreads) {
     const uint64_t key = sorted[s0 + j];
-    const uint32_t idx = GLOBAL ? (uint32_t)(key & 0x1FFFFFFull) : ~(uint32_t)key;
+    const uint32_t idx = GLOBAL ? (uint32_t)(key >> 39) : ~(uint32_t)key;
+    if (idx >= n || (GLOBAL && (int)((key >> 31) & 0xFFu) != t)) {  // never expected: a key of another tensor
+      values[o + j] = 0.0f;
+      indices[o + j] = -1;
+      continue;
+    }
     const float v = __fmul_rn(tp[base + idx], scale);
     values[o + j] = v;
     indices[o + j] = (int64_t)idx;
@@ -590,13 +665,6 @@ size_t sort_tmp_bytes(const omf_plan* p) {
   uint64_t* dummy = nullptr;
   if (global_path(p)) {
     (void)rocprim::radix_sort_keys(nullptr, bytes, dummy, dummy, (size_t)size, 0, 64, (hipStream_t)0, false);
-    int64_t n_items = 0;
-    (void)omf_plan_access::flat_items(p, &n_items);
-    size_t sb = 0;
-    uint32_t* u = nullptr;
-    (void)rocprim::exclusive_scan(nullptr, sb, u, u, 0u, (size_t)n_items, rocprim::plus<uint32_t>(), (hipStream_t)0,
-                                  false);
-    bytes = std::max(bytes, sb);
   } else {
     uint32_t* off = nullptr;
     (void)rocprim::segmented_radix_sort_keys_desc(nullptr, bytes, dummy, dummy, (unsigned int)size, (unsigned int)nt,
@@ -605,7 +673,8 @@ size_t sort_tmp_bytes(const omf_plan* p) {
   return bytes;
 }
 
-// Workspace: everything up to `zero_end` is cleared once per call.
+// Workspace: everything up to `zero_end` is cleared once per call on the exact path; the
+// sampled path clears its redo histograms in topk_sample_threshold and writes the rest.
 struct WsLayout {
   size_t hist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
       item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes;
@@ -709,19 +778,19 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   float* rz = residual_mode ? residual : nullptr;  // selected slots to zero
   const dim3 grid((unsigned)n_items), blk(kThreads);
 
-  OMF_HIP(hipMemsetAsync(w, 0, L.zero_end, st));
-  hipLaunchKernelGGL(topk_setup, dim3(1), blk, 0, st, d_sizes, nt, ratio, kk, koff, tfirst, tlast);
   const bool glob = global_path(plan);
+  if (!glob) OMF_HIP(hipMemsetAsync(w, 0, L.zero_end, st));
+  hipLaunchKernelGGL(topk_setup, dim3(1), blk, 0, st, d_sizes, nt, ratio, kk, koff, tfirst, tlast);
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
     const dim3 sgrid((unsigned)nt), sblk(1024);
     if (residual_mode == 1) {
       hipLaunchKernelGGL((topk_sample_threshold<1>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
-                         tbin);
+                         tbin, hist);
       hipLaunchKernelGGL((topk_fused<1>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt, cand);
     } else {
       hipLaunchKernelGGL((topk_sample_threshold<0>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
-                         tbin);
+                         tbin, hist);
       if (residual_mode == 2)
         hipLaunchKernelGGL((topk_fused<2>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt,
                            cand);
@@ -731,11 +800,8 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     }
     uint32_t host_status[2] = {0, 0};
     auto scan_and_check = [&]() -> int {
-      size_t sb = L.tmp_bytes;
-      OMF_HIP(rocprim::exclusive_scan(w + L.tmp, sb, item_cnt, item_off, 0u, (size_t)n_items,
-                                      rocprim::plus<uint32_t>(), st, false));
-      hipLaunchKernelGGL(topk_check, dim3(1), blk, 0, st, nt, kk, tfirst, tlast, item_cnt, item_off, n_items, cstart,
-                         cnt, flag, status);
+      hipLaunchKernelGGL(topk_scan_check, dim3(1), dim3(1024), 0, st, nt, kk, tfirst, tlast, item_cnt, item_off,
+                         n_items, cstart, cnt, flag, status);
       OMF_HIP(hipGetLastError());
       // the sort needs the candidate count on the host (and the redo decision)
       OMF_HIP(hipMemcpyAsync(host_status, status, 8, hipMemcpyDeviceToHost, st));
@@ -752,8 +818,10 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     }
     const uint64_t total = host_status[0];
     hipLaunchKernelGGL(topk_compact, grid, blk, 0, st, cand, items, item_cnt, item_off, sorted);
-    // sort the packed keys back into `cand` (the per-item regions are no longer needed)
-    OMF_HIP(rocprim::radix_sort_keys(w + L.tmp, tmp_bytes, sorted, cand, (size_t)total, 0, 64, st, false));
+    // sort the packed keys back into `cand` (the per-item regions are no longer needed):
+    // candidates are in index order within each tensor, so a stable sort of the tensor and
+    // magnitude bits alone yields (tensor, |t'| descending, index ascending)
+    OMF_HIP(rocprim::radix_sort_keys(w + L.tmp, tmp_bytes, sorted, cand, (size_t)total, 0, kSortBits, st, false));
   } else {
     if (residual_mode == 0)
       hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
@@ -775,10 +843,10 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((kmax + kThreads - 1) / kThreads, 1024));
   if (glob)
     hipLaunchKernelGGL((topk_gather<true>), dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted_keys, d_begins,
-                       cstart, kk, koff, values, indices);
+                       d_sizes, cstart, kk, koff, values, indices);
   else
     hipLaunchKernelGGL((topk_gather<false>), dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted_keys, d_begins,
-                       cstart, kk, koff, values, indices);
+                       d_sizes, cstart, kk, koff, values, indices);
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }
