@@ -370,7 +370,7 @@ __device__ __forceinline__ float wait_norm_wave(const Args& a, const Tensor& ti,
 
 // ROWS rows per chunk, S LDS slots, LW loader waves (the other 16 - LW quantise), DB:
 // loaders double-buffer their registers (prefetch two chunks ahead).
-template <int ROWS, int S, int LW, bool DB, int WIDTH, bool HAS_U>
+template <int ROWS, int S, int LW, bool DB, int WIDTH, bool HAS_U, bool HELP_ = !DB>
 __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __restrict__ items,
                                                           const Tensor* __restrict__ tinfo) {
   // items / tinfo are read-only for the launch: __restrict__ lets the compiler use scalar
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
   constexpr int PR = 4;  // partial records (per chunk, decoupled from LDS slots)
   constexpr int NTL = ROWS;   // quantisation tiles per chunk (4 rows x 64 float4 positions each)
   constexpr int QC = QW - 1;  // claiming quantiser waves (quantiser wave 0 polls norms)
-  constexpr bool HELP = !DB;  // single-buffered loaders have the registers to help quantise
+  constexpr bool HELP = HELP_;  // loaders claim tiles of a slot's previous chunk before refilling it
   constexpr uint32_t PER_USE = NTL + QC + (HELP ? LW : 0);  // claim tickets per quantised use of a slot
   __shared__ float4 slots[S][ROWS * 256];
   __shared__ double lpart[PR][LW];
@@ -1136,18 +1136,21 @@ constexpr Config kConfigs[] = {
     {16, 4, 0, 0, 1},  // register-resident: 64 KiB chunks, 4 register buffers per thread, lookahead 1
     {16, 3, 0, 0, 1},  // register streams + 2 LDS slots for published chunks: lookahead 2
 };
-// Measured and dropped (Llama-400M, round 2): 48 KiB x 3 slots with 4 / 6 / 12 loader waves
-// 0.84 / 0.63 / 0.78 ms, 32 KiB x 4 slots with 8 / 4 loader waves 0.78 / 0.71 ms, 64 KiB x 2
-// with 4 loader waves 0.85 ms, against cfg 0's 0.63 ms: more, smaller slots do not help.
+// Measured and dropped (Llama-400M, round 2): 48 KiB x 3 slots with 4 / 6 / 12
+// loader waves 0.84 / 0.63 / 0.78 ms, 32 KiB x 4 slots with 8 / 4 loader waves 0.78 / 0.71 ms,
+// 64 KiB x 2 with 4 loader waves 0.85 ms; double-buffered loaders that also help quantise
+// 0.68 ms (64 KiB x 2), 0.70 (48 KiB x 3, 12 one-row loaders), 0.76 (32 KiB x 4) — against
+// cfg 0's 0.63 ms.  With quantisation and norm waits switched off (OMF_RING_DBG=3) every one
+// of them still takes 0.40-0.55 ms: the hand-off machinery, not the slot count, sets the pace.
 
-template <int ROWS, int S, int LW, bool DB>
+template <int ROWS, int S, int LW, bool DB, bool HELP = !DB>
 const void* kernel_ptr(int width, bool has_u) {
   if (width == 1) {
-    return has_u ? (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 1, true>
-                 : (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 1, false>;
+    return has_u ? (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 1, true, HELP>
+                 : (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 1, false, HELP>;
   }
-  return has_u ? (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 4, true>
-               : (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 4, false>;
+  return has_u ? (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 4, true, HELP>
+               : (const void*)qsgd_encode_pc<ROWS, S, LW, DB, 4, false, HELP>;
 }
 
 // Caller uniforms (parity mode) hold 16 more registers per thread: 3 buffers keep them unspilled.

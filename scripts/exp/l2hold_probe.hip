@@ -6,8 +6,8 @@
 #include <stdint.h>
 
 #define NT 1024
-#define PER 4  // float4 per thread per chunk: 16 Ki elements = 64 KiB
 
+template <int PER>  // float4 per thread per chunk (4: 64 KiB chunks)
 __global__ __launch_bounds__(NT) void hold(const float4* __restrict__ x, uint32_t* __restrict__ q,
                                            float* __restrict__ part, int64_t nchunks, int H) {
   const int t = threadIdx.x;
@@ -46,9 +46,16 @@ __global__ __launch_bounds__(NT) void hold(const float4* __restrict__ x, uint32_
   if (acc == 1234.5f) part[0] = acc;
 }
 
-extern "C" int hold_run(const void* x, void* q, void* part, int64_t n, int H, int grid, void* stream) {
-  const int64_t nchunks = n / (NT * PER * 4);
-  hipLaunchKernelGGL(hold, dim3(grid), dim3(NT), 0, (hipStream_t)stream, (const float4*)x, (uint32_t*)q,
-                     (float*)part, nchunks, H);
+extern "C" int hold_run(const void* x, void* q, void* part, int64_t n, int H, int grid, int per, void* stream) {
+  const int64_t nchunks = n / (NT * per * 4);
+  if (per == 1)
+    hipLaunchKernelGGL(hold<1>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, (const float4*)x, (uint32_t*)q,
+                       (float*)part, nchunks, H);
+  else if (per == 2)
+    hipLaunchKernelGGL(hold<2>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, (const float4*)x, (uint32_t*)q,
+                       (float*)part, nchunks, H);
+  else
+    hipLaunchKernelGGL(hold<4>, dim3(grid), dim3(NT), 0, (hipStream_t)stream, (const float4*)x, (uint32_t*)q,
+                       (float*)part, nchunks, H);
   return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -9,7 +9,7 @@ so = "/tmp/l2hold_probe.so"
 subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-shared", "-fPIC", "-o", so, "scripts/exp/l2hold_probe.hip"],
                check=True)
 L = ctypes.CDLL(so)
-L.hold_run.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+L.hold_run.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
 dev = torch.device("cuda", 0)
 N = 400 * (1 << 20)
 x = torch.randn(N, device=dev)
@@ -33,7 +33,9 @@ def timed(fn, reps=5):
 
 
 alg = 5 * N
-for grid in (256, 512, 1024):
-    for H in (0, 1, 2, 3, 4, 6):
-        t = timed(lambda: L.hold_run(x.data_ptr(), q.data_ptr(), part.data_ptr(), N, H, grid, st))
-        print(f"grid {grid:5d} H={H}  {t:.3f} ms  ({alg / t / 1e6:.0f} GB/s algorithmic 5N)", flush=True)
+for per in (4, 2, 1):
+    for grid in (256, 512):
+        for H in (0, 1, 2, 4, 8):
+            t = timed(lambda: L.hold_run(x.data_ptr(), q.data_ptr(), part.data_ptr(), N, H, grid, per, st))
+            print(f"chunk {16 * per:3d} KiB grid {grid:4d} H={H}  {t:.3f} ms  ({alg / t / 1e6:.0f} GB/s algorithmic 5N)",
+                  flush=True)
