@@ -363,6 +363,33 @@ def main():
         del res, yt
 
     extras = {}
+    if not args.no_extras and world == 1 and qsgd is not None and args.config == "llama400m":
+        # the other QSGD configs of BASELINE.json on one GPU: ResNet-18 at "8 levels" (s = 3, int8)
+        # and the base default s = 8 (int32 wire), Llama-150M at the presets' s = 4
+        others = {}
+        for cname, bits in (("resnet18", 3), ("resnet18", 8), ("llama150m", 4)):
+            sz = [shapes.numel(sh) for _, sh in shapes.model_shapes(cname)]
+            pl = codec.Plan.get(sz, device=dev)
+            n_ = sum(sz)
+            w_ = 1 if 2**bits <= 127 else 4
+            xo = torch.randn(pl.arena_end, device=dev, generator=g) * 1e-3
+            qo = torch.empty(pl.payload_elems(8 * w_), dtype=torch.int8 if w_ == 1 else torch.int32, device=dev)
+            no = torch.empty(pl.nt, dtype=torch.float32, device=dev)
+            yo = torch.empty(pl.arena_end, dtype=torch.float32, device=dev)
+
+            def o_step(i, pl=pl, xo=xo, qo=qo, no=no, yo=yo, bits=bits, w_=w_):
+                pl.qsgd_encode(xo, bits, q_out=qo, norm_out=no, alpha=weight, seed=seed, offset=i)
+                pl.qsgd_decode(qo, 8 * w_, 2**bits, no, y_out=yo)
+
+            for i in range(3):
+                o_step(i)
+            reps = 20
+            to = timed(o_step, 3, reps) / reps
+            pl.check()
+            others[f"{cname}_s{bits}"] = {"elements": n_, "tensors": len(sz), "ms_per_step": round(to * 1e3, 4),
+                                           "algorithmic_GBs": round((8 + 2 * w_) * n_ / to / 1e9, 1)}
+            del xo, qo, no, yo
+        extras["other_configs"] = others
     if not args.no_extras and world == 1 and qsgd is not None:
         # PCIe-inclusive rate: host fp32 in -> device encode -> host payload; host payload -> decode -> host fp32
         xh = torch.empty(plan.arena_end, dtype=torch.float32, pin_memory=True)
