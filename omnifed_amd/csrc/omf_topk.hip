@@ -17,8 +17,8 @@
 //   3. topk_fused       ONE streaming pass: read x (+ residual), write t' into the residual,
 //                       and append every |t'| at or above the threshold (~1.1-1.8 k) as a
 //                       64-bit key (index << 39 | tensor << 31 | (2^31-1 - |t'|bits)) into the
-//                       item's own region (one block scan per 8 Ki elements, no contended
-//                       atomics).
+//                       1 Ki-element sub-chunk's own region (one block scan per 1 Ki
+//                       elements, one float4 per thread; no contended atomics).
 //   4. topk_check       candidates per tensor from the item scan; a tensor whose sample put
 //                       the threshold too high (fewer than k) is redone exactly from t': its
 //                       1024-bin histogram, the bin of the k-th magnitude, a re-collection.
@@ -30,6 +30,7 @@
 // descending sort of (|t'|bits << 32 | ~index) per tensor).
 // Decode is a scatter (mode 0 zero-fill, 1 overlay, 2 scatter-add).
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -59,6 +60,26 @@ constexpr int64_t kSub = (int64_t)kV * kThreads * 4;
 // emitted in index order within each tensor, so a stable radix sort of the low 39 bits alone
 // gives (tensor ascending, |t'| descending, index ascending): 5 digit passes instead of 8.
 constexpr int kSortBits = 39;
+// Bucket sort of the candidates (the fast path): fine bins per tensor (<= kFineMax), buckets
+// of whole fine bins whose rank starts fall in one kBucketHalf-wide window (so <= 2x that
+// many keys when no fine bin exceeds kBucketHalf), each sorted in LDS by one block.
+constexpr int kCoarse = 1024;         // coarse (sample-resolution) bins mapped per tensor
+constexpr int kFineMax = 16384;       // fine bins per tensor
+constexpr int kFineMaxBits = 18;      // a coarse bin splits by at most the rest of the mantissa
+constexpr int kFineMargin = 8;        // a fine bin expects <= kBucketHalf / 8 elements
+constexpr int kBucketHalf = 2048;
+constexpr int kBT = 512;              // bucket-sort block: 512 threads x 8 keys = 2 kBucketHalf
+constexpr int kBI = 8;
+constexpr int kPlanMaxBuckets = (1 << 25) / kBucketHalf + 2;
+constexpr int kSupItems = 64;         // items per super-item (x 16 sub-chunks = 1024 runs)
+
+// One bucket of the fast path: its keys at bkeys[key_off, + count), its first rank `start`
+// within the tensor; count | tensor << 16 (a bucket holds <= 2 kBucketHalf keys).
+struct BucketRec {
+  uint64_t key_off;
+  uint32_t start;
+  uint32_t count_tensor;
+};
 
 // Mirrors the QSGD plan's item / tensor tables (omf_qsgd.hip); only the fields used here.
 struct Item {
@@ -76,6 +97,31 @@ __device__ __forceinline__ uint32_t hash32(uint32_t h) {  // murmur3 finaliser
   return h ^ (h >> 16);
 }
 
+// Block-wide inclusive prefix sum of one value per thread (NT threads): wave shuffles and one
+// exchange of the wave totals through s_w[NT / 64].  Every thread must call it; it begins
+// with a barrier, so s_w may be reused from one call to the next.
+template <int NT>
+__device__ __forceinline__ uint32_t block_scan_incl(uint32_t v, uint32_t* s_w, uint32_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
+  }
+  __syncthreads();
+  if (lane == 63) s_w[w] = v;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    const uint32_t x = s_w[i];
+    pre += i < w ? x : 0u;
+    tot += x;
+  }
+  total = tot;
+  return v + pre;
+}
+
 // t' of one element: MODE 0/2: alpha * x ; MODE 1: r + alpha * x (the reference's order).
 template <int MODE>
 __device__ __forceinline__ float tprime(float x, float r, float alpha) {
@@ -83,30 +129,48 @@ __device__ __forceinline__ float tprime(float x, float r, float alpha) {
   return MODE == 1 ? __fadd_rn(r, t) : t;
 }
 
-// Per tensor: k, the output offset, and the tensor's flat-item range (items are 16 Ki
-// sub-chunks in tensor order: omf_qsgd.hip upload_plan).  One block; nt may exceed it.
+// Per tensor: k, the output offset, the tensor's flat-item range (items are 16 Ki
+// sub-chunks in tensor order: omf_qsgd.hip upload_plan), its bucket-table range (bbase) and
+// bucket-buffer region (kb2, k + kBucketHalf keys).  One block; nt may exceed it.  Clears the
+// call's status words.
+__device__ __forceinline__ uint32_t bucket_slots(int64_t k) { return (uint32_t)((k + kBucketHalf) / kBucketHalf + 1); }
+
 __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict__ tsize, int32_t nt, double ratio,
                                                        int64_t* __restrict__ kk, int64_t* __restrict__ koff,
-                                                       uint32_t* __restrict__ tfirst, uint32_t* __restrict__ tlast) {
-  __shared__ int64_t s_k[kThreads], s_i[kThreads];
-  int64_t carry_k = 0, carry_i = 0;
+                                                       uint32_t* __restrict__ tfirst, uint32_t* __restrict__ tlast,
+                                                       uint32_t* __restrict__ bbase, int64_t* __restrict__ kb2,
+                                                       uint32_t* __restrict__ sbase, uint32_t* __restrict__ status) {
+  __shared__ int64_t s_k[kThreads], s_i[kThreads], s_b[kThreads];
+  __shared__ uint32_t s_s[kThreads];
+  if (threadIdx.x < 4) status[threadIdx.x] = 0;
+  int64_t carry_k = 0, carry_i = 0, carry_b = 0;
+  uint32_t carry_s = 0;
   for (int32_t t0 = 0; t0 < nt; t0 += kThreads) {
     const int32_t t = t0 + (int32_t)threadIdx.x;
-    int64_t k = 0, ni = 0;
+    int64_t k = 0, ni = 0, nb = 0;
+    uint32_t ns = 0;
     if (t < nt) {
       k = (int64_t)((double)tsize[t] * ratio);
       if (k < 1) k = 1;
       ni = (tsize[t] + kSub - 1) / kSub;
+      nb = bucket_slots(k);
+      ns = (uint32_t)((ni + kSupItems - 1) / kSupItems);
     }
     s_k[threadIdx.x] = k;
     s_i[threadIdx.x] = ni;
+    s_b[threadIdx.x] = nb;
+    s_s[threadIdx.x] = ns;
     __syncthreads();
     for (int o = 1; o < kThreads; o <<= 1) {  // inclusive scans
       const int64_t ak = threadIdx.x >= (unsigned)o ? s_k[threadIdx.x - o] : 0;
       const int64_t ai = threadIdx.x >= (unsigned)o ? s_i[threadIdx.x - o] : 0;
+      const int64_t ab = threadIdx.x >= (unsigned)o ? s_b[threadIdx.x - o] : 0;
+      const uint32_t as = threadIdx.x >= (unsigned)o ? s_s[threadIdx.x - o] : 0u;
       __syncthreads();
       s_k[threadIdx.x] += ak;
       s_i[threadIdx.x] += ai;
+      s_b[threadIdx.x] += ab;
+      s_s[threadIdx.x] += as;
       __syncthreads();
     }
     if (t < nt) {
@@ -114,10 +178,19 @@ __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict
       koff[t] = carry_k + s_k[threadIdx.x] - k;
       tfirst[t] = (uint32_t)(carry_i + s_i[threadIdx.x] - ni);
       tlast[t] = (uint32_t)(carry_i + s_i[threadIdx.x] - 1);
-      if (t == nt - 1) koff[nt] = carry_k + s_k[threadIdx.x];
+      bbase[t] = (uint32_t)(carry_b + s_b[threadIdx.x] - nb);
+      sbase[t] = carry_s + s_s[threadIdx.x] - ns;
+      kb2[t] = carry_k + s_k[threadIdx.x] - k + (int64_t)t * kBucketHalf;
+      if (t == nt - 1) {
+        koff[nt] = carry_k + s_k[threadIdx.x];
+        bbase[nt] = (uint32_t)(carry_b + s_b[threadIdx.x]);
+        sbase[nt] = carry_s + s_s[threadIdx.x];
+      }
     }
     carry_k += s_k[kThreads - 1];
     carry_i += s_i[kThreads - 1];
+    carry_b += s_b[kThreads - 1];
+    carry_s += s_s[kThreads - 1];
     __syncthreads();
   }
 }
@@ -136,15 +209,22 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
                                                               float alpha, const int64_t* __restrict__ tbegin,
                                                               const int64_t* __restrict__ tsize,
                                                               const int64_t* __restrict__ kk,
+                                                              const uint32_t* __restrict__ tfirst,
+                                                              const uint32_t* __restrict__ tlast,
                                                               uint32_t* __restrict__ tbin,
-                                                              uint32_t* __restrict__ hist) {
+                                                              uint32_t* __restrict__ hist,
+                                                              uint32_t* __restrict__ item_cnt,
+                                                              uint32_t* __restrict__ fmap, uint32_t* __restrict__ tlo,
+                                                              uint32_t* __restrict__ fcount,
+                                                              uint32_t* __restrict__ fhist) {
   constexpr int PER = kSBins / 1024;
   constexpr int U = 4;  // runs in flight per lane group
   __shared__ uint32_t h[kSBins];
-  __shared__ uint32_t part[1024];
+  __shared__ uint32_t s_w[16];
   const int t = blockIdx.x;
   for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
   for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;  // this call's redo histogram
+  for (uint32_t i = tfirst[t] + threadIdx.x; i <= tlast[t]; i += 1024) item_cnt[i] = 0;  // the fused pass adds to them
   __syncthreads();
   const int64_t base = tbegin[t], n = tsize[t];
   const int64_t stride = sample_stride(n), nr = (n + stride - 1) / stride;
@@ -182,27 +262,85 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
     c[j] = h[PER * threadIdx.x + j];
     loc += c[j];
   }
-  part[threadIdx.x] = loc;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // inclusive suffix scan
-    const uint32_t add = threadIdx.x + o < 1024 ? part[threadIdx.x + o] : 0u;
-    __syncthreads();
-    part[threadIdx.x] += add;
-    __syncthreads();
-  }
-  const uint32_t S = part[0];
+  uint32_t S;
+  const uint32_t above0 = [&] {  // samples in the bins of higher threads
+    const uint32_t inc = block_scan_incl<1024>(loc, s_w, S);
+    return S - inc;
+  }();
   const double m = (double)kk[t] * (double)S / (double)max(n, (int64_t)1);
   const double want = m + 6.0 * sqrt(m) + 32.0;
-  if (m < 16.0 || want >= (double)S) {  // too few samples to trust: keep every element
-    if (threadIdx.x == 0) tbin[t] = 0;
-    return;
+  __shared__ uint32_t s_thr, s_min, s_max;
+  if (threadIdx.x == 0) {
+    s_thr = 0;
+    s_min = kSBins;
+    s_max = 0;
   }
-  const uint32_t target = (uint32_t)ceil(want);
-  uint32_t above = threadIdx.x + 1 < 1024 ? part[threadIdx.x + 1] : 0u;  // samples in higher bins
-  for (int j = PER - 1; j >= 0; --j) {
-    if (above < target && above + c[j] >= target) tbin[t] = PER * threadIdx.x + j;  // exactly one match
-    above += c[j];
+  __syncthreads();
+  if (!(m < 16.0 || want >= (double)S)) {  // else too few samples to trust: keep every element
+    const uint32_t target = (uint32_t)ceil(want);
+    uint32_t above = above0;
+    for (int j = PER - 1; j >= 0; --j) {
+      if (above < target && above + c[j] >= target) s_thr = PER * threadIdx.x + j;  // exactly one match
+      above += c[j];
+    }
   }
+#pragma unroll
+  for (int j = 0; j < PER; ++j)
+    if (c[j]) {
+      atomicMin(&s_min, (uint32_t)(PER * threadIdx.x + j));
+      break;
+    }
+#pragma unroll
+  for (int j = PER - 1; j >= 0; --j)
+    if (c[j]) {
+      atomicMax(&s_max, (uint32_t)(PER * threadIdx.x + j));
+      break;
+    }
+  __syncthreads();
+  const uint32_t thr = s_thr;
+  // Fine bins of the candidates (the exact per-tensor histogram the bucket sort plans from):
+  // coarse bin lo + i (i < 1024) is split into 2^r_i fine bins by the next r_i bits of |t'|,
+  // r_i sized from this sample so that a fine bin expects <= kBucketHalf / mg elements,
+  // estimating a coarse bin's elements by an upper bound (h + 3 sqrt(h) + 3) n / S of its h
+  // samples (a bin the sample missed can still hold ~3 n / S), up to two bins above the
+  // largest sampled one.
+  const uint32_t lo = thr > 0 ? thr : (s_min < (uint32_t)kSBins ? s_min : 0u);
+  const uint32_t cb = lo + threadIdx.x;
+  const double scale = (double)n / (double)max(S, 1u);
+  double est = 0.0;
+  if (cb < (uint32_t)kSBins && cb <= s_max + 2) {
+    const double hb = (double)h[cb];
+    est = (hb + 3.0 * sqrt(hb) + 3.0) * scale;
+  }
+  uint32_t rbits = 0, F = 0, inc = 0;
+  for (int mg = kFineMargin; mg >= 0; mg >>= 1) {
+    rbits = 0;
+    if (mg > 0) {
+      const double need = est * (double)mg / (double)kBucketHalf;
+      while (rbits < kFineMaxBits && (double)(1u << rbits) < need) ++rbits;
+    }
+    inc = block_scan_incl<1024>(1u << rbits, s_w, F);  // fine-bin counts
+    if (F <= (uint32_t)kFineMax || mg == 0) break;
+  }
+  const uint32_t off = inc - (1u << rbits);
+  fmap[(size_t)t * kCoarse + threadIdx.x] = off | (rbits << 16);
+  if (threadIdx.x == 0) {
+    tbin[t] = thr;
+    tlo[t] = lo;
+    fcount[t] = F;
+  }
+  for (uint32_t i = threadIdx.x; i < F; i += 1024) fhist[(size_t)t * kFineMax + i] = 0;
+}
+
+// Fine bin of a candidate magnitude (monotone in mag; below / above the mapped range clamp
+// to the lowest / highest fine bin).
+__device__ __forceinline__ uint32_t fine_bin(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t,
+                                             uint32_t F) {
+  const int c = (int)(mag >> kSShift) - (int)lo;
+  if (c < 0) return 0u;
+  if (c >= kCoarse) return F - 1u;
+  const uint32_t m = map_t[c], r = m >> 16;
+  return (m & 0xffffu) + ((mag >> (kSShift - r)) & ((1u << r) - 1u));
 }
 
 // Append the selected elements of one 8 Ki-element pass of an item to the item's region in
@@ -212,8 +350,8 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
 // magnitudes (torch's tie order) without sorting the index bits.
 struct PassCollector {
   uint32_t* s_wsum;  // 4 x kWaves packed row counts
-  __device__ __forceinline__ uint32_t append(const float4 (&v)[8], uint32_t selm, uint64_t* dst, uint32_t idx0,
-                                             uint64_t tag) const {
+  __device__ __forceinline__ uint32_t append(const float4 (&v)[8], uint32_t selm, uint64_t* dst,
+                                             uint32_t idx0) const {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     uint32_t pk[4], mine[4];
 #pragma unroll
@@ -264,7 +402,7 @@ struct PassCollector {
         for (int c = 0; c < 4; ++c) {
           if ((selm >> (4 * k + c)) & 1u) {
             const uint32_t idx = idx0 + 1024u * k + c;
-            dst[r++] = ((uint64_t)idx << 39) | tag | (uint64_t)(0x7fffffffu - mag_key(vv[c]));
+            dst[r++] = ((uint64_t)idx << 32) | (uint64_t)__float_as_uint(vv[c]);
           }
         }
       }
@@ -274,60 +412,96 @@ struct PassCollector {
 };
 
 // Pass 3: t' (written to the residual in the EF modes) and the candidates above the
-// sampled threshold, per item.  MODE 0: t' = alpha x (not stored); 1: r := r + alpha x;
-// 2: r := alpha x.
+// sampled threshold.  One 256-thread block per 1 Ki-element sub-chunk of an item (sub j of
+// item i is block 16 i + j), one float4 of x (and r) per thread: the shape that streams
+// fastest here (scripts/exp/ef_probe.py: r += x at 5.6 TB/s with one float4 per thread vs
+// 5.1 with 8 per thread or a persistent grid).  The sub's candidates go to its own element
+// range of `cand` in index order (one wave scan + one barrier), its count to sub_cnt.
+// MODE 0: t' = alpha x (not stored); 1: r := r + alpha x; 2: r := alpha x.
+constexpr int kSubPer = 1024;                 // elements per block of the fused pass
+constexpr int kSubsPerItem = (int)(kSub / kSubPer);  // 16
 template <int MODE>
-__global__ __launch_bounds__(kThreads, MODE == 0 ? 4 : 6) void topk_fused(const float* __restrict__ x, float* __restrict__ r, float alpha,
+__global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__ x, float* __restrict__ r, float alpha,
                                                        const Item* __restrict__ items,
                                                        const int64_t* __restrict__ tbegin,
                                                        const uint32_t* __restrict__ tbin,
-                                                       uint32_t* __restrict__ item_cnt, uint64_t* __restrict__ cand) {
-  __shared__ uint32_t s_wsum[4 * kWaves];
-  const Item it = items[blockIdx.x];
+                                                       uint32_t* __restrict__ sub_cnt, uint32_t* __restrict__ item_cnt,
+                                                       uint64_t* __restrict__ cand) {
+  __shared__ uint32_t s_w[kWaves];
+  const Item it = items[blockIdx.x / kSubsPerItem];
+  const int64_t b = it.begin + (int64_t)(blockIdx.x % kSubsPerItem) * kSubPer;
+  if (b >= it.end) {  // past a tensor's last sub-chunk
+    if (threadIdx.x == 0) sub_cnt[blockIdx.x] = 0;
+    return;
+  }
   const uint32_t thr = tbin[it.tensor];
   const int64_t base = tbegin[it.tensor];
-  constexpr int64_t CS = 8 * kThreads * 4;  // 8192 elements per pass
-  const PassCollector col{s_wsum};
-  const uint64_t tag = (uint64_t)it.tensor << 31;
-  uint32_t item_total = 0;
-  for (int64_t b = it.begin; b < it.end; b += CS) {
-    const uint32_t lim = (uint32_t)(min(b + CS, it.end) - b);
-    const uint32_t off0 = 4u * threadIdx.x;
-    float4 v[8];
-    uint32_t selm = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const uint32_t o = off0 + 1024u * k;
-      float vv[4] = {0.f, 0.f, 0.f, 0.f};
-      if (o + 4 <= lim) {
-        const float4 xv = *reinterpret_cast<const float4*>(x + b + o);
-        float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (MODE == 1) rv = *reinterpret_cast<const float4*>(r + b + o);
-        vv[0] = tprime<MODE>(xv.x, rv.x, alpha);
-        vv[1] = tprime<MODE>(xv.y, rv.y, alpha);
-        vv[2] = tprime<MODE>(xv.z, rv.z, alpha);
-        vv[3] = tprime<MODE>(xv.w, rv.w, alpha);
-        if (MODE != 0) *reinterpret_cast<float4*>(r + b + o) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-      } else {
-        for (uint32_t c = 0; c < 4 && o + c < lim; ++c) {
-          vv[c] = tprime<MODE>(x[b + o + c], MODE == 1 ? r[b + o + c] : 0.0f, alpha);
-          if (MODE != 0) r[b + o + c] = vv[c];
-        }
-      }
-      v[k] = make_float4(vv[0], vv[1], vv[2], vv[3]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (o + c < lim && (mag_key(vv[c]) >> kSShift) >= thr) selm |= 1u << (4 * k + c);
-    }
-    item_total += col.append(v, selm, cand + it.begin + item_total, (uint32_t)(b - base) + off0, tag);
+  const uint32_t lim = (uint32_t)(min(b + kSubPer, it.end) - b);
+  const uint32_t o = 4u * threadIdx.x;
+  // EF modes store the residual as if every candidate were selected (t' - t': 0, or NaN for
+  // an infinite t'); the candidates that end up unselected get t' back later (fewer random
+  // stores than zeroing the selection afterwards).
+  float vv[4] = {0.f, 0.f, 0.f, 0.f};
+  uint32_t selm = 0;
+  const bool full = o + 4 <= lim;
+  if (full) {
+    const float4 xv = *reinterpret_cast<const float4*>(x + b + o);
+    float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (MODE == 1) rv = *reinterpret_cast<const float4*>(r + b + o);
+    vv[0] = tprime<MODE>(xv.x, rv.x, alpha);
+    vv[1] = tprime<MODE>(xv.y, rv.y, alpha);
+    vv[2] = tprime<MODE>(xv.z, rv.z, alpha);
+    vv[3] = tprime<MODE>(xv.w, rv.w, alpha);
+  } else {
+    for (uint32_t c = 0; c < 4 && o + c < lim; ++c)
+      vv[c] = tprime<MODE>(x[b + o + c], MODE == 1 ? r[b + o + c] : 0.0f, alpha);
   }
-  if (threadIdx.x == 0) item_cnt[blockIdx.x] = item_total;
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    if (o + c < lim && (mag_key(vv[c]) >> kSShift) >= thr) selm |= 1u << c;
+  if (MODE != 0) {
+    float rr[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) rr[c] = ((selm >> c) & 1u) ? __fsub_rn(vv[c], vv[c]) : vv[c];
+    if (full) *reinterpret_cast<float4*>(r + b + o) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+    else
+      for (uint32_t c = 0; c < 4 && o + c < lim; ++c) r[b + o + c] = rr[c];
+  }
+  // ordered positions: wave inclusive scan of the counts, then the waves before mine
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t mine = (uint32_t)__popc(selm);
+  uint32_t inc = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
+  }
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  uint32_t pos = inc - mine, total = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < kWaves; ++w2) {
+    const uint32_t ws = s_w[w2];
+    if (w2 < wave) pos += ws;
+    total += ws;
+  }
+  if (selm) {
+    uint64_t* dst = cand + b;
+    const uint32_t idx0 = (uint32_t)(b - base) + o;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if ((selm >> c) & 1u) dst[pos++] = ((uint64_t)(idx0 + c) << 32) | (uint64_t)__float_as_uint(vv[c]);
+  }
+  if (threadIdx.x == 0) {
+    sub_cnt[blockIdx.x] = total;
+    if (total) atomicAdd(&item_cnt[blockIdx.x / kSubsPerItem], total);
+  }
 }
 
-// One block: exclusive scan of the per-item candidate counts (items in tensor order), then
-// per tensor its candidate count and start; flag the tensors whose threshold was too high.
-// status[0] = all candidates, status[1] = any flagged.  (Replaces a library scan: no
-// workspace clears, one launch.)
+// One block: exclusive scan of the per-item candidate counts (items in tensor order) in
+// tiles of 4 Ki items (coalesced loads, an LDS scan, a running carry), then per tensor its
+// candidate count and start; flag the tensors whose threshold was too high.
+// status[0] = all candidates, status[1] = any flagged.
 __global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_t* __restrict__ kk,
                                                         const uint32_t* __restrict__ tfirst,
                                                         const uint32_t* __restrict__ tlast,
@@ -338,35 +512,33 @@ __global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_
   __shared__ uint32_t part[1024];
   __shared__ uint32_t s_any;
   const int t = threadIdx.x;
-  const int64_t per = (n_items + 1023) / 1024;
-  const int64_t b = min((int64_t)t * per, n_items), e = min(b + per, n_items);
-  uint32_t loc = 0;
-  for (int64_t i = b; i < e; ++i) loc += item_cnt[i];
-  part[t] = loc;
   if (t == 0) s_any = 0;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {  // inclusive scan
-    const uint32_t add = t >= o ? part[t - o] : 0u;
-    __syncthreads();
-    part[t] += add;
-    __syncthreads();
+  uint32_t carry = 0;
+  for (int64_t t0 = 0; t0 < n_items; t0 += 4096) {
+    uint32_t c[4], loc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // items t0 + 4t + j
+      const int64_t i = t0 + 4 * t + j;
+      c[j] = i < n_items ? item_cnt[i] : 0u;
+      loc += c[j];
+    }
+    uint32_t tot;
+    const uint32_t inc = block_scan_incl<1024>(loc, part, tot);
+    uint32_t run = carry + inc - loc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = t0 + 4 * t + j;
+      if (i < n_items) item_off[i] = run;
+      run += c[j];
+    }
+    carry += tot;
   }
-  uint32_t run = part[t] - loc;
-  for (int64_t i = b; i < e; ++i) {
-    item_off[i] = run;
-    run += item_cnt[i];
-  }
-  // exclusive prefix of item i from the thread prefixes (no read-back of item_off)
-  auto prefix = [&](int64_t i) -> uint32_t {
-    const int64_t owner = i / per;
-    uint32_t v = owner > 0 ? part[owner - 1] : 0u;
-    for (int64_t j = owner * per; j < i; ++j) v += item_cnt[j];
-    return v;
-  };
+  __threadfence_block();
+  __syncthreads();  // item_off of every item visible to the block
   for (int32_t q = t; q < nt; q += 1024) {
     const uint32_t f = tfirst[q], l = tlast[q];
-    const uint32_t of = prefix(f);
-    const uint32_t c = prefix(l) + item_cnt[l] - of;
+    const uint32_t of = item_off[f];
+    const uint32_t c = item_off[l] + item_cnt[l] - of;
     cstart[q] = of;
     cnt[q] = c;
     const uint32_t redo = (int64_t)c < kk[q] ? 1u : 0u;
@@ -375,7 +547,7 @@ __global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_
   }
   __syncthreads();
   if (t == 0) {
-    status[0] = part[1023];
+    status[0] = carry;
     status[1] = s_any;
   }
 }
@@ -474,7 +646,8 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
                                                          const int64_t* __restrict__ tbegin,
                                                          const uint32_t* __restrict__ bin,
                                                          const uint32_t* __restrict__ flag, uint32_t* __restrict__ cnt,
-                                                         uint32_t* __restrict__ item_cnt, uint64_t* __restrict__ cand) {
+                                                         uint32_t* __restrict__ sub_cnt, uint32_t* __restrict__ item_cnt,
+                                                         uint64_t* __restrict__ cand) {
   __shared__ uint32_t s_wsum[4 * kWaves];
   __shared__ uint32_t s_base;
   const Item it = items[blockIdx.x];
@@ -485,7 +658,6 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
   constexpr int CV = 8;
   constexpr int64_t CS = (int64_t)CV * kThreads * 4;
   const PassCollector col{s_wsum};
-  const uint64_t tag = (uint64_t)it.tensor << 31;
   uint32_t item_total = 0;
   for (int64_t b = it.begin; b < it.end; b += CS) {
     const uint32_t lim = (uint32_t)(min(b + CS, it.end) - b);
@@ -510,7 +682,7 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
         if (o + c < lim && (mag_key(vv[c]) >> kShift) >= b1) selm |= 1u << (4 * k + c);
     }
     if (GLOBAL) {
-      item_total += col.append(v, selm, cand + it.begin + item_total, (uint32_t)(b - base) + off0, tag);
+      item_total += col.append(v, selm, cand + it.begin + item_total, (uint32_t)(b - base) + off0);
       continue;
     }
     const uint32_t nsel = (uint32_t)__popc(selm);
@@ -548,18 +720,457 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
     }
     __syncthreads();  // s_wsum / s_base reuse
   }
+  if (GLOBAL && threadIdx.x < kSubsPerItem)  // the item's candidates as one run (sub 0)
+    sub_cnt[(size_t)blockIdx.x * kSubsPerItem + threadIdx.x] = threadIdx.x == 0 ? item_total : 0u;
   if (GLOBAL && threadIdx.x == 0) item_cnt[blockIdx.x] = item_total;
 }
 
-// Pack every item's candidates (stored at the item's element range) at its scanned offset.
+// The 16 sub-chunk candidate counts of item `item` -> s_pre[0..16] (exclusive prefix, s_pre[16]
+// = the item's total).  Wave 0 scans; ends with a block barrier.
+__device__ __forceinline__ void item_prefix(const uint32_t* __restrict__ sub_cnt, int64_t item, uint32_t* s_pre) {
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    uint32_t v = l < kSubsPerItem ? sub_cnt[(size_t)item * kSubsPerItem + l] : 0u;
+#pragma unroll
+    for (int d = 1; d < kSubsPerItem; d <<= 1) {
+      const uint32_t u = __shfl_up(v, d, 64);
+      if (l >= d) v += u;
+    }
+    if (l < kSubsPerItem) s_pre[l + 1] = v;
+    if (l == 0) s_pre[0] = 0;
+  }
+  __syncthreads();
+}
+
+// Candidate e of the item (in index order): sub j's run lives at the sub's element range.
+__device__ __forceinline__ uint64_t item_key(const uint64_t* __restrict__ cand, int64_t begin, const uint32_t* s_pre,
+                                             uint32_t e) {
+  int j = 0;  // the sub with s_pre[j] <= e < s_pre[j + 1]
+#pragma unroll
+  for (int h = kSubsPerItem / 2; h > 0; h >>= 1)
+    if (s_pre[j + h] <= e) j += h;
+  return cand[begin + (int64_t)j * kSubPer + (e - s_pre[j])];
+}
+
+// Fallback path: pack every item's candidates at its scanned offset, in order, as device-wide
+// sort keys index << 39 | tensor << 31 | (2^31 - 1 - |t'|bits) (a stable sort of the low 39
+// bits gives tensor ascending, |t'| descending, index ascending).
 __global__ __launch_bounds__(kThreads) void topk_compact(const uint64_t* __restrict__ cand,
                                                          const Item* __restrict__ items,
-                                                         const uint32_t* __restrict__ item_cnt,
+                                                         const uint32_t* __restrict__ sub_cnt,
                                                          const uint32_t* __restrict__ item_off,
                                                          uint64_t* __restrict__ packed) {
+  __shared__ uint32_t s_pre[kSubsPerItem + 1];
   const Item it = items[blockIdx.x];
-  const uint32_t n = item_cnt[blockIdx.x], dst = item_off[blockIdx.x];
-  for (uint32_t j = threadIdx.x; j < n; j += kThreads) packed[dst + j] = cand[it.begin + j];
+  item_prefix(sub_cnt, blockIdx.x, s_pre);
+  const uint32_t n = s_pre[kSubsPerItem];
+  uint64_t* dst = packed + item_off[blockIdx.x];
+  const uint64_t tag = (uint64_t)it.tensor << 31;
+  for (uint32_t e = threadIdx.x; e < n; e += kThreads) {
+    const uint64_t key = item_key(cand, it.begin, s_pre, e);
+    dst[e] = ((key >> 32) << 39) | tag | (uint64_t)(0x7fffffffu - ((uint32_t)key & 0x7fffffffu));
+  }
+}
+
+// Fast path: a "super-item" is up to kSupItems consecutive items (16 Ki-element chunks) of one
+// tensor, handled by one 1024-thread block so that per-tensor LDS tables (fine-bin counts,
+// bucket counts) aggregate many keys before touching global memory.  SupView maps the block
+// to its tensor and lists its candidates (sub-chunk runs, in index order).
+struct SupView {
+  uint32_t* s_spre;   // [1025] exclusive prefix of the runs' counts
+  int64_t* s_ibeg;    // [kSupItems] arena offsets of the items
+  int t;
+  uint32_t total;
+  __device__ __forceinline__ void init(const uint32_t* __restrict__ sbase, int32_t nt,
+                                       const uint32_t* __restrict__ tfirst, const uint32_t* __restrict__ tlast,
+                                       const Item* __restrict__ items, const uint32_t* __restrict__ sub_cnt,
+                                       uint32_t* s_part, int* s_t) {
+    if (threadIdx.x == 0) {  // the tensor: sbase[t] <= blockIdx.x < sbase[t + 1]
+      int lo = 0, hi = nt - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (sbase[mid] <= blockIdx.x) lo = mid;
+        else hi = mid - 1;
+      }
+      *s_t = lo;
+    }
+    __syncthreads();
+    t = *s_t;
+    const uint32_t i0 = tfirst[t] + (blockIdx.x - sbase[t]) * kSupItems;
+    const uint32_t ni = min((uint32_t)kSupItems, tlast[t] + 1 - i0);
+    const uint32_t run = threadIdx.x;  // run j of item j / 16
+    const uint32_t c = run < ni * kSubsPerItem ? sub_cnt[(size_t)i0 * kSubsPerItem + run] : 0u;
+    if (threadIdx.x < ni) s_ibeg[threadIdx.x] = items[i0 + threadIdx.x].begin;
+    uint32_t tot;
+    s_spre[threadIdx.x + 1] = block_scan_incl<1024>(c, s_part, tot);
+    if (threadIdx.x == 0) s_spre[0] = 0;
+    __syncthreads();
+    total = s_spre[1024];
+  }
+  // arena position of candidate e (< total) in the cand buffer
+  __device__ __forceinline__ int64_t pos(uint32_t e) const {
+    int j = 0;  // the run with s_spre[j] <= e < s_spre[j + 1]
+#pragma unroll
+    for (int h = 512; h > 0; h >>= 1)
+      if (s_spre[j + h] <= e) j += h;
+    return s_ibeg[j >> 4] + (int64_t)(j & 15) * kSubPer + (e - s_spre[j]);
+  }
+};
+
+// Fallback path, first step in the EF modes: the residual of every candidate back to t'
+// (the fused pass stored t' - t' there), so the radix-sort path sees the plain t' state.
+__global__ __launch_bounds__(kThreads) void topk_restore(const uint64_t* __restrict__ cand,
+                                                         const Item* __restrict__ items,
+                                                         const uint32_t* __restrict__ sub_cnt,
+                                                         const int64_t* __restrict__ tbegin,
+                                                         float* __restrict__ r) {
+  __shared__ uint32_t s_pre[kSubsPerItem + 1];
+  const Item it = items[blockIdx.x];
+  item_prefix(sub_cnt, blockIdx.x, s_pre);
+  const uint32_t n = s_pre[kSubsPerItem];
+  const int64_t base = tbegin[it.tensor];
+  for (uint32_t e = threadIdx.x; e < n; e += kThreads) {
+    const uint64_t key = item_key(cand, it.begin, s_pre, e);
+    r[base + (key >> 32)] = __uint_as_float((uint32_t)key);
+  }
+}
+
+// Fast path, pass H: the exact fine-bin histogram of every tensor's candidates (LDS counts per
+// super-item, flushed with one global atomic per touched bin).
+__global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restrict__ cand,
+                                                       const Item* __restrict__ items,
+                                                       const uint32_t* __restrict__ sub_cnt,
+                                                       const uint32_t* __restrict__ sbase, int32_t nt,
+                                                       const uint32_t* __restrict__ tfirst,
+                                                       const uint32_t* __restrict__ tlast,
+                                                       const uint32_t* __restrict__ fmap,
+                                                       const uint32_t* __restrict__ tlo,
+                                                       const uint32_t* __restrict__ fcount,
+                                                       uint32_t* __restrict__ fhist) {
+  __shared__ uint32_t s_h[kFineMax];
+  __shared__ uint32_t s_spre[1025], s_part[1024];
+  __shared__ int64_t s_ibeg[kSupItems];
+  __shared__ int s_t;
+  SupView v{s_spre, s_ibeg, 0, 0};
+  for (int i = threadIdx.x; i < kFineMax; i += 1024) s_h[i] = 0;
+  v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t);
+  const uint32_t lo = tlo[v.t], F = fcount[v.t];
+  const uint32_t* map_t = fmap + (size_t)v.t * kCoarse;
+  constexpr int U = 4;
+  for (uint32_t e0 = threadIdx.x; e0 < v.total; e0 += U * 1024) {
+    uint64_t key[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e = min(e0 + (uint32_t)u * 1024, v.total - 1);
+      key[u] = cand[v.pos(e)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (e0 + (uint32_t)u * 1024 < v.total)
+        atomicAdd(&s_h[fine_bin((uint32_t)key[u] & 0x7fffffffu, lo, map_t, F)], 1u);
+  }
+  __syncthreads();
+  uint32_t* h = fhist + (size_t)v.t * kFineMax;
+  for (uint32_t i = threadIdx.x; i < F; i += 1024)
+    if (s_h[i]) atomicAdd(&h[i], s_h[i]);
+}
+
+// Fast path, plan (one block per tensor): suffix counts of the fine bins from the top; the
+// bins that start above rank k are kept, bin i goes to bucket floor(se_i / kBucketHalf)
+// (se_i = keys in higher bins), a bucket starts at its smallest se.  Flags the tensor for
+// the exact redo when it has fewer than k candidates, and the call for the fallback sort
+// when a kept fine bin holds more than kBucketHalf keys.  status[1] |= redo, [2] |= overflow.
+__global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
+                                                  const uint32_t* __restrict__ fhist,
+                                                  const uint32_t* __restrict__ bbase, int32_t* __restrict__ fbucket,
+                                                  uint32_t* __restrict__ bstart, BucketRec* __restrict__ brec,
+                                                  uint32_t* __restrict__ bfill, const int64_t* __restrict__ kb2,
+                                                  uint32_t* __restrict__ flag, uint32_t* __restrict__ status,
+                                                  int dbg) {
+  constexpr int PER = kFineMax / 1024;
+  __shared__ uint32_t s_bs[kPlanMaxBuckets];
+  __shared__ uint32_t part[1024];
+  __shared__ uint32_t s_kend, s_nb, s_over;
+  const int t = blockIdx.x;
+  const uint32_t F = fcount[t];
+  const uint64_t k = (uint64_t)kk[t];
+  const uint32_t b0 = bbase[t], nbmax = bbase[t + 1] - b0;
+  const uint32_t* ht = fhist + (size_t)t * kFineMax;
+  uint32_t h[PER], loc = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t i = PER * threadIdx.x + j;
+    h[j] = i < F ? ht[i] : 0u;
+    loc += h[j];
+  }
+  if (threadIdx.x == 0) {
+    s_kend = 0;
+    s_nb = 0;
+    s_over = 0;
+  }
+  for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) s_bs[j] = 0xffffffffu;
+  uint32_t tot32;
+  const uint32_t inc = block_scan_incl<1024>(loc, part, tot32);
+  const uint64_t total = tot32;
+  if (total < k) {  // the sampled threshold was too high: exact redo (fallback path)
+    if (threadIdx.x == 0) {
+      flag[t] = 1u;
+      atomicOr(&status[1], 1u);
+    }
+    for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) brec[b0 + j] = BucketRec{0, 0, 0};
+    return;
+  }
+  uint64_t se = tot32 - inc;  // keys in the bins of higher threads
+  int32_t* fb = fbucket + (size_t)t * kFineMax;
+  for (int j = PER - 1; j >= 0; --j) {
+    const uint32_t i = PER * threadIdx.x + j;
+    int32_t bucket = -1;
+    if (h[j] && se < k) {
+      bucket = (int32_t)(se / kBucketHalf);
+      atomicMin(&s_bs[bucket], (uint32_t)se);
+      if (h[j] > (uint32_t)kBucketHalf) {
+        s_over = 1u;
+        if (dbg & 8) printf("omf_topk plan: tensor %d fine bin %u of %u holds %u (se %llu k %llu)\n", t, i, F, h[j],
+                            (unsigned long long)se, (unsigned long long)k);
+      }
+      if (se + h[j] >= k) {  // the bin of the k-th key (exactly one)
+        s_kend = (uint32_t)(se + h[j]);
+        s_nb = (uint32_t)bucket + 1u;
+      }
+    }
+    if (i < F) fb[i] = bucket;
+    se += h[j];
+  }
+  __syncthreads();
+  const uint32_t nb = s_nb;
+  for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) {
+    const uint32_t g = b0 + j;
+    uint32_t st = 0, c = 0;
+    if (j < nb && s_bs[j] != 0xffffffffu) {
+      st = s_bs[j];
+      const uint32_t en = j + 1 < nb ? s_bs[j + 1] : s_kend;
+      c = en > st ? en - st : 0u;
+    }
+    bstart[g] = st;
+    brec[g] = BucketRec{(uint64_t)kb2[t] + st, st, min(c, 0xffffu) | ((uint32_t)t << 16)};
+    bfill[g] = 0;
+  }
+  if (threadIdx.x == 0) {
+    flag[t] = 0;
+    if (s_over) atomicOr(&status[2], 1u);
+  }
+}
+
+// Fast path, scatter: every kept candidate into its bucket (rank window of the tensor's
+// region kb2[t] of the bucket buffer).  Per super-item: LDS counts per bucket, one global
+// reservation per touched bucket, then LDS ranks.  Order inside a bucket is arbitrary (the
+// bucket sort orders by the full key).
+__global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __restrict__ cand,
+                                                            const Item* __restrict__ items,
+                                                            const uint32_t* __restrict__ sub_cnt,
+                                                            const uint32_t* __restrict__ sbase, int32_t nt,
+                                                            const uint32_t* __restrict__ tfirst,
+                                                            const uint32_t* __restrict__ tlast,
+                                                            const uint32_t* __restrict__ fmap,
+                                                            const uint32_t* __restrict__ tlo,
+                                                            const uint32_t* __restrict__ fcount,
+                                                            const int32_t* __restrict__ fbucket,
+                                                            const uint32_t* __restrict__ bbase,
+                                                            const uint32_t* __restrict__ bstart,
+                                                            uint32_t* __restrict__ bfill,
+                                                            const int64_t* __restrict__ kb2,
+                                                            const int64_t* __restrict__ tbegin,
+                                                            float* __restrict__ r, uint64_t* __restrict__ bkeys,
+                                                            const uint32_t* __restrict__ status) {
+  if (status[1] | status[2]) return;  // the plan's verdict is a fallback: nothing to do
+  __shared__ uint32_t s_b[kPlanMaxBuckets];
+  __shared__ uint32_t s_spre[1025], s_part[1024];
+  __shared__ int64_t s_ibeg[kSupItems];
+  __shared__ int s_t;
+  SupView v{s_spre, s_ibeg, 0, 0};
+  v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t);
+  const int t = v.t;
+  const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nb = bbase[t + 1] - b0;
+  const int64_t base = tbegin[t];
+  for (uint32_t j = threadIdx.x; j < nb; j += 1024) s_b[j] = 0;
+  __syncthreads();
+  const uint32_t* map_t = fmap + (size_t)t * kCoarse;
+  const int32_t* fb = fbucket + (size_t)t * kFineMax;
+  constexpr int U = 4;
+  for (int phase = 0; phase < 2; ++phase) {  // 0: count per bucket; 1: place
+    uint64_t* dst = bkeys + kb2[t];
+    for (uint32_t e0 = threadIdx.x; e0 < v.total; e0 += U * 1024) {
+      uint64_t key[U];
+      int32_t j[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t e = min(e0 + (uint32_t)u * 1024, v.total - 1);
+        key[u] = cand[v.pos(e)];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) j[u] = fb[fine_bin((uint32_t)key[u] & 0x7fffffffu, lo, map_t, F)];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (e0 + (uint32_t)u * 1024 >= v.total) continue;
+        if (j[u] < 0) {  // below the k-th key's bin: never selected; its residual is t' again
+          if (phase == 1 && r) r[base + (key[u] >> 32)] = __uint_as_float((uint32_t)key[u]);
+          continue;
+        }
+        if (phase == 0) {
+          atomicAdd(&s_b[j[u]], 1u);
+        } else {
+          const uint32_t p = atomicAdd(&s_b[j[u]], 1u);
+          dst[p] = key[u];
+        }
+      }
+    }
+    __syncthreads();
+    if (phase == 0) {  // reserve each touched bucket's range; s_b := this block's first slot
+      for (uint32_t q = threadIdx.x; q < nb; q += 1024)
+        if (s_b[q]) s_b[q] = bstart[b0 + q] + atomicAdd(&bfill[b0 + q], s_b[q]);
+      __syncthreads();
+    }
+  }
+}
+
+// Fast path, one block per bucket: order its <= 2 kBucketHalf keys by (|t'| descending, index
+// ascending) in LDS and write the ranks below k: values, int64 indices, and (error feedback)
+// zero the selected residual slots.  Ordering is a counting sort on 4096 sub-bins that split
+// the bucket's |t'| range evenly (about one key per sub-bin), then an insertion sort inside
+// each sub-bin; a bucket with a sub-bin of more than kMaxRun keys (ties, clusters) is merge
+// sorted instead.  Sort key: (2^31-1-|t'|bits) << 33 | index << 1 | sign.
+constexpr int kSubBins = kBT * kBI;  // 4096
+constexpr uint32_t kMaxRun = 32;
+using BucketSort = rocprim::block_sort<uint64_t, kBT, kBI, rocprim::empty_type,
+                                       rocprim::block_sort_algorithm::merge_sort>;
+__global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void topk_bucket_sort(const uint64_t* __restrict__ bkeys,
+                                                             const BucketRec* __restrict__ brec,
+                                                             const int64_t* __restrict__ kk,
+                                                             const int64_t* __restrict__ koff,
+                                                             const int64_t* __restrict__ tbegin,
+                                                             const int64_t* __restrict__ tsize, float* __restrict__ r,
+                                                             float* __restrict__ values,
+                                                             int64_t* __restrict__ indices,
+                                                             const uint32_t* __restrict__ status, int dbg) {
+  __shared__ union {
+    typename BucketSort::storage_type sort;
+    uint64_t xch[kSubBins];
+    struct {
+      uint64_t out[kSubBins];
+      uint32_t start[kSubBins];
+    } cs;
+  } s_u;
+  __shared__ uint32_t s_part[kBT];
+  __shared__ uint32_t s_min, s_max, s_cmax;
+  const BucketRec rec = brec[blockIdx.x];
+  const uint32_t cnt = rec.count_tensor & 0xffffu;
+  if (cnt == 0 || (status[1] | status[2])) return;  // block-uniform (a fallback verdict: nothing to do)
+  const int t = (int)(rec.count_tensor >> 16);
+  const uint32_t st = rec.start;
+  const uint64_t* src = bkeys + rec.key_off;
+  const int64_t k = kk[t], o = koff[t], base = tbegin[t], n = tsize[t];  // issued with the key loads
+  if (threadIdx.x == 0) {
+    s_min = 0xffffffffu;
+    s_max = 0;
+    s_cmax = 0;
+  }
+  uint64_t keys[kBI];
+  uint32_t lmin = 0xffffffffu, lmax = 0;
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {  // striped loads
+    const uint32_t e = threadIdx.x + (uint32_t)j * kBT;
+    uint64_t sk = ~0ull;
+    if (e < cnt) {
+      const uint64_t key = src[e];
+      const uint32_t bits = (uint32_t)key, inv = 0x7fffffffu - (bits & 0x7fffffffu);
+      sk = ((uint64_t)inv << 33) | ((key >> 32) << 1) | (uint64_t)(bits >> 31);
+      lmin = min(lmin, inv);
+      lmax = max(lmax, inv);
+    }
+    keys[j] = sk;
+  }
+  for (int i = threadIdx.x; i < kSubBins; i += kBT) s_u.cs.start[i] = 0;
+  __syncthreads();
+  if (lmin <= lmax) {
+    atomicMin(&s_min, lmin);
+    atomicMax(&s_max, lmax);
+  }
+  __syncthreads();
+  const uint32_t imin = s_min;
+  const uint64_t span = (uint64_t)(s_max - imin) + 1;
+  uint32_t meta[kBI];  // sub-bin << 16 | slot in it
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {
+    meta[j] = 0xffffffffu;
+    if (threadIdx.x + (uint32_t)j * kBT < cnt) {
+      const uint32_t sub = (uint32_t)((((keys[j] >> 33) - imin) * (uint64_t)kSubBins) / span);
+      meta[j] = (sub << 16) | atomicAdd(&s_u.cs.start[sub], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t c[kBI], loc = 0, cmx = 0;  // this thread's sub-bins kBI tid ..
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {
+    c[j] = s_u.cs.start[threadIdx.x * kBI + j];
+    loc += c[j];
+    cmx = max(cmx, c[j]);
+  }
+  if (cmx > kMaxRun) atomicMax(&s_cmax, cmx);
+  uint32_t tot;
+  const uint32_t inc = block_scan_incl<kBT>(loc, s_part, tot);  // (its barriers publish s_cmax)
+  const bool merge = s_cmax > kMaxRun;  // block-uniform
+  if (!merge && !(dbg & 1)) {
+    uint32_t run = inc - loc;
+#pragma unroll
+    for (int j = 0; j < kBI; ++j) {
+      s_u.cs.start[threadIdx.x * kBI + j] = run;
+      run += c[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kBI; ++j)
+      if (meta[j] != 0xffffffffu) s_u.cs.out[s_u.cs.start[meta[j] >> 16] + (meta[j] & 0xffffu)] = keys[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kBI; ++j) {  // insertion sort inside each sub-bin
+      if (c[j] < 2) continue;
+      uint64_t* a = s_u.cs.out + s_u.cs.start[threadIdx.x * kBI + j];
+      for (uint32_t x = 1; x < c[j]; ++x) {
+        const uint64_t v = a[x];
+        uint32_t y = x;
+        for (; y > 0 && a[y - 1] > v; --y) a[y] = a[y - 1];
+        a[y] = v;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kBI; ++j) keys[j] = s_u.cs.out[threadIdx.x + j * kBT];
+  } else if (merge) {
+    __syncthreads();
+    BucketSort().sort(keys, s_u.sort);
+    __syncthreads();  // blocked (thread i: ranks kBI i ..) -> striped, for coalesced stores
+#pragma unroll
+    for (int j = 0; j < kBI; ++j) s_u.xch[threadIdx.x * kBI + j] = keys[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kBI; ++j) keys[j] = s_u.xch[threadIdx.x + j * kBT];
+  }
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {
+    const uint32_t p = threadIdx.x + (uint32_t)j * kBT;
+    if (p >= cnt) break;
+    const int64_t rank = (int64_t)st + p;
+    const uint64_t sk = keys[j];
+    const uint32_t idx = (uint32_t)(sk >> 1) & 0x3ffffffu;
+    if ((int64_t)idx >= n) continue;  // never expected (a padding key inside the bucket's count)
+    const float v = __uint_as_float(((uint32_t)(sk & 1u) << 31) | (0x7fffffffu - (uint32_t)(sk >> 33)));
+    if (rank < k) {
+      values[o + rank] = v;
+      indices[o + rank] = (int64_t)idx;
+    } else if (r && !(dbg & 2)) {
+      r[base + idx] = v;  // a candidate of the k-th key's bin below rank k: unselected
+    }
+  }
 }
 
 template <bool GLOBAL>
@@ -651,6 +1262,40 @@ namespace {
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// OMF_TOPK_FALLBACK=1: always take the device-wide radix-sort path (tests of that path).
+// Per host thread and device: a pinned 16-byte status buffer and an event (never freed: a
+// few bytes per thread that calls the encoder).
+struct HostSync {
+  uint32_t* pinned = nullptr;
+  hipEvent_t ev = nullptr;
+};
+HostSync* host_sync(int dev) {
+  constexpr int kMaxDev = 64;
+  thread_local HostSync hs[kMaxDev];
+  if (dev < 0 || dev >= kMaxDev) return nullptr;
+  HostSync& h = hs[dev];
+  if (!h.pinned) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 16, hipHostMallocDefault) != hipSuccess) return nullptr;
+    if (hipEventCreateWithFlags(&h.ev, hipEventDisableTiming) != hipSuccess) {
+      (void)hipHostFree(p);
+      return nullptr;
+    }
+    h.pinned = static_cast<uint32_t*>(p);
+  }
+  return &h;
+}
+
+int dbg_bits() {  // OMF_TOPK_DBG (experiments): 1 = no bucket sort, 2 = no residual zeroing
+  const char* e = std::getenv("OMF_TOPK_DBG");
+  return e ? std::atoi(e) : 0;
+}
+
+bool force_fallback() {
+  const char* e = std::getenv("OMF_TOPK_FALLBACK");
+  return e && e[0] == '1';
+}
+
 bool global_path(const omf_plan* p) {
   if (omf_plan_access::ntensors(p) > 256) return false;
   for (int64_t n : omf_plan_access::sizes(p))
@@ -677,8 +1322,16 @@ size_t sort_tmp_bytes(const omf_plan* p) {
 // sampled path clears its redo histograms in topk_sample_threshold and writes the rest.
 struct WsLayout {
   size_t hist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
-      item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes;
+      sub_cnt, item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes, bbase, kb2, fmap, tlo, fcount, fhist,
+      fbucket, bstart, brec, bfill, nb_max, sbase;
 };
+
+// Bucket-table slots for any ratio (k <= n).
+size_t bucket_slots_max(const omf_plan* p) {
+  size_t nb = 0;
+  for (int64_t n : omf_plan_access::sizes(p)) nb += (size_t)((n + kBucketHalf) / kBucketHalf + 1);
+  return nb;
+}
 
 WsLayout layout(const omf_plan* p) {
   const int32_t nt = omf_plan_access::ntensors(p);
@@ -701,10 +1354,24 @@ WsLayout layout(const omf_plan* p) {
   L.cstart = o; o = align256(o + 8 * (size_t)nt);
   int64_t n_items = 0;
   (void)omf_plan_access::flat_items(p, &n_items);
+  L.sub_cnt = o; o = align256(o + 4 * (size_t)n_items * kSubsPerItem);
   L.item_cnt = o; o = align256(o + 4 * (size_t)n_items);
   L.item_off = o; o = align256(o + 4 * (size_t)n_items);
   L.cand = o; o = align256(o + 8 * (size_t)ae);
-  L.sorted = o; o = align256(o + 8 * (size_t)ae);
+  // the fallback's packed keys, or the fast path's buckets (k_t + kBucketHalf per tensor)
+  L.sorted = o; o = align256(o + 8 * ((size_t)ae + (size_t)nt * kBucketHalf));
+  L.bbase = o; o = align256(o + 4 * (size_t)(nt + 1));
+  L.sbase = o; o = align256(o + 4 * (size_t)(nt + 1));
+  L.kb2 = o; o = align256(o + 8 * (size_t)nt);
+  L.fmap = o; o = align256(o + 4 * (size_t)nt * kCoarse);
+  L.tlo = o; o = align256(o + 4 * (size_t)nt);
+  L.fcount = o; o = align256(o + 4 * (size_t)nt);
+  L.fhist = o; o = align256(o + 4 * (size_t)nt * kFineMax);
+  L.fbucket = o; o = align256(o + 4 * (size_t)nt * kFineMax);
+  L.nb_max = bucket_slots_max(p);
+  L.bstart = o; o = align256(o + 4 * L.nb_max);
+  L.brec = o; o = align256(o + sizeof(BucketRec) * L.nb_max);
+  L.bfill = o; o = align256(o + 4 * L.nb_max);
   L.tmp_bytes = sort_tmp_bytes(p);
   L.tmp = o; o = align256(o + L.tmp_bytes);
   L.total = o;
@@ -735,11 +1402,15 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   if (!(ratio == ratio)) return fail(OMF_EINVAL, "ratio is NaN");
   const std::vector<int64_t>& sizes = omf_plan_access::sizes(plan);
   int64_t kmax = 0;
+  size_t nbuckets = 0;  // bucket-table slots of this ratio
+  size_t nsup = 0;      // super-items
   for (int64_t n : sizes) {
     const int64_t k = omf_topk_k(n, ratio);
     if (k > n) return fail(OMF_EINVAL, "selected index k out of range (k > numel): compress_ratio too large");
     if (n > 0x7fffffffLL) return fail(OMF_EINVAL, "tensor too large for 32-bit candidate indices");
     kmax = std::max(kmax, k);
+    nbuckets += (size_t)((k + kBucketHalf) / kBucketHalf + 1);
+    nsup += (size_t)(((n + kSub - 1) / kSub + kSupItems - 1) / kSupItems);
   }
   if (omf_plan_access::arena_end(plan) > 0xffffffffLL) return fail(OMF_EINVAL, "arena too large for the sort");
   if (((uintptr_t)x & 15) || (residual && ((uintptr_t)residual & 15)))
@@ -763,10 +1434,22 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   uint32_t* seg_b = reinterpret_cast<uint32_t*>(w + L.seg_b);
   uint32_t* seg_e = reinterpret_cast<uint32_t*>(w + L.seg_e);
   int64_t* cstart = reinterpret_cast<int64_t*>(w + L.cstart);
+  uint32_t* sub_cnt = reinterpret_cast<uint32_t*>(w + L.sub_cnt);
   uint32_t* item_cnt = reinterpret_cast<uint32_t*>(w + L.item_cnt);
   uint32_t* item_off = reinterpret_cast<uint32_t*>(w + L.item_off);
   uint64_t* cand = reinterpret_cast<uint64_t*>(w + L.cand);
   uint64_t* sorted = reinterpret_cast<uint64_t*>(w + L.sorted);
+  uint32_t* bbase = reinterpret_cast<uint32_t*>(w + L.bbase);
+  uint32_t* sbase = reinterpret_cast<uint32_t*>(w + L.sbase);
+  int64_t* kb2 = reinterpret_cast<int64_t*>(w + L.kb2);
+  uint32_t* fmap = reinterpret_cast<uint32_t*>(w + L.fmap);
+  uint32_t* tlo = reinterpret_cast<uint32_t*>(w + L.tlo);
+  uint32_t* fcount = reinterpret_cast<uint32_t*>(w + L.fcount);
+  uint32_t* fhist = reinterpret_cast<uint32_t*>(w + L.fhist);
+  int32_t* fbucket = reinterpret_cast<int32_t*>(w + L.fbucket);
+  uint32_t* bstart = reinterpret_cast<uint32_t*>(w + L.bstart);
+  BucketRec* brec = reinterpret_cast<BucketRec*>(w + L.brec);
+  uint32_t* bfill = reinterpret_cast<uint32_t*>(w + L.bfill);
   const int32_t nt = omf_plan_access::ntensors(plan);
   int64_t n_items = 0;
   const Item* items = static_cast<const Item*>(omf_plan_access::flat_items(plan, &n_items));
@@ -775,30 +1458,58 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   // t' lives in the residual (EF modes) or is alpha * x (mode 0)
   const float* tp = residual_mode == 0 ? x : residual;
   const float scale = residual_mode == 0 ? alpha : 1.0f;
-  float* rz = residual_mode ? residual : nullptr;  // selected slots to zero
+  float* rz = residual_mode ? residual : nullptr;  // residual fix-ups (restores / zeroing)
   const dim3 grid((unsigned)n_items), blk(kThreads);
 
   const bool glob = global_path(plan);
   if (!glob) OMF_HIP(hipMemsetAsync(w, 0, L.zero_end, st));
-  hipLaunchKernelGGL(topk_setup, dim3(1), blk, 0, st, d_sizes, nt, ratio, kk, koff, tfirst, tlast);
+  hipLaunchKernelGGL(topk_setup, dim3(1), blk, 0, st, d_sizes, nt, ratio, kk, koff, tfirst, tlast, bbase, kb2, sbase, status);
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
-    const dim3 sgrid((unsigned)nt), sblk(1024);
+    const dim3 sgrid((unsigned)nt), sblk(1024), fgrid((unsigned)(n_items * kSubsPerItem));
     if (residual_mode == 1) {
       hipLaunchKernelGGL((topk_sample_threshold<1>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
-                         tbin, hist);
-      hipLaunchKernelGGL((topk_fused<1>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt, cand);
+                         tfirst, tlast, tbin, hist, item_cnt, fmap, tlo, fcount, fhist);
+      hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, sub_cnt, item_cnt, cand);
     } else {
       hipLaunchKernelGGL((topk_sample_threshold<0>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
-                         tbin, hist);
+                         tfirst, tlast, tbin, hist, item_cnt, fmap, tlo, fcount, fhist);
       if (residual_mode == 2)
-        hipLaunchKernelGGL((topk_fused<2>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt,
-                           cand);
+        hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, sub_cnt,
+                           item_cnt, cand);
       else
-        hipLaunchKernelGGL((topk_fused<0>), grid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, item_cnt,
-                           cand);
+        hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, sub_cnt,
+                           item_cnt, cand);
     }
-    uint32_t host_status[2] = {0, 0};
+    // fast path: exact fine-bin histograms, bucket plan; one status read decides
+    const dim3 supgrid((unsigned)nsup), supblk(1024);
+    hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast, fmap,
+                       tlo, fcount, fhist);
+    hipLaunchKernelGGL(topk_plan, sgrid, sblk, 0, st, kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2,
+                       flag, status, dbg_bits());
+    OMF_HIP(hipGetLastError());
+    // The plan's verdict goes to pinned host memory behind an event; the bucket kernels are
+    // enqueued before the host waits for it (they do nothing when the verdict is a fallback),
+    // so the GPU does not idle while the host reads it.
+    HostSync* hsync = host_sync(omf_plan_access::device(plan));
+    if (!hsync) return fail(OMF_EHIP, "omf_topk_encode: pinned status buffer");
+    OMF_HIP(hipMemcpyAsync(hsync->pinned, status, 16, hipMemcpyDeviceToHost, st));
+    OMF_HIP(hipEventRecord(hsync->ev, st));
+    const bool forced = force_fallback();
+    if (!forced) {
+      hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast,
+                         fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins, rz, sorted, status);
+      hipLaunchKernelGGL(topk_bucket_sort, dim3((unsigned)nbuckets), dim3(kBT), 0, st, sorted, brec, kk, koff, d_begins,
+                         d_sizes, rz, values, indices, status, dbg_bits());
+      OMF_HIP(hipGetLastError());
+    }
+    OMF_HIP(hipEventSynchronize(hsync->ev));
+    uint32_t host_status[4];
+    std::memcpy(host_status, hsync->pinned, 16);
+    if (dbg_bits() & 4) fprintf(stderr, "omf_topk: redo %u overflow %u\n", host_status[1], host_status[2]);
+    if (!host_status[1] && !host_status[2] && !forced) return OMF_OK;
+    // fallback (a redo, a fine bin over kBucketHalf keys, or forced): device-wide radix sort
+    if (rz) hipLaunchKernelGGL(topk_restore, grid, blk, 0, st, cand, items, sub_cnt, d_begins, rz);
     auto scan_and_check = [&]() -> int {
       hipLaunchKernelGGL(topk_scan_check, dim3(1), dim3(1024), 0, st, nt, kk, tfirst, tlast, item_cnt, item_off,
                          n_items, cstart, cnt, flag, status);
@@ -812,12 +1523,12 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     if (host_status[1]) {  // a sample set the threshold too high for some tensor: redo it exactly
       hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, tp, nullptr, scale, items, flag, hist);
       hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, flag, bin);
-      hipLaunchKernelGGL((topk_collect<true>), grid, blk, 0, st, tp, scale, items, d_begins, bin, flag, cnt, item_cnt,
-                         cand);
+      hipLaunchKernelGGL((topk_collect<true>), grid, blk, 0, st, tp, scale, items, d_begins, bin, flag, cnt, sub_cnt,
+                         item_cnt, cand);
       if (int rc = scan_and_check()) return rc;
     }
     const uint64_t total = host_status[0];
-    hipLaunchKernelGGL(topk_compact, grid, blk, 0, st, cand, items, item_cnt, item_off, sorted);
+    hipLaunchKernelGGL(topk_compact, grid, blk, 0, st, cand, items, sub_cnt, item_off, sorted);
     // sort the packed keys back into `cand` (the per-item regions are no longer needed):
     // candidates are in index order within each tensor, so a stable sort of the tensor and
     // magnitude bits alone yields (tensor, |t'| descending, index ascending)
@@ -830,8 +1541,8 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     else
       hipLaunchKernelGGL((topk_prep_hist<2>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
     hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, nullptr, bin);
-    hipLaunchKernelGGL((topk_collect<false>), grid, blk, 0, st, tp, scale, items, d_begins, bin, nullptr, cnt, item_cnt,
-                       cand);
+    hipLaunchKernelGGL((topk_collect<false>), grid, blk, 0, st, tp, scale, items, d_begins, bin, nullptr, cnt, sub_cnt,
+                       item_cnt, cand);
     hipLaunchKernelGGL(topk_segments, dim3(((unsigned)nt + kThreads - 1) / kThreads), blk, 0, st, nt, d_begins, cnt,
                        seg_b, seg_e);
     OMF_HIP(hipGetLastError());

@@ -1,4 +1,5 @@
-"""Top-K encode on the Llama-400M arena (k = 1 %), for rocprofv3 --stats (experiment)."""
+"""Top-K encode on the Llama-400M arena (k = 1 %), for rocprofv3 (experiment).  Error-feedback
+calls take a fresh gradient each call (t' = residual + x_i), as in training."""
 import sys
 import time
 
@@ -10,13 +11,14 @@ from omnifed_amd import codec, shapes  # noqa: E402
 dev = torch.device("cuda", 0)
 sizes = [shapes.numel(s) for _, s in shapes.model_shapes(sys.argv[1] if len(sys.argv) > 1 else "llama400m")]
 p = codec.Plan.get(sizes, device=dev)
-x = torch.randn(p.arena_end, device=dev) * 1e-3
+g = torch.Generator(device=dev).manual_seed(0)
+xs = [torch.randn(p.arena_end, device=dev, generator=g) * 1e-3 for _ in range(6)]
 res = torch.zeros(p.arena_end, device=dev)
-p.topk_encode(x, 0.01, residual=res, residual_mode=2)
+p.topk_encode(xs[0], 0.01, residual=res, residual_mode=2)
 torch.cuda.synchronize()
 for mode in (1, 0):
     t0 = time.perf_counter()
-    for _ in range(5):
-        p.topk_encode(x, 0.01, residual=res if mode else None, residual_mode=mode)
+    for i in range(5):
+        p.topk_encode(xs[1 + i], 0.01, residual=res if mode else None, residual_mode=mode)
     torch.cuda.synchronize()
-    print(f"topk mode {mode}: {(time.perf_counter() - t0) / 5 * 1e3:.3f} ms")
+    print(f"topk mode {mode}: {(time.perf_counter() - t0) / 5 * 1e3:.3f} ms", flush=True)

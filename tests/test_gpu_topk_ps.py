@@ -261,3 +261,63 @@ def test_encode_updates_dict_mt_matches_reference_when_norm_agrees(gpu, golden, 
             assert L.values_data == q.numpy().tobytes(), name
             if L.meta_tensor == G.meta_tensor:
                 assert L.SerializeToString() == G.SerializeToString(), name
+
+
+def _encode_both_paths(plan, x, ratio, residual0=None, mode=0, alpha=1.0):
+    """Top-K encode through the bucket-sort fast path and through the device-wide radix-sort
+    fallback (OMF_TOPK_FALLBACK=1, read per call by the library) on the same input."""
+    import os
+    outs = []
+    for fb in ("0", "1"):
+        res = residual0.clone() if residual0 is not None else None
+        os.environ["OMF_TOPK_FALLBACK"] = fb
+        try:
+            v, i, ks = plan.topk_encode(x, ratio, residual=res, residual_mode=mode, alpha=alpha)
+            torch.cuda.synchronize()
+        finally:
+            os.environ.pop("OMF_TOPK_FALLBACK", None)
+        outs.append((v, i, res))
+    return outs, ks
+
+
+@pytest.mark.parametrize("ratio", [0.01, 0.1])
+def test_topk_fast_path_equals_fallback_sort(gpu, ratio):
+    """The bucket sort (fine-bin histogram, per-bucket LDS counting sort) and the device-wide
+    radix sort give the same bytes: values, indices and the error-feedback residual."""
+    sizes = [3 << 20, 1000, 1_000_003, 70000, 5 << 20]
+    plan = codec.Plan(sizes, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(11)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g)
+    x[plan.offsets[4]:plan.offsets[4] + sizes[4]] *= torch.rand(sizes[4], device=gpu, generator=g) ** 4  # heavy tail
+    r0 = torch.randn(plan.arena_end, device=gpu, generator=g) * 0.1
+    (a, b), ks = _encode_both_paths(plan, x, ratio, residual0=r0, mode=1, alpha=2.0)
+    assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0])
+    assert torch.equal(a[2], b[2])
+    K = 0
+    for t, (o, n) in enumerate(zip(plan.offsets, sizes)):
+        tp = r0[o:o + n] + x[o:o + n] * 2.0
+        want, _ = torch.topk(tp.abs(), ks[t], sorted=True)
+        assert torch.equal(a[0][K:K + ks[t]].abs(), want), t
+        K += ks[t]
+
+
+def test_topk_clustered_magnitudes_bucket_merge(gpu):
+    """Magnitudes repeated in runs of 50 (a sub-bin holds more keys than the counting sort's
+    insertion limit, so those buckets are merge sorted): torch.topk's magnitudes, descending,
+    ties by ascending index, and the same bytes as the fallback sort."""
+    n = 1 << 20
+    g = torch.Generator().manual_seed(3)
+    levels = torch.rand(n // 50 + 1, generator=g) + 0.5
+    xh = levels.repeat_interleave(50)[:n]
+    xh = xh[torch.randperm(n, generator=g)] * torch.where(torch.rand(n, generator=g) < 0.5, -1.0, 1.0)
+    plan = codec.Plan([n], device=gpu)
+    (a, b), ks = _encode_both_paths(plan, xh.to(gpu), 0.01)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
+    k = ks[0]
+    vh, ih = a[0].cpu(), a[1].cpu()
+    want, _ = torch.topk(xh.abs(), k, sorted=True)
+    assert torch.equal(vh.abs(), want)
+    m = vh.abs()
+    same = m[:-1] == m[1:]
+    assert bool(torch.all(ih[:-1][same] < ih[1:][same]))
+    assert torch.equal(vh, xh[ih])
