@@ -103,7 +103,7 @@ class Plan:
         self._lock = threading.Lock()
         self._topk_ws: Dict[int, torch.Tensor] = {}  # per stream: launches on two streams never share one
         # the library's default (omf_qsgd.hip), unless an experiment overrides it
-        self.strategy = {"0": "resident", "1": "ordered"}.get(os.environ.get("OMF_ENCODE_STRATEGY", ""), "ring")
+        self.strategy = {"0": "resident", "2": "ring"}.get(os.environ.get("OMF_ENCODE_STRATEGY", ""), "ordered")
 
     @classmethod
     def get(cls, sizes, offsets=None, device=None, chunk: int = 0) -> "Plan":

@@ -81,15 +81,21 @@ struct DecArgs {
   const Item* items;
   float levels;      // fl32(levels)
   float inv_levels;  // 2^-s when levels is a power of two (exact), else unused
+  int ntl;           // nontemporal payload / accumulator loads
 };
 
-template <int V, bool FULL>
+template <int V, bool FULL, bool NT = false>
 __device__ __forceinline__ void load_f4(const float* __restrict__ p, int64_t b, int64_t end, float4 (&v)[V]) {
 #pragma unroll
   for (int k = 0; k < V; ++k) {
     const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
     if (FULL || e + 4 <= end) {
-      v[k] = *reinterpret_cast<const float4*>(p + e);
+      if (NT) {  // a last read (the second pass of a two-pass tensor)
+        const f32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p + e));
+        v[k] = make_float4(t[0], t[1], t[2], t[3]);
+      } else {
+        v[k] = *reinterpret_cast<const float4*>(p + e);
+      }
     } else {
       float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
       if (e < end) t.x = p[e];
@@ -208,16 +214,16 @@ __device__ __forceinline__ void quant_store(const float4 (&v)[V], const EncArgs&
 }
 
 // Load + scale + quantise + store one sub-chunk [b, e) of V rows (V * 1024 elements).
-template <int WIDTH, bool HAS_U, int V = kV>
+template <int WIDTH, bool HAS_U, int V = kV, bool NT = false>
 __device__ __forceinline__ void quant_sub(const EncArgs& a, int64_t b, int64_t e, int64_t tbegin, int32_t tensor,
                                           float norm) {
   float4 v[V];
   if (e - b == (int64_t)V * 1024) {
-    load_f4<V, true>(a.x, b, e, v);
+    load_f4<V, true, NT>(a.x, b, e, v);
     scale_f4<V>(v, a);
     quant_store<WIDTH, HAS_U, true, V>(v, a, b, e, tbegin, tensor, norm);
   } else {
-    load_f4<V, false>(a.x, b, e, v);
+    load_f4<V, false, NT>(a.x, b, e, v);
     scale_f4<V>(v, a);
     quant_store<WIDTH, HAS_U, false, V>(v, a, b, e, tbegin, tensor, norm);
   }
@@ -378,8 +384,9 @@ __device__ __forceinline__ void decode_sub(const DecArgs& a, int64_t b, int64_t 
     const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
     if (WIDTH == 1) {
       const int8_t* q8 = reinterpret_cast<const int8_t*>(a.q);
-      if (FULL || e + 4 <= end) {
-        raw[k][0] = *reinterpret_cast<const int32_t*>(q8 + e);
+      if (FULL || e + 4 <= end) {  // streamed once
+        const int32_t* pq = reinterpret_cast<const int32_t*>(q8 + e);
+        raw[k][0] = a.ntl ? __builtin_nontemporal_load(pq) : *pq;
       } else {
         uint32_t t = 0;
         if (e < end) t |= (uint32_t)(uint8_t)q8[e];
@@ -390,8 +397,8 @@ __device__ __forceinline__ void decode_sub(const DecArgs& a, int64_t b, int64_t 
     } else {
       const int32_t* q32 = reinterpret_cast<const int32_t*>(a.q);
       if (FULL || e + 4 <= end) {
-        const int4 t = *reinterpret_cast<const int4*>(q32 + e);
-        raw[k][0] = t.x; raw[k][1] = t.y; raw[k][2] = t.z; raw[k][3] = t.w;
+        const i32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(q32 + e));
+        raw[k][0] = t[0]; raw[k][1] = t[1]; raw[k][2] = t[2]; raw[k][3] = t[3];
       } else {
         raw[k][0] = (e < end) ? q32[e] : 0;
         raw[k][1] = (e + 1 < end) ? q32[e + 1] : 0;
@@ -424,7 +431,8 @@ __device__ __forceinline__ void decode_sub(const DecArgs& a, int64_t b, int64_t 
     if (FULL || e + 4 <= end) {
       float4 o = make_float4(yv[0], yv[1], yv[2], yv[3]);
       if (ACC) {
-        const float4 prev = *reinterpret_cast<const float4*>(y);
+        const f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(y));
+        const float4 prev = make_float4(pv[0], pv[1], pv[2], pv[3]);
         o.x = __fadd_rn(prev.x, o.x); o.y = __fadd_rn(prev.y, o.y);
         o.z = __fadd_rn(prev.z, o.z); o.w = __fadd_rn(prev.w, o.w);
       }
@@ -472,7 +480,7 @@ struct omf_plan {
   std::vector<int64_t> sizes, offsets;
   int64_t arena_end = 0;
   int64_t cap = 0;               // tensors of <= cap items take the register-resident path
-  int32_t strategy = 2;          // 0 register-resident + two-pass, 1 two-pass only, 2 single-read ring (default)
+  int32_t strategy = 1;          // 0 register-resident + two-pass, 1 ticket-ordered two-pass (default), 2 single-read ring
   uint64_t wait_ticks = kWaitTicks;
   uint32_t epoch = 0;            // last granule tag used (host-side launch counter)
   int32_t ev = 16;               // encode rows per thread (sub-chunk = ev * 1024 elements)
@@ -1011,7 +1019,8 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }
-  if (p->strategy == 2 && !norm_only) {
+  // The ring also serves the fused PS step (divide + encode in one launch) under any strategy.
+  if ((p->strategy == 2 || divisor != 0.0f) && !norm_only) {
     omf::ring::Args r;
     r.x = x; r.u = u; r.q = q; r.norm_out = norm_out;
     r.items = p->d_ring; r.tinfo = p->d_ring_t; r.gran = p->d_ring_gran;
@@ -1097,10 +1106,10 @@ int omf_ps_apply_encode(omf_plan* p, const float* acc, float divisor, float* avg
   // The fused launch reads acc while it writes avg (second-pass chunks of large tensors
   // re-read acc, the bounded-wait fallback recomputes partials from it), so it needs
   // avg_out disjoint from acc; in place it runs as divide + encode.
-  if (p->strategy == 2 && !alias)  // one launch: read acc once, write avg and the payload
+  if (!alias)  // one ring launch: read acc once, write avg and the payload
     return encode_impl(p, acc, 1.0f, bit_width, u, seed, offset, nullptr, q_out, norm_out, false, stream, divisor,
                        avg_out);
-  // other strategies: the same results in two passes
+  // in place: the same results as divide, then encode
   DeviceGuard g(p->device);
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   if (avg_out != acc)
@@ -1128,6 +1137,10 @@ int omf_qsgd_decode(omf_plan* p, const void* q, int32_t width, int32_t levels, c
   a.levels = (float)levels;
   const bool pow2 = (levels & (levels - 1)) == 0;
   a.inv_levels = pow2 ? 1.0f / (float)levels : 0.0f;  // exact for a power of two
+  {
+    const char* e = std::getenv("OMF_DEC_NTL");  // experiments: 0 = default-policy payload loads
+    a.ntl = e && e[0] == '0' ? 0 : 1;
+  }
   const dim3 grid((unsigned)p->n_flat), blk(kThreads);
   hipStream_t st = (hipStream_t)stream;
 #define OMF_DEC(W, A, P) hipLaunchKernelGGL((qsgd_decode_flat<W, A, P>), grid, blk, 0, st, a)

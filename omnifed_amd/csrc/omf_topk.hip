@@ -334,6 +334,21 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
 
 // Fine bin of a candidate magnitude (monotone in mag; below / above the mapped range clamp
 // to the lowest / highest fine bin).
+// fine_bin plus the key's position inside its fine bin: the low `wbits` bits of |t'| (0 bits
+// for the clamped bottom / top bins).
+__device__ __forceinline__ uint32_t fine_bin_pos(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t,
+                                                 uint32_t F, uint32_t& low, uint32_t& wbits) {
+  const int c = (int)(mag >> kSShift) - (int)lo;
+  low = 0;
+  wbits = 0;
+  if (c < 0) return 0u;
+  if (c >= kCoarse) return F - 1u;
+  const uint32_t m = map_t[c], r = m >> 16;
+  wbits = kSShift - r;
+  low = mag & ((1u << wbits) - 1u);
+  return (m & 0xffffu) + ((mag >> wbits) & ((1u << r) - 1u));
+}
+
 __device__ __forceinline__ uint32_t fine_bin(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t,
                                              uint32_t F) {
   const int c = (int)(mag >> kSShift) - (int)lo;
@@ -445,9 +460,13 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
   uint32_t selm = 0;
   const bool full = o + 4 <= lim;
   if (full) {
-    const float4 xv = *reinterpret_cast<const float4*>(x + b + o);
+    const f32x4_t xl = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(x + b + o));  // read once
+    const float4 xv = make_float4(xl[0], xl[1], xl[2], xl[3]);
     float4 rv = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (MODE == 1) rv = *reinterpret_cast<const float4*>(r + b + o);
+    if (MODE == 1) {
+      const f32x4_t rl = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(r + b + o));
+      rv = make_float4(rl[0], rl[1], rl[2], rl[3]);
+    }
     vv[0] = tprime<MODE>(xv.x, rv.x, alpha);
     vv[1] = tprime<MODE>(xv.y, rv.y, alpha);
     vv[2] = tprime<MODE>(xv.z, rv.z, alpha);
@@ -463,7 +482,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
     float rr[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) rr[c] = ((selm >> c) & 1u) ? __fsub_rn(vv[c], vv[c]) : vv[c];
-    if (full) *reinterpret_cast<float4*>(r + b + o) = make_float4(rr[0], rr[1], rr[2], rr[3]);
+    if (full) store_nt(r + b + o, make_float4(rr[0], rr[1], rr[2], rr[3]));
     else
       for (uint32_t c = 0; c < 4 && o + c < lim; ++c) r[b + o + c] = rr[c];
   }
@@ -886,7 +905,7 @@ __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk
                                                   uint32_t* __restrict__ bstart, BucketRec* __restrict__ brec,
                                                   uint32_t* __restrict__ bfill, const int64_t* __restrict__ kb2,
                                                   uint32_t* __restrict__ flag, uint32_t* __restrict__ status,
-                                                  int dbg) {
+                                                  uint32_t* __restrict__ fse, int dbg) {
   constexpr int PER = kFineMax / 1024;
   __shared__ uint32_t s_bs[kPlanMaxBuckets];
   __shared__ uint32_t part[1024];
@@ -938,7 +957,10 @@ __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk
         s_nb = (uint32_t)bucket + 1u;
       }
     }
-    if (i < F) fb[i] = bucket;
+    if (i < F) {
+      fb[i] = bucket;
+      if (bucket >= 0) fse[(size_t)t * kFineMax + i] = (uint32_t)se;
+    }
     se += h[j];
   }
   __syncthreads();
@@ -1051,7 +1073,12 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
                                                              const int64_t* __restrict__ tsize, float* __restrict__ r,
                                                              float* __restrict__ values,
                                                              int64_t* __restrict__ indices,
-                                                             const uint32_t* __restrict__ status, int dbg) {
+                                                             const uint32_t* __restrict__ status,
+                                                             const uint32_t* __restrict__ fmap,
+                                                             const uint32_t* __restrict__ tlo,
+                                                             const uint32_t* __restrict__ fcount,
+                                                             const uint32_t* __restrict__ fhist,
+                                                             const uint32_t* __restrict__ fse, int dbg) {
   __shared__ union {
     typename BucketSort::storage_type sort;
     uint64_t xch[kSubBins];
@@ -1061,7 +1088,7 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
     } cs;
   } s_u;
   __shared__ uint32_t s_part[kBT];
-  __shared__ uint32_t s_min, s_max, s_cmax;
+  __shared__ uint32_t s_cmax;
   const BucketRec rec = brec[blockIdx.x];
   const uint32_t cnt = rec.count_tensor & 0xffffu;
   if (cnt == 0 || (status[1] | status[2])) return;  // block-uniform (a fallback verdict: nothing to do)
@@ -1069,43 +1096,40 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
   const uint32_t st = rec.start;
   const uint64_t* src = bkeys + rec.key_off;
   const int64_t k = kk[t], o = koff[t], base = tbegin[t], n = tsize[t];  // issued with the key loads
-  if (threadIdx.x == 0) {
-    s_min = 0xffffffffu;
-    s_max = 0;
-    s_cmax = 0;
-  }
+  const uint32_t lo = tlo[t], F = fcount[t];
+  const uint32_t* map_t = fmap + (size_t)t * kCoarse;
+  const uint32_t* h_t = fhist + (size_t)t * kFineMax;
+  const uint32_t* se_t = fse + (size_t)t * kFineMax;
+  if (threadIdx.x == 0) s_cmax = 0;
+  // Sub-bin of a key = its rank slot if keys were spread evenly inside their fine bin: the fine
+  // bin's first rank in the bucket (se - start) plus (c - 1 - low * c / 2^wbits) for a bin of
+  // c keys, descending |t'|.  Sub-bins = the bucket's key count, about one key each.
   uint64_t keys[kBI];
-  uint32_t lmin = 0xffffffffu, lmax = 0;
+  uint32_t sub[kBI];
 #pragma unroll
   for (int j = 0; j < kBI; ++j) {  // striped loads
     const uint32_t e = threadIdx.x + (uint32_t)j * kBT;
     uint64_t sk = ~0ull;
+    sub[j] = 0xffffffffu;
     if (e < cnt) {
       const uint64_t key = src[e];
-      const uint32_t bits = (uint32_t)key, inv = 0x7fffffffu - (bits & 0x7fffffffu);
-      sk = ((uint64_t)inv << 33) | ((key >> 32) << 1) | (uint64_t)(bits >> 31);
-      lmin = min(lmin, inv);
-      lmax = max(lmax, inv);
+      const uint32_t bits = (uint32_t)key, mag = bits & 0x7fffffffu;
+      sk = ((uint64_t)(0x7fffffffu - mag) << 33) | ((key >> 32) << 1) | (uint64_t)(bits >> 31);
+      uint32_t low, wbits;
+      const uint32_t fb = fine_bin_pos(mag, lo, map_t, F, low, wbits);
+      const uint32_t cb = h_t[fb], rel = se_t[fb] - st;
+      const uint32_t in = cb - 1u - (uint32_t)(((uint64_t)low * cb) >> wbits);
+      sub[j] = min(rel + in, cnt - 1u);
     }
     keys[j] = sk;
   }
   for (int i = threadIdx.x; i < kSubBins; i += kBT) s_u.cs.start[i] = 0;
   __syncthreads();
-  if (lmin <= lmax) {
-    atomicMin(&s_min, lmin);
-    atomicMax(&s_max, lmax);
-  }
-  __syncthreads();
-  const uint32_t imin = s_min;
-  const uint64_t span = (uint64_t)(s_max - imin) + 1;
   uint32_t meta[kBI];  // sub-bin << 16 | slot in it
 #pragma unroll
   for (int j = 0; j < kBI; ++j) {
     meta[j] = 0xffffffffu;
-    if (threadIdx.x + (uint32_t)j * kBT < cnt) {
-      const uint32_t sub = (uint32_t)((((keys[j] >> 33) - imin) * (uint64_t)kSubBins) / span);
-      meta[j] = (sub << 16) | atomicAdd(&s_u.cs.start[sub], 1u);
-    }
+    if (sub[j] != 0xffffffffu) meta[j] = (sub[j] << 16) | atomicAdd(&s_u.cs.start[sub[j]], 1u);
   }
   __syncthreads();
   uint32_t c[kBI], loc = 0, cmx = 0;  // this thread's sub-bins kBI tid ..
@@ -1220,14 +1244,37 @@ __global__ __launch_bounds__(kThreads) void topk_scatter_arena(const float* __re
                                                                double ratio, int64_t ktot, float* __restrict__ y,
                                                                int add) {
   __shared__ int64_t koff[kArenaMaxTensors + 1];
-  if (threadIdx.x == 0) {  // k_t exactly as omf_topk_k, prefix-summed (nt is small)
-    int64_t acc = 0;
-    for (int t = 0; t < nt; ++t) {
-      koff[t] = acc;
-      const int64_t k = (int64_t)((double)sizes[t] * ratio);
-      acc += k < 1 ? 1 : k;
+  __shared__ int64_t s_part[kThreads];
+  {  // k_t exactly as omf_topk_k, prefix-summed by the whole block (16 tensors per thread)
+    constexpr int PER = kArenaMaxTensors / kThreads;
+    int64_t kv[PER], loc = 0;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int t = threadIdx.x * PER + j;
+      int64_t k = 0;
+      if (t < nt) {
+        k = (int64_t)((double)sizes[t] * ratio);
+        if (k < 1) k = 1;
+      }
+      kv[j] = k;
+      loc += k;
     }
-    koff[nt] = acc;
+    s_part[threadIdx.x] = loc;
+    __syncthreads();
+    for (int o = 1; o < kThreads; o <<= 1) {  // inclusive scan (once per block)
+      const int64_t add = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0;
+      __syncthreads();
+      s_part[threadIdx.x] += add;
+      __syncthreads();
+    }
+    int64_t run = s_part[threadIdx.x] - loc;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int t = threadIdx.x * PER + j;
+      if (t <= nt) koff[t] = run;
+      run += kv[j];
+    }
+    if (threadIdx.x == kThreads - 1) koff[nt] = s_part[kThreads - 1];
   }
   __syncthreads();
   for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < ktot; j += (int64_t)gridDim.x * kThreads) {
@@ -1323,7 +1370,7 @@ size_t sort_tmp_bytes(const omf_plan* p) {
 struct WsLayout {
   size_t hist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
       sub_cnt, item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes, bbase, kb2, fmap, tlo, fcount, fhist,
-      fbucket, bstart, brec, bfill, nb_max, sbase;
+      fbucket, fse, bstart, brec, bfill, nb_max, sbase;
 };
 
 // Bucket-table slots for any ratio (k <= n).
@@ -1368,6 +1415,7 @@ WsLayout layout(const omf_plan* p) {
   L.fcount = o; o = align256(o + 4 * (size_t)nt);
   L.fhist = o; o = align256(o + 4 * (size_t)nt * kFineMax);
   L.fbucket = o; o = align256(o + 4 * (size_t)nt * kFineMax);
+  L.fse = o; o = align256(o + 4 * (size_t)nt * kFineMax);
   L.nb_max = bucket_slots_max(p);
   L.bstart = o; o = align256(o + 4 * L.nb_max);
   L.brec = o; o = align256(o + sizeof(BucketRec) * L.nb_max);
@@ -1447,6 +1495,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   uint32_t* fcount = reinterpret_cast<uint32_t*>(w + L.fcount);
   uint32_t* fhist = reinterpret_cast<uint32_t*>(w + L.fhist);
   int32_t* fbucket = reinterpret_cast<int32_t*>(w + L.fbucket);
+  uint32_t* fse = reinterpret_cast<uint32_t*>(w + L.fse);
   uint32_t* bstart = reinterpret_cast<uint32_t*>(w + L.bstart);
   BucketRec* brec = reinterpret_cast<BucketRec*>(w + L.brec);
   uint32_t* bfill = reinterpret_cast<uint32_t*>(w + L.bfill);
@@ -1486,7 +1535,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast, fmap,
                        tlo, fcount, fhist);
     hipLaunchKernelGGL(topk_plan, sgrid, sblk, 0, st, kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2,
-                       flag, status, dbg_bits());
+                       flag, status, fse, dbg_bits());
     OMF_HIP(hipGetLastError());
     // The plan's verdict goes to pinned host memory behind an event; the bucket kernels are
     // enqueued before the host waits for it (they do nothing when the verdict is a fallback),
@@ -1500,7 +1549,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast,
                          fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins, rz, sorted, status);
       hipLaunchKernelGGL(topk_bucket_sort, dim3((unsigned)nbuckets), dim3(kBT), 0, st, sorted, brec, kk, koff, d_begins,
-                         d_sizes, rz, values, indices, status, dbg_bits());
+                         d_sizes, rz, values, indices, status, fmap, tlo, fcount, fhist, fse, dbg_bits());
       OMF_HIP(hipGetLastError());
     }
     OMF_HIP(hipEventSynchronize(hsync->ev));

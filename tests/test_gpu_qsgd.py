@@ -122,7 +122,7 @@ def test_gpu_norm_accuracy_and_single_launch_parity(gpu, strategy):
             assert torch.equal(n2, norms)
         else:
             torch.testing.assert_close(n2, norms, rtol=2e-6, atol=0)
-        plan.set_encode_strategy("ring")  # restore the default on the cached plan
+        plan.set_encode_strategy("ordered")  # restore the default on the cached plan
 
 
 def test_strategies_agree_and_fallback_exact(gpu):
@@ -145,6 +145,7 @@ def test_strategies_agree_and_fallback_exact(gpu):
     q3, n3 = plan.qsgd_encode(x, 4, seed=3, offset=1)
     assert plan.check()
     torch.testing.assert_close(n3, n2, rtol=2e-6, atol=0)
+    plan.set_encode_strategy("ordered")  # the default, on the cached plan
     for strategy in ("ring", "resident", "ordered"):
         small = codec.Plan([40000] * 8 + [1 << 20], device=gpu)
         small.set_encode_strategy(strategy)

@@ -73,6 +73,7 @@ def test_ring_debug_timing_modes_complete(gpu, dbg, monkeypatch):
     assert ref.check()
     monkeypatch.setenv("OMF_RING_DBG", str(dbg))
     p = codec.Plan(sizes, device=gpu)  # the debug switch is read at plan creation
+    p.set_encode_strategy("ring")
     for hold in (0, 3):
         p.set_ring(hold_max=hold)
         _, nd = p.qsgd_encode(x, 4, seed=1)
@@ -81,11 +82,13 @@ def test_ring_debug_timing_modes_complete(gpu, dbg, monkeypatch):
             assert torch.equal(nd, n_ref) if hold == 0 else torch.allclose(nd, n_ref, rtol=2e-6, atol=0)
 
 
-def test_encodes_on_two_streams_are_ordered(gpu):
+@pytest.mark.parametrize("strategy", ["ordered", "ring"])
+def test_encodes_on_two_streams_are_ordered(gpu, strategy):
     """One plan, launches alternating between two streams with no host synchronisation: each
     result equals the sequential one (the plan orders a launch after the previous stream's)."""
     sizes = [5000, 1 << 20, 70001, 3 << 20]
     plan = codec.Plan(sizes, device=gpu)
+    plan.set_encode_strategy(strategy)
     g = torch.Generator(device=gpu).manual_seed(8)
     xs = [torch.randn(plan.arena_end, device=gpu, generator=g) for _ in range(4)]
     want = []
@@ -132,7 +135,7 @@ def test_int8_payload_stays_inside_its_buffer(gpu):
         o = plan.offsets[2]
         want, *_ = oracle.qsgd_quantize(x[o:o + sizes[2]].cpu(), 4, norm=float(norms[2]), u=torch.from_numpy(ref))
         assert q[o:o + sizes[2]].cpu().numpy().tobytes() == want.numpy().tobytes()
-    plan.set_encode_strategy("ring")
+    plan.set_encode_strategy("ordered")
 
 
 # ---------------------------------------------------------------- bf16 / fp16 (golden_r2 half/*)
