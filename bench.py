@@ -219,14 +219,18 @@ def pmc_traffic(kernel, config, bits):
 
 
 def event_ms(torch, st, fn, reps):
-    """Mean duration of ``fn`` (its launches on stream ``st``) from HIP events recorded on ``st``."""
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    """Mean duration of ``fn`` (its launches on stream ``st``) in a back-to-back loop, from two
+    HIP events recorded on ``st`` around ``reps`` calls (the steady-state launch duration;
+    per-call event pairs would also count the host's part of a call that waits mid-way, as
+    the Top-K encoder does for its verdict)."""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn(0)  # one untimed call: the loop starts in steady state
+    a.record(st)
     for i in range(reps):
-        ev[i][0].record(st)
         fn(i)
-        ev[i][1].record(st)
+    b.record(st)
     torch.cuda.synchronize()
-    return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    return float(a.elapsed_time(b)) / reps
 
 
 def main():

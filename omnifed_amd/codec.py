@@ -102,6 +102,7 @@ class Plan:
         self._h = h
         self._lock = threading.Lock()
         self._topk_ws: Dict[int, torch.Tensor] = {}  # per stream: launches on two streams never share one
+        self._topk_cache: Dict[float, tuple] = {}
         # the library's default (omf_qsgd.hip), unless an experiment overrides it
         self.strategy = {"0": "resident", "2": "ring"}.get(os.environ.get("OMF_ENCODE_STRATEGY", ""), "ordered")
 
@@ -339,8 +340,22 @@ class Plan:
 
     # ------------------------------------------------------------ Top-K
     def topk_ks(self, ratio: float) -> List[int]:
-        L = lib()
-        return [int(L.omf_topk_k(n, float(ratio))) for n in self.sizes]
+        return list(self._topk_geom(ratio)[0])
+
+    def _topk_geom(self, ratio: float):
+        """(ks, K, workspace bytes) of one ratio, cached: the per-call host path stays short
+        (the library's sizing runs once per ratio, not once per tensor per call)."""
+        key = float(ratio)
+        g = self._topk_cache.get(key)
+        if g is None:
+            L = lib()
+            ks = tuple(int(L.omf_topk_k(n, key)) for n in self.sizes)
+            for n, k in zip(self.sizes, ks):
+                if k > n:
+                    raise ValueError("selected index k out of range: compress_ratio too large")
+            g = (ks, sum(ks), int(L.omf_topk_workspace_bytes(self._h, key)))
+            self._topk_cache[key] = g
+        return g
 
     def topk_encode(self, x: torch.Tensor, ratio: float, residual: Optional[torch.Tensor] = None,
                     residual_mode: int = 0, values: Optional[torch.Tensor] = None,
@@ -349,11 +364,8 @@ class Plan:
 
         ``alpha``: the client weighting (t' = residual + fl32(alpha * x)), fused in."""
         dev = self.device
-        ks = self.topk_ks(ratio)
-        for n, k in zip(self.sizes, ks):
-            if k > n:
-                raise ValueError("selected index k out of range: compress_ratio too large")
-        K = sum(ks)
+        ks, K, need = self._topk_geom(ratio)
+        ks = list(ks)
         _need(x, "x", torch.float32, dev, self.arena_end, 16)
         if residual_mode not in (0, 1, 2):
             raise ValueError("residual_mode must be 0, 1 or 2")
@@ -368,7 +380,6 @@ class Plan:
         _need(values, "values", torch.float32, dev, K, 4)
         _need(indices, "indices", torch.int64, dev, K, 8)
         L = lib()
-        need = int(L.omf_topk_workspace_bytes(self._h, float(ratio)))
         st = stream if stream is not None else _stream(dev)
         with self._lock:
             ws = self._topk_ws.get(st)
@@ -387,7 +398,7 @@ class Plan:
         """Decode one client's whole Top-K selection (topk_encode's packed layout at ``ratio``)
         into the arena ``y``: mode 0 zeros + set, 1 overlay, 2 scatter-add (one launch)."""
         dev = self.device
-        K = sum(self.topk_ks(ratio))
+        K = self._topk_geom(ratio)[1]
         _need(values, "values", torch.float32, dev, K, 4)
         _need(indices, "indices", torch.int64, dev, K, 8)
         if mode not in (0, 1, 2):

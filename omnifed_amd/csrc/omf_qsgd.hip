@@ -81,7 +81,6 @@ struct DecArgs {
   const Item* items;
   float levels;      // fl32(levels)
   float inv_levels;  // 2^-s when levels is a power of two (exact), else unused
-  int ntl;           // nontemporal payload / accumulator loads
 };
 
 template <int V, bool FULL, bool NT = false>
@@ -376,17 +375,16 @@ __global__ __launch_bounds__(kThreads) void qsgd_quant_flat(EncArgs a) {
 }
 
 // Decode one sub-chunk [b, end): y = fl32(fl32(norm * q) / L) (optionally acc += y).
-template <int WIDTH, bool ACC, bool POW2, bool FULL>
+template <int WIDTH, bool ACC, bool POW2, bool FULL, int V = kV>
 __device__ __forceinline__ void decode_sub(const DecArgs& a, int64_t b, int64_t end, float norm) {
-  int32_t raw[kV][WIDTH == 1 ? 1 : 4];
+  int32_t raw[V][WIDTH == 1 ? 1 : 4];
 #pragma unroll
-  for (int k = 0; k < kV; ++k) {
+  for (int k = 0; k < V; ++k) {
     const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
     if (WIDTH == 1) {
       const int8_t* q8 = reinterpret_cast<const int8_t*>(a.q);
-      if (FULL || e + 4 <= end) {  // streamed once
-        const int32_t* pq = reinterpret_cast<const int32_t*>(q8 + e);
-        raw[k][0] = a.ntl ? __builtin_nontemporal_load(pq) : *pq;
+      if (FULL || e + 4 <= end) {  // streamed once: nontemporal
+        raw[k][0] = __builtin_nontemporal_load(reinterpret_cast<const int32_t*>(q8 + e));
       } else {
         uint32_t t = 0;
         if (e < end) t |= (uint32_t)(uint8_t)q8[e];
@@ -408,7 +406,7 @@ __device__ __forceinline__ void decode_sub(const DecArgs& a, int64_t b, int64_t 
     }
   }
 #pragma unroll
-  for (int k = 0; k < kV; ++k) {
+  for (int k = 0; k < V; ++k) {
     const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
     if (!FULL && e >= end) continue;
     int32_t qi[4];
@@ -1137,10 +1135,6 @@ int omf_qsgd_decode(omf_plan* p, const void* q, int32_t width, int32_t levels, c
   a.levels = (float)levels;
   const bool pow2 = (levels & (levels - 1)) == 0;
   a.inv_levels = pow2 ? 1.0f / (float)levels : 0.0f;  // exact for a power of two
-  {
-    const char* e = std::getenv("OMF_DEC_NTL");  // experiments: 0 = default-policy payload loads
-    a.ntl = e && e[0] == '0' ? 0 : 1;
-  }
   const dim3 grid((unsigned)p->n_flat), blk(kThreads);
   hipStream_t st = (hipStream_t)stream;
 #define OMF_DEC(W, A, P) hipLaunchKernelGGL((qsgd_decode_flat<W, A, P>), grid, blk, 0, st, a)

@@ -37,6 +37,7 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 #include "../../include/omf_codec.h"
@@ -139,10 +140,11 @@ __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict
                                                        int64_t* __restrict__ kk, int64_t* __restrict__ koff,
                                                        uint32_t* __restrict__ tfirst, uint32_t* __restrict__ tlast,
                                                        uint32_t* __restrict__ bbase, int64_t* __restrict__ kb2,
-                                                       uint32_t* __restrict__ sbase, uint32_t* __restrict__ status) {
+                                                       uint32_t* __restrict__ sbase, uint32_t* __restrict__ status,
+                                                       uint32_t seq) {
   __shared__ int64_t s_k[kThreads], s_i[kThreads], s_b[kThreads];
   __shared__ uint32_t s_s[kThreads];
-  if (threadIdx.x < 4) status[threadIdx.x] = 0;
+  if (threadIdx.x < 4) status[threadIdx.x] = threadIdx.x == 3 ? seq : 0u;  // [3]: this call's sequence number
   int64_t carry_k = 0, carry_i = 0, carry_b = 0;
   uint32_t carry_s = 0;
   for (int32_t t0 = 0; t0 < nt; t0 += kThreads) {
@@ -214,6 +216,7 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
                                                               uint32_t* __restrict__ tbin,
                                                               uint32_t* __restrict__ hist,
                                                               uint32_t* __restrict__ item_cnt,
+                                                              uint32_t* __restrict__ thi,
                                                               uint32_t* __restrict__ fmap, uint32_t* __restrict__ tlo,
                                                               uint32_t* __restrict__ fcount,
                                                               uint32_t* __restrict__ fhist) {
@@ -269,9 +272,10 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
   }();
   const double m = (double)kk[t] * (double)S / (double)max(n, (int64_t)1);
   const double want = m + 6.0 * sqrt(m) + 32.0;
-  __shared__ uint32_t s_thr, s_min, s_max;
+  __shared__ uint32_t s_thr, s_hi, s_min, s_max;
   if (threadIdx.x == 0) {
     s_thr = 0;
+    s_hi = kSBins;
     s_min = kSBins;
     s_max = 0;
   }
@@ -282,6 +286,17 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
     for (int j = PER - 1; j >= 0; --j) {
       if (above < target && above + c[j] >= target) s_thr = PER * threadIdx.x + j;  // exactly one match
       above += c[j];
+    }
+    // The "sure" bin: every bin from it up holds, with ~6 sigma of margin, fewer than k
+    // elements in total, so its elements are selected (the fused pass zeroes their residual).
+    const double sure = m - 6.0 * sqrt(m) - 32.0;
+    if (sure >= 1.0) {
+      const uint32_t ts = (uint32_t)sure;
+      above = above0;
+      for (int j = PER - 1; j >= 0; --j) {
+        if (above <= ts && above + c[j] > ts) s_hi = PER * threadIdx.x + j + 1;  // exactly one crossing
+        above += c[j];
+      }
     }
   }
 #pragma unroll
@@ -326,6 +341,7 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
   fmap[(size_t)t * kCoarse + threadIdx.x] = off | (rbits << 16);
   if (threadIdx.x == 0) {
     tbin[t] = thr;
+    thi[t] = max(s_hi, thr + 1);
     tlo[t] = lo;
     fcount[t] = F;
   }
@@ -440,6 +456,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
                                                        const Item* __restrict__ items,
                                                        const int64_t* __restrict__ tbegin,
                                                        const uint32_t* __restrict__ tbin,
+                                                       const uint32_t* __restrict__ thi,
                                                        uint32_t* __restrict__ sub_cnt, uint32_t* __restrict__ item_cnt,
                                                        uint64_t* __restrict__ cand) {
   __shared__ uint32_t s_w[kWaves];
@@ -449,13 +466,13 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
     if (threadIdx.x == 0) sub_cnt[blockIdx.x] = 0;
     return;
   }
-  const uint32_t thr = tbin[it.tensor];
+  const uint32_t thr = tbin[it.tensor], hi = thi[it.tensor];
   const int64_t base = tbegin[it.tensor];
   const uint32_t lim = (uint32_t)(min(b + kSubPer, it.end) - b);
   const uint32_t o = 4u * threadIdx.x;
-  // EF modes store the residual as if every candidate were selected (t' - t': 0, or NaN for
-  // an infinite t'); the candidates that end up unselected get t' back later (fewer random
-  // stores than zeroing the selection afterwards).
+  // EF modes store t' - t' (0, or NaN for an infinite t') for the "sure" elements (bin >= hi:
+  // selected with ~6 sigma of margin) and t' for the rest; the bucket kernels then zero only
+  // the selected keys below the sure bin (and restore a sure key that was not selected).
   float vv[4] = {0.f, 0.f, 0.f, 0.f};
   uint32_t selm = 0;
   const bool full = o + 4 <= lim;
@@ -481,7 +498,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
   if (MODE != 0) {
     float rr[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) rr[c] = ((selm >> c) & 1u) ? __fsub_rn(vv[c], vv[c]) : vv[c];
+    for (int c = 0; c < 4; ++c) rr[c] = (mag_key(vv[c]) >> kSShift) >= hi ? __fsub_rn(vv[c], vv[c]) : vv[c];
     if (full) store_nt(r + b + o, make_float4(rr[0], rr[1], rr[2], rr[3]));
     else
       for (uint32_t c = 0; c < 4 && o + c < lim; ++c) r[b + o + c] = rr[c];
@@ -1003,7 +1020,8 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
                                                             const int64_t* __restrict__ kb2,
                                                             const int64_t* __restrict__ tbegin,
                                                             float* __restrict__ r, uint64_t* __restrict__ bkeys,
-                                                            const uint32_t* __restrict__ status) {
+                                                            const uint32_t* __restrict__ status,
+                                                            const uint32_t* __restrict__ thi) {
   if (status[1] | status[2]) return;  // the plan's verdict is a fallback: nothing to do
   __shared__ uint32_t s_b[kPlanMaxBuckets];
   __shared__ uint32_t s_spre[1025], s_part[1024];
@@ -1012,7 +1030,7 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
   SupView v{s_spre, s_ibeg, 0, 0};
   v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t);
   const int t = v.t;
-  const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nb = bbase[t + 1] - b0;
+  const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nb = bbase[t + 1] - b0, hi = thi[t];
   const int64_t base = tbegin[t];
   for (uint32_t j = threadIdx.x; j < nb; j += 1024) s_b[j] = 0;
   __syncthreads();
@@ -1034,8 +1052,9 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         if (e0 + (uint32_t)u * 1024 >= v.total) continue;
-        if (j[u] < 0) {  // below the k-th key's bin: never selected; its residual is t' again
-          if (phase == 1 && r) r[base + (key[u] >> 32)] = __uint_as_float((uint32_t)key[u]);
+        if (j[u] < 0) {  // below the k-th key's bin: not selected (a "sure" key gets its t' back)
+          if (phase == 1 && r && (((uint32_t)key[u] & 0x7fffffffu) >> kSShift) >= hi)
+            r[base + (key[u] >> 32)] = __uint_as_float((uint32_t)key[u]);
           continue;
         }
         if (phase == 0) {
@@ -1078,7 +1097,8 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
                                                              const uint32_t* __restrict__ tlo,
                                                              const uint32_t* __restrict__ fcount,
                                                              const uint32_t* __restrict__ fhist,
-                                                             const uint32_t* __restrict__ fse, int dbg) {
+                                                             const uint32_t* __restrict__ fse,
+                                                             const uint32_t* __restrict__ thi, int dbg) {
   __shared__ union {
     typename BucketSort::storage_type sort;
     uint64_t xch[kSubBins];
@@ -1096,7 +1116,7 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
   const uint32_t st = rec.start;
   const uint64_t* src = bkeys + rec.key_off;
   const int64_t k = kk[t], o = koff[t], base = tbegin[t], n = tsize[t];  // issued with the key loads
-  const uint32_t lo = tlo[t], F = fcount[t];
+  const uint32_t lo = tlo[t], F = fcount[t], hi = thi[t];
   const uint32_t* map_t = fmap + (size_t)t * kCoarse;
   const uint32_t* h_t = fhist + (size_t)t * kFineMax;
   const uint32_t* se_t = fse + (size_t)t * kFineMax;
@@ -1188,11 +1208,13 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
     const uint32_t idx = (uint32_t)(sk >> 1) & 0x3ffffffu;
     if ((int64_t)idx >= n) continue;  // never expected (a padding key inside the bucket's count)
     const float v = __uint_as_float(((uint32_t)(sk & 1u) << 31) | (0x7fffffffu - (uint32_t)(sk >> 33)));
+    const bool sure = ((0x7fffffffu - (uint32_t)(sk >> 33)) >> kSShift) >= hi;
     if (rank < k) {
       values[o + rank] = v;
       indices[o + rank] = (int64_t)idx;
-    } else if (r && !(dbg & 2)) {
-      r[base + idx] = v;  // a candidate of the k-th key's bin below rank k: unselected
+      if (r && !sure && !(dbg & 2)) r[base + idx] = __fsub_rn(v, v);  // selected below the sure bin
+    } else if (r && sure && !(dbg & 2)) {
+      r[base + idx] = v;  // a "sure" key that was not selected after all: t' back
     }
   }
 }
@@ -1315,7 +1337,22 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 struct HostSync {
   uint32_t* pinned = nullptr;
   hipEvent_t ev = nullptr;
+  uint32_t seq = 0;
 };
+
+// Wait for the status copy of call `seq`: spin on the pinned word (the copy lands a few µs
+// after the plan kernel; an event wait costs tens of µs of wake-up, and every µs the host
+// spends here is a µs the next call's launches come later), then the event (which also
+// reports a failed launch).
+int wait_status(HostSync* h, uint32_t seq) {
+  const auto t0 = std::chrono::steady_clock::now();
+  while (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq) {
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;  // let the event decide
+    __builtin_ia32_pause();
+  }
+  OMF_HIP(hipEventSynchronize(h->ev));
+  return OMF_OK;
+}
 HostSync* host_sync(int dev) {
   constexpr int kMaxDev = 64;
   thread_local HostSync hs[kMaxDev];
@@ -1370,7 +1407,7 @@ size_t sort_tmp_bytes(const omf_plan* p) {
 struct WsLayout {
   size_t hist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
       sub_cnt, item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes, bbase, kb2, fmap, tlo, fcount, fhist,
-      fbucket, fse, bstart, brec, bfill, nb_max, sbase;
+      fbucket, fse, bstart, brec, bfill, nb_max, sbase, thi;
 };
 
 // Bucket-table slots for any ratio (k <= n).
@@ -1380,7 +1417,27 @@ size_t bucket_slots_max(const omf_plan* p) {
   return nb;
 }
 
+WsLayout layout_uncached(const omf_plan* p);
+
+// The layout depends on the plan's shape only; the last one computed on this thread is kept
+// (sizing the library sort is not free, and this runs on every call).
 WsLayout layout(const omf_plan* p) {
+  struct Key {
+    const omf_plan* p;
+    int64_t ae;
+    int32_t nt;
+  };
+  thread_local Key key{nullptr, -1, -1};
+  thread_local WsLayout cached;
+  const Key k{p, omf_plan_access::arena_end(p), omf_plan_access::ntensors(p)};
+  if (k.p != key.p || k.ae != key.ae || k.nt != key.nt) {
+    cached = layout_uncached(p);
+    key = k;
+  }
+  return cached;
+}
+
+WsLayout layout_uncached(const omf_plan* p) {
   const int32_t nt = omf_plan_access::ntensors(p);
   const int64_t ae = omf_plan_access::arena_end(p);
   WsLayout L;
@@ -1412,6 +1469,7 @@ WsLayout layout(const omf_plan* p) {
   L.kb2 = o; o = align256(o + 8 * (size_t)nt);
   L.fmap = o; o = align256(o + 4 * (size_t)nt * kCoarse);
   L.tlo = o; o = align256(o + 4 * (size_t)nt);
+  L.thi = o; o = align256(o + 4 * (size_t)nt);
   L.fcount = o; o = align256(o + 4 * (size_t)nt);
   L.fhist = o; o = align256(o + 4 * (size_t)nt * kFineMax);
   L.fbucket = o; o = align256(o + 4 * (size_t)nt * kFineMax);
@@ -1492,6 +1550,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   int64_t* kb2 = reinterpret_cast<int64_t*>(w + L.kb2);
   uint32_t* fmap = reinterpret_cast<uint32_t*>(w + L.fmap);
   uint32_t* tlo = reinterpret_cast<uint32_t*>(w + L.tlo);
+  uint32_t* thi = reinterpret_cast<uint32_t*>(w + L.thi);
   uint32_t* fcount = reinterpret_cast<uint32_t*>(w + L.fcount);
   uint32_t* fhist = reinterpret_cast<uint32_t*>(w + L.fhist);
   int32_t* fbucket = reinterpret_cast<int32_t*>(w + L.fbucket);
@@ -1512,23 +1571,27 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
 
   const bool glob = global_path(plan);
   if (!glob) OMF_HIP(hipMemsetAsync(w, 0, L.zero_end, st));
-  hipLaunchKernelGGL(topk_setup, dim3(1), blk, 0, st, d_sizes, nt, ratio, kk, koff, tfirst, tlast, bbase, kb2, sbase, status);
+  HostSync* hsync = host_sync(omf_plan_access::device(plan));
+  if (!hsync) return fail(OMF_EHIP, "omf_topk_encode: pinned status buffer");
+  const uint32_t seq = ++hsync->seq == 0 ? ++hsync->seq : hsync->seq;
+  hipLaunchKernelGGL(topk_setup, dim3(1), blk, 0, st, d_sizes, nt, ratio, kk, koff, tfirst, tlast, bbase, kb2, sbase, status,
+                     seq);
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
     const dim3 sgrid((unsigned)nt), sblk(1024), fgrid((unsigned)(n_items * kSubsPerItem));
     if (residual_mode == 1) {
       hipLaunchKernelGGL((topk_sample_threshold<1>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
-                         tfirst, tlast, tbin, hist, item_cnt, fmap, tlo, fcount, fhist);
-      hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, sub_cnt, item_cnt, cand);
+                         tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
+      hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt, item_cnt, cand);
     } else {
       hipLaunchKernelGGL((topk_sample_threshold<0>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
-                         tfirst, tlast, tbin, hist, item_cnt, fmap, tlo, fcount, fhist);
+                         tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
       if (residual_mode == 2)
-        hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, sub_cnt,
-                           item_cnt, cand);
+        hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi,
+                           sub_cnt, item_cnt, cand);
       else
-        hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, sub_cnt,
-                           item_cnt, cand);
+        hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi,
+                           sub_cnt, item_cnt, cand);
     }
     // fast path: exact fine-bin histograms, bucket plan; one status read decides
     const dim3 supgrid((unsigned)nsup), supblk(1024);
@@ -1540,19 +1603,17 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     // The plan's verdict goes to pinned host memory behind an event; the bucket kernels are
     // enqueued before the host waits for it (they do nothing when the verdict is a fallback),
     // so the GPU does not idle while the host reads it.
-    HostSync* hsync = host_sync(omf_plan_access::device(plan));
-    if (!hsync) return fail(OMF_EHIP, "omf_topk_encode: pinned status buffer");
     OMF_HIP(hipMemcpyAsync(hsync->pinned, status, 16, hipMemcpyDeviceToHost, st));
     OMF_HIP(hipEventRecord(hsync->ev, st));
     const bool forced = force_fallback();
     if (!forced) {
       hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast,
-                         fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins, rz, sorted, status);
+                         fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins, rz, sorted, status, thi);
       hipLaunchKernelGGL(topk_bucket_sort, dim3((unsigned)nbuckets), dim3(kBT), 0, st, sorted, brec, kk, koff, d_begins,
-                         d_sizes, rz, values, indices, status, fmap, tlo, fcount, fhist, fse, dbg_bits());
+                         d_sizes, rz, values, indices, status, fmap, tlo, fcount, fhist, fse, thi, dbg_bits());
       OMF_HIP(hipGetLastError());
     }
-    OMF_HIP(hipEventSynchronize(hsync->ev));
+    if (int rc = wait_status(hsync, seq)) return rc;
     uint32_t host_status[4];
     std::memcpy(host_status, hsync->pinned, 16);
     if (dbg_bits() & 4) fprintf(stderr, "omf_topk: redo %u overflow %u\n", host_status[1], host_status[2]);

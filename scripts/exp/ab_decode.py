@@ -17,9 +17,10 @@ nr = torch.empty(len(sizes), device=dev)
 p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1)
 y = torch.empty(p.arena_end, device=dev)
 res = {"0": [], "1": []}
+VAR = sys.argv[1] if len(sys.argv) > 1 else "OMF_DEC_NTL"
 for rnd in range(8):
     for v in ("0", "1"):
-        os.environ["OMF_DEC_NTL"] = v
+        os.environ[VAR] = v
         p.qsgd_decode(q, 8, 16, nr, y_out=y)
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -31,4 +32,4 @@ for rnd in range(8):
         res[v].append(e0.elapsed_time(e1) / 10)
 for v in res:
     t = sorted(res[v])
-    print(f"decode ntl={v}: median {t[len(t) // 2]:.4f} ms min {t[0]:.4f}", flush=True)
+    print(f"decode {VAR}={v}: median {t[len(t) // 2]:.4f} ms min {t[0]:.4f}", flush=True)

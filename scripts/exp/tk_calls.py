@@ -22,3 +22,9 @@ for i, c in enumerate(calls):
     tot = sum(d for _, d in c["_k"])
     print(f"call {i:2d}: span {(c['_end'] - c['_start']) / 1e3:7.1f} us, kernels {tot:7.1f}: " +
           " ".join(f"{n.split('<')[0][-14:]}={d:.0f}" for n, d in c["_k"]))
+
+# gaps: GPU idle between consecutive kernels inside each call, and before each call's setup
+prev_end = None
+for i, c in enumerate(calls):
+    print(f"call {i:2d}: idle before setup {((c['_start'] - prev_end) / 1e3) if prev_end else 0:7.1f} us")
+    prev_end = c["_end"]
