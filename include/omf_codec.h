@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct omf_plan omf_plan;
 
-/* ABI version (major*100 + minor). */
+/* ABI version (major*100 + minor): 102. */
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -85,6 +85,10 @@ int omf_plan_check(omf_plan* plan, void* stream);
  * hold limit take a second read.  Identical payloads given the norm; the norms fold
  * partials over different chunk sizes, so strategies agree to rounding. */
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy);
+/* The plan's encode strategy (0/1/2 as above).  A new plan picks 1 (two-pass, whose second
+ * read is served by the Infinity Cache) for arenas of >= 2^28 elements and 2 (the ring)
+ * below: the measured crossover; OMF_ENCODE_STRATEGY overrides. */
+int32_t omf_plan_encode_strategy(const omf_plan* plan);
 /* Ring encoder tuning / test hook (rebuilds the chunk sequence; not for the hot path):
  * cfg = kernel configuration (-1 keep), big_mode 0/1 (placement of second-read chunks,
  * -1 keep), gap = items between a large tensor's first and second pass (-2 keep, -1 one

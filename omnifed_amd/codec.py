@@ -103,8 +103,8 @@ class Plan:
         self._lock = threading.Lock()
         self._topk_ws: Dict[int, torch.Tensor] = {}  # per stream: launches on two streams never share one
         self._topk_cache: Dict[float, tuple] = {}
-        # the library's default (omf_qsgd.hip), unless an experiment overrides it
-        self.strategy = {"0": "resident", "2": "ring"}.get(os.environ.get("OMF_ENCODE_STRATEGY", ""), "ordered")
+        # the library's choice (by arena size, or OMF_ENCODE_STRATEGY)
+        self.strategy = ("resident", "ordered", "ring")[int(L.omf_plan_encode_strategy(h))]
 
     @classmethod
     def get(cls, sizes, offsets=None, device=None, chunk: int = 0) -> "Plan":

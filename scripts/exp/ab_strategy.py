@@ -9,7 +9,8 @@ sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(_
 from omnifed_amd import codec, shapes  # noqa: E402
 
 dev = torch.device("cuda", 0)
-sizes = [shapes.numel(s) for _, s in shapes.model_shapes("llama400m")]
+MODEL = __import__("os").environ.get("MODEL", "llama400m")
+sizes = [shapes.numel(s) for _, s in shapes.model_shapes(MODEL)]
 strats = sys.argv[1:] or ["ring", "ordered"]
 plans = {}
 for sname in strats:
@@ -42,4 +43,4 @@ for rnd in range(6):
         res[sn].append(e0.elapsed_time(e1) / 10)
 for sn in strats:
     v = sorted(res[sn])
-    print(f"{sn:8s}: median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f}", flush=True)
+    print(f"{MODEL} {sn:8s}: median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f}", flush=True)

@@ -102,6 +102,7 @@ def test_gpu_norm_accuracy_and_single_launch_parity(gpu, strategy):
     """Single-launch encode (in-kernel norm hand-off; every strategy) vs oracle given the GPU norm."""
     for s in (3, 4, 8):
         plan, x, parts = _mixed_arena(gpu, MIXED_SIZES, seed=10 * s)
+        prev = plan.strategy
         plan.set_encode_strategy(strategy)
         u_host = np.zeros(plan.arena_end, np.float32)
         stream = oracle.MTStream(7 + s)
@@ -122,7 +123,7 @@ def test_gpu_norm_accuracy_and_single_launch_parity(gpu, strategy):
             assert torch.equal(n2, norms)
         else:
             torch.testing.assert_close(n2, norms, rtol=2e-6, atol=0)
-        plan.set_encode_strategy("ordered")  # restore the default on the cached plan
+        plan.set_encode_strategy(prev)  # restore the default on the cached plan
 
 
 def test_strategies_agree_and_fallback_exact(gpu):
@@ -132,6 +133,7 @@ def test_strategies_agree_and_fallback_exact(gpu):
     g = torch.Generator(device=gpu)
     g.manual_seed(5)
     x = torch.randn(plan.arena_end, device=gpu, generator=g)
+    prev = plan.strategy
     plan.set_encode_strategy("resident")
     q1, n1 = plan.qsgd_encode(x, 4, seed=3, offset=1)
     assert plan.check()
@@ -145,7 +147,7 @@ def test_strategies_agree_and_fallback_exact(gpu):
     q3, n3 = plan.qsgd_encode(x, 4, seed=3, offset=1)
     assert plan.check()
     torch.testing.assert_close(n3, n2, rtol=2e-6, atol=0)
-    plan.set_encode_strategy("ordered")  # the default, on the cached plan
+    plan.set_encode_strategy(prev)  # the default, on the cached plan
     for strategy in ("ring", "resident", "ordered"):
         small = codec.Plan([40000] * 8 + [1 << 20], device=gpu)
         small.set_encode_strategy(strategy)

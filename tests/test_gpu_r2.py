@@ -124,6 +124,7 @@ def test_int8_payload_stays_inside_its_buffer(gpu):
     buf = torch.full((plan.payload_elems(8) + 64,), 0x5A, dtype=torch.int8, device=gpu)
     with pytest.raises(ValueError):
         plan.qsgd_encode(x, 4, q_out=buf[:plan.arena_end], seed=3)
+    prev = plan.strategy
     for strategy in ("ring", "ordered"):
         plan.set_encode_strategy(strategy)
         buf.fill_(0x5A)
@@ -135,7 +136,7 @@ def test_int8_payload_stays_inside_its_buffer(gpu):
         o = plan.offsets[2]
         want, *_ = oracle.qsgd_quantize(x[o:o + sizes[2]].cpu(), 4, norm=float(norms[2]), u=torch.from_numpy(ref))
         assert q[o:o + sizes[2]].cpu().numpy().tobytes() == want.numpy().tobytes()
-    plan.set_encode_strategy("ordered")
+    plan.set_encode_strategy(prev)
 
 
 # ---------------------------------------------------------------- bf16 / fp16 (golden_r2 half/*)
@@ -394,3 +395,12 @@ def test_layer_states_belong_to_the_callers_pb2(gpu, monkeypatch):
         stand_in.ModelParameters(round_number=1, layers=layers, is_ready=True)
         with pytest.raises(TypeError):  # the private schema's messages would be refused
             stand_in.ModelUpdate(layers=[pb.LayerState(layer_name="x")])
+
+
+def test_default_encode_strategy_by_arena_size(gpu):
+    """A new plan takes the two-pass encoder for arenas of >= 2^28 elements (its second read is
+    served by the Infinity Cache) and the single-read ring below."""
+    small = codec.Plan([1 << 20, 5000], device=gpu)
+    assert small.strategy == "ring"
+    big = codec.Plan([1 << 27, 1 << 27, 1000], device=gpu)
+    assert big.strategy == "ordered"
