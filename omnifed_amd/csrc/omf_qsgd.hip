@@ -239,7 +239,7 @@ __device__ __forceinline__ float chunk_sumsq(const EncArgs& a, int64_t b, int64_
   for (int64_t sb = b; sb < e; sb += S) {
     const int64_t se = min(sb + S, e);
     float4 v[V];
-    if (se - sb == S) load_f4<V, true>(a.x, sb, se, v);
+    if (se - sb == S) load_f4<V, true>(a.x, sb, se, v);  // default policy: the QUANT re-read hits the Infinity Cache
     else load_f4<V, false>(a.x, sb, se, v);
     scale_f4<V>(v, a);
     acc = sumsq_f4<V>(v, acc);

@@ -15,8 +15,10 @@ strats = sys.argv[1:] or ["ring", "ordered"]
 plans = {}
 for sname in strats:
     p = codec.Plan(sizes, device=dev)
-    if sname != "flat":
+    if sname not in ("flat", "norms"):
         p.set_encode_strategy(sname)
+    elif sname == "norms":
+        p.set_encode_strategy("ordered")
     plans[sname] = p
 x = torch.randn(plans[strats[0]].arena_end, device=dev) * 1e-3
 q = torch.empty(plans[strats[0]].payload_elems(8), dtype=torch.int8, device=dev)
@@ -30,6 +32,8 @@ for rnd in range(6):
         def run(o):
             if sn == "flat":
                 p.qsgd_encode(x, 4, q_out=q, norm_in=nr, seed=1, offset=o)
+            elif sn == "norms":
+                p.qsgd_norms(x, norm_out=nr)
             else:
                 p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1, offset=o)
         run(0)
