@@ -321,3 +321,30 @@ def test_topk_clustered_magnitudes_bucket_merge(gpu):
     same = m[:-1] == m[1:]
     assert bool(torch.all(ih[:-1][same] < ih[1:][same]))
     assert torch.equal(vh, xh[ih])
+
+
+def test_topk_exact_path_many_tensors_and_arena_decode(gpu):
+    """A plan of more than 256 tensors takes the exact path (histogram of every t', segmented
+    sort): selection = torch.topk's magnitudes in descending order, values = t' at the indices,
+    the residual zeroed there; the whole-arena decode (k offsets over > 256 tensors) rebuilds it."""
+    g = torch.Generator().manual_seed(21)
+    sizes = [int(s) for s in torch.randint(50, 4000, (300,), generator=g)]
+    plan = codec.Plan(sizes, device=gpu)
+    x = torch.randn(plan.arena_end, generator=g).to(gpu)
+    res = torch.zeros(plan.arena_end, device=gpu)
+    values, indices, ks = plan.topk_encode(x, 0.05, residual=res, residual_mode=2)
+    K = 0
+    for t, (o, n) in enumerate(zip(plan.offsets, sizes)):
+        k = ks[t]
+        tp = x[o:o + n]
+        v, i = values[K:K + k], indices[K:K + k]
+        want, _ = torch.topk(tp.abs(), k, sorted=True)
+        assert torch.equal(v.abs(), want), t
+        assert torch.equal(v, tp[i]), t
+        r = tp.clone()
+        r[i] = 0.0
+        assert torch.equal(res[o:o + n], r), t
+        K += k
+    y = plan.topk_decode_arena(values, indices, 0.05)
+    for o, n in zip(plan.offsets, sizes):
+        assert torch.equal(y[o:o + n] + res[o:o + n], x[o:o + n])
