@@ -27,7 +27,7 @@ def load(d, counter):
 
 
 def short(name):
-    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_decode_flat", "qsgd_quant_flat",
+    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_decode_flat", "qsgd_quant_sub",
               "topk_fused", "topk_prep_hist", "topk_collect", "topk_gather", "topk_scatter_arena"):
         if k in name:
             return k
