@@ -60,9 +60,10 @@ const char* omf_last_error(void);
 /*
  * Plan over a fixed list of named tensors (one client's update dict).
  * sizes/offsets are HOST arrays of ntensors elements; chunk_elems is the work unit of
- * one workgroup in the two-pass encoder (0 = default 65536; a multiple of 16384).
- * Decode and the other passes use 16384-element items; tensors of <= 16384 elements
- * are encoded by one workgroup each (norm and levels from registers).
+ * one workgroup in the two-pass encoder (0 = default 32768; a multiple of 16384).
+ * Decode and the other passes use 16384-element items; tensors of <= 8192 elements
+ * (the encoder's rows x 1024) are encoded by one workgroup each (norm and levels from
+ * registers).
  * Replaces the per-call Python loop of encode_updates_dict /
  * decode_updates_dict (src/omnifed/hybrid/communicator/global_grpc_compression.py:207-223).
  */

@@ -805,7 +805,8 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
   if (!out) return fail(OMF_EINVAL, "omf_plan_create: out is NULL");
   *out = nullptr;
   if (ntensors <= 0 || !sizes || !offsets) return fail(OMF_EINVAL, "omf_plan_create: need >= 1 tensor");
-  if (chunk_elems == 0) chunk_elems = 4 * kSub;  // two-pass encode items: 256 KiB of fp32
+  if (chunk_elems == 0) chunk_elems = 2 * kSub;  // two-pass encode items: 128 KiB of fp32 (32 Ki: 0.579 vs
+                                                 // 0.595 ms at 64 Ki on Llama-400M, scripts/exp/ab_chunk.py)
   if (chunk_elems < kSub || chunk_elems % kSub != 0)
     return fail(OMF_EINVAL, "omf_plan_create: chunk_elems must be a positive multiple of 16384");
   for (int32_t t = 0; t < ntensors; ++t) {

@@ -9,7 +9,7 @@ from omnifed_amd import codec, shapes  # noqa: E402
 
 dev = torch.device("cuda", 0)
 sizes = [shapes.numel(s) for _, s in shapes.model_shapes(sys.argv[1] if len(sys.argv) > 1 else "llama400m")]
-chunks = [16384 * m for m in (1, 2, 4, 8, 16, 32)]
+chunks = [16384 * m for m in (2, 4)]
 plans = {c: codec.Plan(sizes, device=dev, chunk=c) for c in chunks}
 for p in plans.values():
     p.set_encode_strategy("ordered")
@@ -18,7 +18,7 @@ x = torch.randn(p0.arena_end, device=dev) * 1e-3
 q = torch.empty(p0.payload_elems(8), dtype=torch.int8, device=dev)
 nr = torch.empty(len(sizes), device=dev)
 res = {c: [] for c in chunks}
-for rnd in range(6):
+for rnd in range(12):
     for c in chunks:
         p = plans[c]
         p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1)
