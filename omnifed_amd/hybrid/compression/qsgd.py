@@ -17,9 +17,10 @@ Random draws (``rng``):
     Statistically the reference's ``rand_like`` (24-bit uniforms), not the same bits.
   * ``"mt19937"``: the reference's own stream: ``torch.rand`` on the default CPU
     generator, consumed tensor by tensor and skipped for zero-norm tensors
-    (qsgd.py:47-48, 58), handed to the kernel as an input buffer.  Bit-identical
-    payloads follow whenever the norm equals the reference's (its fp32
-    ``torch.norm`` is ISA dependent).
+    (qsgd.py:47-48, 58), handed to the kernel as an input buffer, and the reference's own
+    norm: ``torch.norm`` of the tensor's CPU copy (ISA dependent, SURVEY.md §0.6, so it is
+    computed by the same op on the same host).  Payloads are then bit-identical to the
+    reference's on that host.  A parity / debugging mode: the draws and norms run on the CPU.
 
 Dtypes: the reference quantises in the tensor's own dtype.  float32, bfloat16 and
 float16 tensors are encoded with that dtype's rounding (``omf_qsgd_encode_ex``
@@ -97,8 +98,20 @@ def encode_groups(flats: Sequence[torch.Tensor], bit_width: int, dev: torch.devi
     s = int(bit_width)
     out = []
     if rng == "mt19937":
-        norms = [plan.qsgd_norms(x, alpha=alpha, value_format=fmt) for plan, x, fmt, _ in groups]
-        host = [n.cpu().tolist() for n in norms]
+        # Parity mode: each norm is the reference's own op on the host, torch.norm of the
+        # (weighted) tensor's CPU copy in its dtype (qsgd.py:46 after global_grpc.py:101-123's
+        # torch.mul) - so the payload is the reference's bit for bit on the same host, not only
+        # when the GPU's fp32 norm happens to round alike.
+        host = []
+        for plan, x, fmt, idx in groups:
+            hn = []
+            for i in idx:
+                v = flats[i].detach().reshape(-1)
+                if alpha != 1.0:
+                    v = torch.mul(v, alpha)
+                hn.append(float(torch.norm(v.cpu()).item()))
+            host.append(hn)
+        norms = [torch.tensor(hn, dtype=torch.float32).to(dev) for hn in host]
         where = {i: (g, k) for g, (_, _, _, idx) in enumerate(groups) for k, i in enumerate(idx)}
         u_host = [torch.zeros(plan.arena_end, dtype=torch.float32) for plan, _, _, _ in groups]
         for i in range(len(flats)):  # the reference's draw order: tensor by tensor

@@ -348,3 +348,26 @@ def test_topk_exact_path_many_tensors_and_arena_decode(gpu):
     y = plan.topk_decode_arena(values, indices, 0.05)
     for o, n in zip(plan.offsets, sizes):
         assert torch.equal(y[o:o + n] + res[o:o + n], x[o:o + n])
+
+
+def test_encode_updates_dict_mt_is_the_reference_bit_for_bit(gpu, golden, golden_index):
+    """Parity RNG mode computes each norm with the reference's own op on this host
+    (torch.norm of the CPU copy), so every LayerState equals the reference's byte for byte -
+    provided this host's torch.norm rounds like the fixture host's (ISA dependent, SURVEY §0.6;
+    checked first, skipped otherwise)."""
+    for c in golden_index["dict"]:
+        key = f"dict/{c['s']}"
+        upd = {n: torch.from_numpy(golden[f"{key}/in/{n}"]) for n in c["names"]}
+        for n in c["names"]:
+            G = _layer(golden, f"{key}/layer/{n}")
+            if G.meta_tensor:
+                ref = float(np.frombuffer(G.meta_tensor, np.float32)[0])
+                if float(torch.norm(upd[n].reshape(-1)).item()) != ref:
+                    pytest.skip("this host's torch.norm rounds differently from the fixture host's")
+        comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=c["s"])
+        comp.rng = "mt19937"
+        torch.manual_seed(c["seed"])
+        layers = encode_updates_dict(upd, comp)
+        for L, n in zip(layers, c["names"]):
+            G = _layer(golden, f"{key}/layer/{n}")
+            assert L.SerializeToString() == G.SerializeToString(), n
