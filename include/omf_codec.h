@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct omf_plan omf_plan;
 
-/* ABI version (major*100 + minor): 102. */
+/* ABI version (major*100 + minor): 103. */
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -83,13 +83,23 @@ int omf_plan_check(omf_plan* plan, void* stream);
  * 1 = two-pass for every tensor (x re-read after the norm);
  * 2 = single-read "ring" encoder: persistent workgroups keep each chunk in an LDS ring
  * until its tensor's norm is complete; tensors larger than the ring's
- * hold limit take a second read.  Identical payloads given the norm; the norms fold
+ * hold limit take a second read;
+ * 3 = bracketed single-read encoder (fp32 values, on-device draws; otherwise as 1): a sampled
+ * bracket of each tensor's norm, one pass that reads x once and writes every level that is
+ * the same for every norm in the bracket, a fold of the exact norm, and a fix pass for the
+ * few undecided quads.  Identical payloads given the norm; the norms fold
  * partials over different chunk sizes, so strategies agree to rounding. */
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy);
 /* The plan's encode strategy (0/1/2 as above).  A new plan picks 1 (two-pass, whose second
  * read is served by the Infinity Cache) for arenas of >= 2^28 elements and 2 (the ring)
  * below: the measured crossover; OMF_ENCODE_STRATEGY overrides. */
 int32_t omf_plan_encode_strategy(const omf_plan* plan);
+/* Diagnostics of the last bracketed single-read encode (strategy 3; synchronises `stream`,
+ * not for the hot path): out[0] tensors requantised whole (norm outside the sampled bracket,
+ * a wave's undecided-quad slot overflowed, or a degenerate sample), out[1] of those the
+ * deferred ones (degenerate sample), out[2] undecided quads fixed from the slots, out[3]
+ * wave slots filled to capacity. */
+int omf_plan_spec_stats(omf_plan* plan, void* stream, int64_t* out4);
 /* Ring encoder tuning / test hook (rebuilds the chunk sequence; not for the hot path):
  * cfg = kernel configuration (-1 keep), big_mode 0/1 (placement of second-read chunks,
  * -1 keep), gap = items between a large tensor's first and second pass (-2 keep, -1 one

@@ -43,6 +43,7 @@ SIGNATURES = {
     "omf_plan_set_resident_capacity": (ctypes.c_int, [_c_p, _c_i64, _c_i64]),
     "omf_plan_set_ring": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i64, _c_i64]),
     "omf_plan_ring_info": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64)]),
+    "omf_plan_spec_stats": (ctypes.c_int, [_c_p, _c_p, ctypes.POINTER(_c_i64)]),
     "omf_plan_ring_profile": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64)]),
     "omf_qsgd_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p, _c_p, _c_p]),
     "omf_qsgd_norms": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_p]),

@@ -68,6 +68,10 @@ def _need(t: torch.Tensor, name: str, dtype, device, numel: int, align: int):
         raise ValueError(f"{name} must be {align}-byte aligned")
 
 
+# encoder strategies by omf_plan_set_encode_strategy code (include/omf_codec.h)
+STRATEGIES = ("resident", "ordered", "ring", "bracket")
+
+
 class Plan:
     """An ``omf_plan`` over fixed tensor sizes/offsets on one device (cached, reusable)."""
 
@@ -104,7 +108,7 @@ class Plan:
         self._topk_ws: Dict[int, torch.Tensor] = {}  # per stream: launches on two streams never share one
         self._topk_cache: Dict[float, tuple] = {}
         # the library's choice (by arena size, or OMF_ENCODE_STRATEGY)
-        self.strategy = ("resident", "ordered", "ring")[int(L.omf_plan_encode_strategy(h))]
+        self.strategy = STRATEGIES[int(L.omf_plan_encode_strategy(h))]
 
     @classmethod
     def get(cls, sizes, offsets=None, device=None, chunk: int = 0) -> "Plan":
@@ -155,16 +159,16 @@ class Plan:
         check(lib().omf_plan_set_resident_capacity(self._h, int(cap), int(wait_us)), "omf_plan_set_resident_capacity")
 
     def set_encode_strategy(self, strategy: str) -> None:
-        """'ring' (single-read encoder), 'ordered' (two-pass everywhere) or 'resident'
-        (register-resident small tensors + two-pass)."""
-        code = {"resident": 0, "ordered": 1, "ring": 2}[strategy]
+        """'bracket' (bracketed single-read encoder), 'ring' (single-read ring encoder),
+        'ordered' (two-pass everywhere) or 'resident' (register-resident small tensors + two-pass)."""
+        code = STRATEGIES.index(strategy)
         check(lib().omf_plan_set_encode_strategy(self._h, code), "omf_plan_set_encode_strategy")
         self.strategy = strategy
 
     @property
     def encoder_kernel(self) -> str:
         """Name of the kernel one encode launch runs (profiling / roofline bookkeeping)."""
-        return "qsgd_encode_pc" if self.strategy == "ring" else "qsgd_encode_ordered"
+        return {"ring": "qsgd_encode_pc", "bracket": "qsgd_spec_quant"}.get(self.strategy, "qsgd_encode_ordered")
 
     def set_ring(self, cfg: int = -1, big_mode: int = -1, gap: int = -2, hold_max: int = -1) -> None:
         """Tuning / test hook of the ring encoder: see omf_plan_set_ring."""
@@ -175,6 +179,13 @@ class Plan:
         out = (ctypes.c_int64 * 16)()
         check(lib().omf_plan_ring_profile(self._h, out), "omf_plan_ring_profile")
         return [int(v) for v in out]
+
+    def spec_stats(self, stream: Optional[int] = None) -> Dict[str, int]:
+        """Diagnostics of the last bracketed encode (omf_plan_spec_stats; synchronises)."""
+        out = (ctypes.c_int64 * 4)()
+        st = stream if stream is not None else _stream(self.device)
+        check(lib().omf_plan_spec_stats(self._h, ctypes.c_void_p(st), out), "omf_plan_spec_stats")
+        return dict(zip(("whole", "deferred", "listed", "full_slots"), (int(v) for v in out)))
 
     @property
     def ring_info(self) -> Dict[str, int]:

@@ -379,6 +379,438 @@ __global__ __launch_bounds__(kThreads) void qsgd_quant_sub(EncArgs a) {
   quant_sub<WIDTH, HAS_U, V, NT>(a, b, min(b + (int64_t)V * 1024, it.end), ti.begin, it.tensor, norm);
 }
 
+// ---------------------------------------------------------------- bracketed single-read encoder
+//
+// Strategy 3: x is read once without waiting for any norm.
+//   qsgd_spec_bracket  one workgroup per tensor: a bracket [n_lo, n_hi] of its norm from a
+//                      stratified sample (exact for small tensors) and the multipliers
+//                      c_lo <= L / n_hi, c_hi >= L / n_lo (outward margins of 2^-20).
+//   qsgd_spec_quant    one workgroup per 4 Ki-element block, no barrier: each wave's fp64
+//                      partial sum of squares, and every element's level for ANY norm in the
+//                      bracket: dl = fma(|x|, c_lo, -u), dh = fma(|x|, c_hi, -u); the level is
+//                      ceil(dl) == ceil(dh) (clamped to L, sign of x) when they agree — the
+//                      exact level is ceil(|RN(x/n)| L - u), monotone in n — else the quad is
+//                      "undecided" and listed in the wave's slot (scripts/exp/spec_check.c
+//                      checks the rule: 0 mismatches at brackets' end points and at decision
+//                      points j + u; u == 0 with x != 0 is always undecided).
+//   qsgd_spec_fold     one workgroup per tensor: folds its wave partials in a fixed order
+//                      (the norm), checks it lies in the bracket.
+//   qsgd_spec_fix      one thread per wave slot: the listed quads exactly (Markstein division,
+//                      the shared element math); a tensor whose norm fell outside its bracket,
+//                      whose slots overflowed or whose sample was degenerate is requantised
+//                      whole from x (exact; the rare path).
+// Payload bits equal every other strategy's for the same norm.
+constexpr int kSpecV = 4;                                    // float4 rows per thread
+constexpr int64_t kSpecBlk = (int64_t)kSpecV * kThreads * 4;  // 4096 elements per block
+constexpr int kSpecSlot = 32;                                 // words per block: 4 wave counts + 4 x 7 quads
+constexpr int kSpecPerWave = 7;                               // listed quads per wave
+constexpr int64_t kSpecExact = 16384;                         // tensors read whole by the bracket
+constexpr int kSpecRuns = 2048;                               // sampled 16-element runs otherwise (at most)
+constexpr int kSpecRunsPerPart = 512;                         // runs per bracket workgroup (2 per thread)
+constexpr int kSpecSeg = 2048;                                // wave partials per fold workgroup
+// Widest level count the bracket serves: the undecided fraction grows with L (a level step is
+// norm / L wide), and at L = 32 a 1 Mi-element tensor's sampled bracket already leaves ~1.3
+// undecided quads per wave; wider payloads take the two-pass encoder.
+constexpr int kSpecMaxBits = 4;
+constexpr int kSpecMinBits = 1;  // L >= 2 (spec_check.c's underflow argument)
+
+struct SpecBracket {
+  float c_lo, c_hi, n_lo, n_hi;
+  uint32_t mode;  // 0 speculate, 1 deferred (degenerate sample: the fix pass requantises)
+  uint32_t pad[3];
+};
+
+// Bracket work item: part `part` of `nparts` of tensor `tensor` (a sampled tensor's runs are
+// split over up to 4 workgroups; a small tensor is one exact part).
+struct SpecBrItem {
+  int64_t base;  // stratum length n / R (R = runs of the tensor); rem = n % R strata are one longer
+  int32_t R, rem;
+  int32_t tensor, part, nparts, pbase;
+};
+// Fold work item: wave partials [p_begin, p_end) of tensor `tensor`, segment `seg` of `nsegs`.
+struct SpecFoldItem {
+  int64_t p_begin, p_end;
+  int32_t tensor, seg, nsegs, sbase;
+};
+
+struct SpecArgs {
+  EncArgs e;               // x, q, norm_out, items (flat 16 Ki items), alpha, levels, Philox key
+  const int64_t* begins;   // per tensor
+  const int64_t* sizes;
+  const SpecBrItem* br_items;
+  const SpecFoldItem* fold_items;
+  SpecBracket* br;
+  uint64_t* br_part;       // per bracket item: {S1, S2} fp64 bits
+  uint64_t* seg_part;      // per fold item: fp64 bits
+  uint32_t* br_cnt;        // per tensor arrival counters (reset by the last arriver)
+  uint32_t* fold_cnt;
+  uint64_t* partials;      // fp64 bits, one per wave (kWaves per block)
+  uint32_t* slots;         // kSpecSlot words per block; word w < kWaves: (tensor << 8) | count of wave w
+  uint32_t* flags;         // per tensor: a wave's slot overflowed (set by quant, cleared by fold)
+  uint32_t* status;        // per tensor: 0 = listed quads only, 1 = requantise whole
+  uint32_t* any_whole;     // = epoch when some tensor of this launch is requantised whole
+  uint32_t epoch;          // per-launch tag (never 0)
+  int64_t nblocks;
+};
+
+__device__ __forceinline__ uint32_t spec_hash(uint32_t a, uint32_t b) {
+  uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
+  h ^= h >> 15; h *= 0x2C1B3C6Du; h ^= h >> 12; h *= 0x297A2D39u; h ^= h >> 15;
+  return h;
+}
+
+__device__ __forceinline__ float4 scale_alpha(float4 v, float alpha) {
+  if (alpha != 1.0f) {
+    v.x = __fmul_rn(v.x, alpha); v.y = __fmul_rn(v.y, alpha);
+    v.z = __fmul_rn(v.z, alpha); v.w = __fmul_rn(v.w, alpha);
+  }
+  return v;
+}
+
+__device__ __forceinline__ float sq4(float4 v, float s) {
+  s = fmaf(v.x, v.x, s); s = fmaf(v.y, v.y, s);
+  s = fmaf(v.z, v.z, s); return fmaf(v.w, v.w, s);
+}
+
+__global__ __launch_bounds__(kThreads) void qsgd_spec_bracket(SpecArgs a) {
+  __shared__ double red[kWaves];
+  __shared__ uint32_t s_last;
+  const SpecBrItem bi = a.br_items[blockIdx.x];
+  const int32_t t = bi.tensor;
+  const int64_t tb = a.begins[t], n = a.sizes[t];
+  const float* __restrict__ x = a.e.x + tb;
+  const float alpha = a.e.alpha;
+  double s1 = 0.0, s2 = 0.0;
+  const bool exact = n <= kSpecExact;
+  // runs of 16 elements: one at a hashed position inside each of R balanced strata (strata of
+  // >= 32 elements); this part takes runs [part * 512, part * 512 + 512)
+  const int64_t R = bi.R;
+  if (exact) {  // 16 float4 per thread, all loads in flight
+    constexpr int PER = (int)(kSpecExact / (4 * kThreads));
+    float4 v[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int64_t e = 4 * ((int64_t)i * kThreads + threadIdx.x);
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (e + 4 <= n) {
+        v[i] = *reinterpret_cast<const float4*>(x + e);
+      } else if (e < n) {
+        v[i].x = x[e];
+        if (e + 1 < n) v[i].y = x[e + 1];
+        if (e + 2 < n) v[i].z = x[e + 2];
+      }
+    }
+    float acc = 0.0f;
+#pragma unroll
+    for (int i = 0; i < PER; ++i) acc = sq4(scale_alpha(v[i], alpha), acc);
+    s1 = acc;
+  } else {
+    constexpr int PER = kSpecRunsPerPart / kThreads;
+    const int64_t base = bi.base, rem = bi.rem;
+    float4 v[PER][4];
+    bool live[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int64_t r = (int64_t)bi.part * kSpecRunsPerPart + threadIdx.x + (int64_t)i * kThreads;
+      live[i] = r < R;
+      if (live[i]) {
+        const int64_t lo = r * base + min(r, rem), len = base + (r < rem ? 1 : 0);
+        const int64_t pos = (lo + (int64_t)(spec_hash((uint32_t)r, (uint32_t)t) % (uint32_t)(len - 15))) & ~(int64_t)3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[i][j] = *reinterpret_cast<const float4*>(x + pos + 4 * j);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      if (live[i]) {
+        float sr = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) sr = sq4(scale_alpha(v[i][j], alpha), sr);
+        s1 += (double)sr;
+        s2 += (double)sr * (double)sr;
+      }
+    }
+  }
+  const double S1p = block_sum_f64(s1, red);
+  const double S2p = block_sum_f64(s2, red);
+  // publish this part; the last arriver of the tensor folds the parts in order (cdna_hip_
+  // programming.md §6 G16: sc1 stores drained before the agent-scope counter add)
+  if (threadIdx.x == 0) {
+    uint32_t last = 1u;
+    if (bi.nparts > 1) {
+      st_agent(&a.br_part[2 * (bi.pbase + bi.part)], (uint64_t)__double_as_longlong(S1p));
+      st_agent(&a.br_part[2 * (bi.pbase + bi.part) + 1], (uint64_t)__double_as_longlong(S2p));
+      drain_vmem();
+      last = add_agent(&a.br_cnt[t], 1u) == (uint32_t)(bi.nparts - 1) ? 1u : 0u;
+      if (last) __hip_atomic_store(&a.br_cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  double S1 = S1p, S2 = S2p;
+  if (bi.nparts > 1) {  // the parts in order (one per thread, a fixed reduction)
+    const bool mine = (int)threadIdx.x < bi.nparts;
+    const int pi = 2 * (bi.pbase + (mine ? (int)threadIdx.x : 0));
+    const double p1 = mine ? __longlong_as_double((long long)ld_agent(&a.br_part[pi])) : 0.0;
+    const double p2 = mine ? __longlong_as_double((long long)ld_agent(&a.br_part[pi + 1])) : 0.0;
+    S1 = block_sum_f64(p1, red);
+    S2 = block_sum_f64(p2, red);
+  }
+  if (threadIdx.x != 0) return;
+  double ss, k;
+  if (exact) {
+    ss = S1;
+    k = 0x1p-12;  // fp32 per-thread accumulation differs from the fold's grouping
+  } else {
+    const double Rd = (double)R, m = S1 / Rd;
+    const double var = fmax(0.0, (S2 - Rd * m * m) / (Rd - 1.0));
+    ss = S1 * ((double)n / (16.0 * Rd));
+    k = 6.0 * sqrt(var / Rd) / m + 0x1p-10;  // 6 sigma of the run-sum estimate + 0.1 %
+  }
+  SpecBracket o{0.f, 0.f, 0.f, 0.f, 1u, {0u, 0u, 0u}};
+  if (ss > 0.0 && ss < 1e300 && k < 0.5) {
+    const float n_lo = nextafterf((float)sqrt(ss * (1.0 - k)), 0.0f);
+    const float n_hi = nextafterf((float)sqrt(ss * (1.0 + k)), INFINITY);
+    if (n_lo >= 0x1p-90f && n_hi < INFINITY) {  // c_hi finite for L <= 2^30
+      const double L = (double)a.e.levels;
+      o.n_lo = n_lo;
+      o.n_hi = n_hi;
+      o.c_lo = nextafterf((float)(L / (double)n_hi * (1.0 - 0x1p-20)), 0.0f);
+      o.c_hi = nextafterf((float)(L / (double)n_lo * (1.0 + 0x1p-20)), INFINITY);
+      o.mode = 0u;
+    }
+  }
+  a.br[t] = o;
+}
+
+// Levels of a quad for every norm of the bracket; und: some element is undecided.  u == 0 is
+// raised to 2^-26 in the lower product only (x / n may underflow to 0 where |x| c does not:
+// such an element is left undecided); a decided level needs no clamp (ceil(dl) <= the exact
+// level <= L); NaN gives kl != kh.  scripts/exp/spec_check.c checks this exact form.
+__device__ __forceinline__ void spec_quad(float4 x, float4 u, float c_lo, float c_hi, int32_t (&q)[4], bool& und) {
+  const float xs[4] = {x.x, x.y, x.z, x.w}, us[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float ax = fabsf(xs[c]);
+    const float kl = ceilf(fmaf(ax, c_lo, -fmaxf(us[c], 0x1p-26f)));
+    const float kh = ceilf(fmaf(ax, c_hi, -us[c]));
+    und |= kl != kh;
+    q[c] = (int32_t)copysignf(kh, xs[c]);
+  }
+}
+
+template <int WIDTH>
+__device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t end, const int32_t (&qq)[4]) {
+  if (WIDTH == 1) {
+    int8_t* q8 = reinterpret_cast<int8_t*>(a.q);
+    if (e + 4 <= end) {
+      store_nt(reinterpret_cast<uint32_t*>(q8 + e), pack_i8x4(qq));
+    } else {
+      q8[e] = (int8_t)qq[0];
+      if (e + 1 < end) q8[e + 1] = (int8_t)qq[1];
+      if (e + 2 < end) q8[e + 2] = (int8_t)qq[2];
+    }
+  } else {
+    int32_t* q32 = reinterpret_cast<int32_t*>(a.q);
+    if (e + 4 <= end) {
+      store_nt(q32 + e, make_int4(qq[0], qq[1], qq[2], qq[3]));
+    } else {
+      q32[e] = qq[0];
+      if (e + 1 < end) q32[e + 1] = qq[1];
+      if (e + 2 < end) q32[e + 2] = qq[2];
+    }
+  }
+}
+
+template <int WIDTH>
+__global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a) {
+  const EncArgs& e = a.e;
+  const int64_t blk = blockIdx.x;
+  const Item it = e.items[blk >> 2];
+  const int64_t b = it.begin + (blk & 3) * kSpecBlk;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t* slot = a.slots + blk * kSpecSlot;
+  uint64_t* part = a.partials + blk * kWaves + wave;
+  if (b >= it.end) {  // past the tensor's end: an empty block still reports (stale values otherwise)
+    if (lane == 0) {
+      *part = 0ull;
+      slot[wave] = (uint32_t)it.tensor << 8;
+    }
+    return;
+  }
+  const int64_t end = min(b + kSpecBlk, it.end);
+  const bool full = end - b == kSpecBlk;
+  float4 v[kSpecV];
+  if (full) load_f4<kSpecV, true>(e.x, b, end, v);
+  else load_f4<kSpecV, false>(e.x, b, end, v);
+  scale_f4<kSpecV>(v, e);
+  const float acc = sumsq_f4<kSpecV>(v, 0.0f);
+  const SpecBracket br = a.br[it.tensor];
+  uint32_t cnt = 0;  // wave-uniform
+  if (br.mode == 0u) {
+    float4 uu[4];
+    philox_rows(e, b, a.begins[it.tensor], it.tensor, 0, uu);
+    uint32_t* list = slot + kWaves + kSpecPerWave * wave;
+#pragma unroll
+    for (int k = 0; k < kSpecV; ++k) {
+      const int64_t el = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+      const bool live = full || el < end;
+      int32_t qq[4];
+      bool und = false;
+      spec_quad(v[k], uu[k], br.c_lo, br.c_hi, qq, und);
+      if (live) {
+        if (full) store_quad<WIDTH>(e, el, el + 4, qq);
+        else store_quad<WIDTH>(e, el, end, qq);
+      }
+      const uint64_t m = __ballot(live && und);
+      if (m) {  // rare: list this wave's undecided quads
+        const uint32_t pos = cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        if (live && und && pos < (uint32_t)kSpecPerWave) list[pos] = (uint32_t)(el >> 2);
+        cnt += (uint32_t)__popcll(m);
+      }
+    }
+  }
+  const double s = wave_sum_f64((double)acc);
+  if (lane == 0) {
+    *part = (uint64_t)__double_as_longlong(s);
+    slot[wave] = ((uint32_t)it.tensor << 8) | min(cnt, (uint32_t)kSpecPerWave);
+    if (cnt > (uint32_t)kSpecPerWave)
+      __hip_atomic_fetch_or(&a.flags[it.tensor], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void qsgd_spec_fold(SpecArgs a) {
+  __shared__ double red[kWaves];
+  __shared__ uint32_t s_last;
+  const SpecFoldItem fi = a.fold_items[blockIdx.x];
+  const int32_t t = fi.tensor;
+  // up to kSpecSeg partials: 8 loads in flight per thread, a fixed order
+  constexpr int U = kSpecSeg / kThreads;
+  double v[U];
+#pragma unroll
+  for (int i = 0; i < U; ++i) {
+    const int64_t j = fi.p_begin + threadIdx.x + (int64_t)i * kThreads;
+    v[i] = j < fi.p_end ? __longlong_as_double((long long)a.partials[j]) : 0.0;
+  }
+  double p = 0.0;
+#pragma unroll
+  for (int i = 0; i < U; ++i) p += v[i];
+  double tot = block_sum_f64(p, red);
+  if (fi.nsegs > 1) {
+    if (threadIdx.x == 0) {
+      st_agent(&a.seg_part[fi.sbase + fi.seg], (uint64_t)__double_as_longlong(tot));
+      drain_vmem();
+      const uint32_t last = add_agent(&a.fold_cnt[t], 1u) == (uint32_t)(fi.nsegs - 1) ? 1u : 0u;
+      if (last) __hip_atomic_store(&a.fold_cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    double q = 0.0;
+    for (int j = threadIdx.x; j < fi.nsegs; j += kThreads)
+      q += __longlong_as_double((long long)ld_agent(&a.seg_part[fi.sbase + j]));
+    tot = block_sum_f64(q, red);
+  }
+  if (threadIdx.x != 0) return;
+  const float norm = finish_norm(tot, kFmtF32);
+  a.e.norm_out[t] = norm;
+  const SpecBracket br = a.br[t];
+  const uint32_t fl = a.flags[t];
+  const bool ok = br.mode == 0u && fl == 0u && norm >= br.n_lo && norm <= br.n_hi;
+  a.status[t] = ok ? 0u : 1u;
+  if (fl) a.flags[t] = 0u;
+  if (!ok) *a.any_whole = a.epoch;
+}
+
+// Uniforms of the quad at tensor-relative element rel (the Philox layout of philox_rows).
+__device__ __forceinline__ float4 spec_quad_uniforms(const EncArgs& a, int64_t rel, int32_t t) {
+  const uint64_t G = (uint64_t)(rel >> 12) * (uint64_t)kThreads + (uint64_t)((rel >> 2) & (kThreads - 1));
+  const int sl = (int)((rel >> 10) & 3);
+  uint32_t w[12];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const uint64_t ctr = 3 * G + c;
+    const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, a.offset),
+                                  a.seed_lo, a.seed_hi);
+    w[4 * c] = r.x; w[4 * c + 1] = r.y; w[4 * c + 2] = r.z; w[4 * c + 3] = r.w;
+  }
+  float4 u = u24x4(w[0], w[1], w[2]);
+#pragma unroll
+  for (int s = 1; s < 4; ++s)
+    if (s == sl) u = u24x4(w[3 * s], w[3 * s + 1], w[3 * s + 2]);
+  return u;
+}
+
+__device__ __forceinline__ float4 load_quad(const float* __restrict__ x, int64_t e, int64_t end) {
+  if (e + 4 <= end) return *reinterpret_cast<const float4*>(x + e);
+  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+  v.x = x[e];
+  if (e + 1 < end) v.y = x[e + 1];
+  if (e + 2 < end) v.z = x[e + 2];
+  return v;
+}
+
+template <int WIDTH>
+__global__ __launch_bounds__(kThreads) void qsgd_spec_fix(SpecArgs a) {
+  constexpr int BPW = kThreads / kWaves;  // blocks per workgroup (one thread per wave slot)
+  __shared__ uint32_t s_rep[BPW];
+  __shared__ uint32_t s_nrep;
+  const EncArgs& e = a.e;
+  const bool whole = *a.any_whole == a.epoch;  // uniform: some tensor is requantised whole
+  if (whole) {
+    if (threadIdx.x == 0) s_nrep = 0u;
+    __syncthreads();
+  }
+  const int64_t blk = (int64_t)blockIdx.x * BPW + (threadIdx.x >> 2);
+  const int w = threadIdx.x & 3;
+  if (blk < a.nblocks) {
+    const uint32_t* slot = a.slots + blk * kSpecSlot;
+    const uint32_t head = slot[w];
+    const int32_t t = (int32_t)(head >> 8);
+    const uint32_t cnt = head & 0xffu;
+    if (!whole || a.status[t] == 0u) {
+      if (cnt) {
+        const Item it = e.items[blk >> 2];
+        const int64_t b = it.begin + (blk & 3) * kSpecBlk;
+        {
+          const int64_t end = min(b + kSpecBlk, it.end), tb = a.begins[it.tensor];
+          int64_t el[kSpecPerWave];
+          float4 xv[kSpecPerWave];
+#pragma unroll
+          for (int j = 0; j < kSpecPerWave; ++j) {  // every load in flight before any arithmetic
+            el[j] = (uint32_t)j < cnt ? 4 * (int64_t)slot[kWaves + kSpecPerWave * w + j] : b;
+            xv[j] = (uint32_t)j < cnt ? load_quad(e.x, el[j], end) : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+          const Divisor dv(e.norm_out[it.tensor]);
+#pragma unroll
+          for (int j = 0; j < kSpecPerWave; ++j) {
+            if ((uint32_t)j >= cnt) break;
+            float4 x1[1] = {xv[j]};
+            scale_f4<1>(x1, e);
+            int32_t qq[4];
+            qsgd_quad<false>(x1[0], spec_quad_uniforms(e, el[j] - tb, it.tensor), dv, e.levels, false, qq);
+            store_quad<WIDTH>(e, el[j], end, qq);
+          }
+        }
+      }
+    } else if (w == 0) {
+      s_rep[atomicAdd(&s_nrep, 1u)] = (uint32_t)(threadIdx.x >> 2);
+    }
+  }
+  if (!whole) return;
+  __syncthreads();
+  const uint32_t nrep = s_nrep;
+  for (uint32_t r = 0; r < nrep; ++r) {  // whole blocks of requantised tensors, all 256 threads
+    const int64_t rb = (int64_t)blockIdx.x * BPW + s_rep[r];
+    const Item it = e.items[rb >> 2];
+    const int64_t b = it.begin + (rb & 3) * kSpecBlk;
+    if (b < it.end)
+      quant_sub<WIDTH, false, kSpecV>(e, b, min(b + kSpecBlk, it.end), a.begins[it.tensor], it.tensor,
+                                      e.norm_out[it.tensor]);
+  }
+}
+
 // Decode one sub-chunk [b, end): y = fl32(fl32(norm * q) / L) (optionally acc += y).
 template <int WIDTH, bool ACC, bool POW2, bool FULL, int V = kV>
 __device__ __forceinline__ void decode_sub(const DecArgs& a, int64_t b, int64_t end, float norm) {
@@ -483,7 +915,8 @@ struct omf_plan {
   std::vector<int64_t> sizes, offsets;
   int64_t arena_end = 0;
   int64_t cap = 0;               // tensors of <= cap items take the register-resident path
-  int32_t strategy = 2;          // 0 register-resident + two-pass, 1 ticket-ordered two-pass, 2 single-read ring (default by size: omf_plan_create)
+  int32_t strategy = 2;          // 0 register-resident + two-pass, 1 ticket-ordered two-pass, 2 single-read ring,
+                                 // 3 bracketed single-read (default by size: omf_plan_create)
   uint64_t wait_ticks = kWaitTicks;
   uint32_t epoch = 0;            // last granule tag used (host-side launch counter)
   int32_t ev = 8;                // encode rows per thread (sub-chunk = ev * 1024 elements): 8 measured
@@ -512,6 +945,20 @@ struct omf_plan {
   omf::ring::Tensor* d_ring_t = nullptr;
   uint64_t* d_ring_gran = nullptr;
   unsigned long long* d_ring_prof = nullptr;  // 16 phase counters (OMF_RING_DBG & 4)
+  // bracketed single-read encoder, strategy 3: per-tensor brackets / flags / status, per
+  // 4 Ki-element block partials and undecided-quad slots
+  int64_t n_spec_blocks = 0, n_spec_br = 0, n_spec_fold = 0;
+  SpecBrItem* d_spec_br_items = nullptr;
+  SpecFoldItem* d_spec_fold_items = nullptr;
+  uint64_t* d_spec_br_part = nullptr;
+  uint64_t* d_spec_seg_part = nullptr;
+  uint32_t* d_spec_cnt = nullptr;  // [br_cnt x nt][fold_cnt x nt][any_whole]
+  uint32_t spec_epoch = 0;
+  SpecBracket* d_spec_br = nullptr;
+  uint64_t* d_spec_part = nullptr;
+  uint32_t* d_spec_slots = nullptr;
+  uint32_t* d_spec_flags = nullptr;
+  uint32_t* d_spec_status = nullptr;
   // Launches that use the sync block / granules are ordered across streams: a launch on a
   // stream other than the previous one first waits for the previous launch's event.
   hipEvent_t last_ev = nullptr;
@@ -731,14 +1178,35 @@ static int upload_plan(omf_plan* p) {
   p->n_ring = (int64_t)rseq.size();
   // Flat items (decode, norm-supplied quantise, Top-K passes): one 16 Ki sub-chunk each,
   // the fastest decode granularity measured (profiles/r01_notes.md).
+  // Bracketed encoder tables: bracket parts (up to 4 per sampled tensor) and fold segments of
+  // kSpecSeg wave partials (4 per 4 Ki block, kSub / kSpecBlk = 4 blocks per flat item).
+  std::vector<SpecBrItem> br_items;
+  std::vector<SpecFoldItem> fold_items;
+  int32_t br_pbase = 0, seg_base = 0;
   for (int32_t t = 0; t < p->nt; ++t) {
     const int64_t n = p->sizes[t], b = p->offsets[t];
+    const int64_t p_begin = (int64_t)kWaves * 4 * (int64_t)flat.size();
     for (int64_t c = 0; c * kSub < n; ++c) {
       const int64_t cb = b + c * kSub;
       flat.push_back(Item{cb, std::min(b + n, cb + kSub), t, kQuant, (int32_t)c, 0});
     }
+    const int64_t p_end = (int64_t)kWaves * 4 * (int64_t)flat.size();
+    const int64_t R = std::max<int64_t>(1, std::min<int64_t>(kSpecRuns, n / 32));
+    const int32_t nparts = n <= kSpecExact ? 1 : (int32_t)((R + kSpecRunsPerPart - 1) / kSpecRunsPerPart);
+    for (int32_t q = 0; q < nparts; ++q)
+      br_items.push_back(SpecBrItem{n / R, (int32_t)R, (int32_t)(n % R), t, q, nparts, br_pbase});
+    br_pbase += nparts;
+    const int32_t nsegs = (int32_t)((p_end - p_begin + kSpecSeg - 1) / kSpecSeg);
+    for (int32_t q = 0; q < nsegs; ++q)
+      fold_items.push_back(SpecFoldItem{p_begin + (int64_t)q * kSpecSeg, std::min(p_end, p_begin + (int64_t)(q + 1) * kSpecSeg),
+                                        t, q, nsegs, seg_base});
+    seg_base += nsegs;
   }
-  if ((int64_t)std::max(seq[0].size(), flat.size()) > 0x7fffffffLL) return fail(OMF_EINVAL, "too many work items");
+  static_assert(kSub == 4 * kSpecBlk, "four spec blocks per flat item");
+  p->n_spec_blocks = 4 * (int64_t)flat.size();
+  p->n_spec_br = (int64_t)br_items.size();
+  p->n_spec_fold = (int64_t)fold_items.size();
+  if ((int64_t)std::max(seq[0].size(), 4 * flat.size()) > 0x7fffffffLL) return fail(OMF_EINVAL, "too many work items");
   p->n_enc[0] = (int64_t)seq[0].size();
   p->n_enc[1] = (int64_t)seq[1].size();
   p->n_flat = (int64_t)flat.size();
@@ -760,6 +1228,16 @@ static int upload_plan(omf_plan* p) {
   const size_t o_ring_t = o; o = round16(o + sizeof(omf::ring::Tensor) * rtens.size());
   const size_t o_ring_g = o; o = round16(o + 8 * (size_t)p->n_ring_gran);
   const size_t o_ring_p = o; o = round16(o + 8 * 16);
+  const size_t o_sp_bri = o; o = round16(o + sizeof(SpecBrItem) * br_items.size());
+  const size_t o_sp_foi = o; o = round16(o + sizeof(SpecFoldItem) * fold_items.size());
+  const size_t o_sp_brp = o; o = round16(o + 16 * br_items.size());
+  const size_t o_sp_segp = o; o = round16(o + 8 * fold_items.size());
+  const size_t o_sp_cnt = o; o = round16(o + 8 * (size_t)p->nt + 4);
+  const size_t o_sp_br = o; o = round16(o + sizeof(SpecBracket) * (size_t)p->nt);
+  const size_t o_sp_part = o; o = round16(o + 8 * (size_t)kWaves * (size_t)p->n_spec_blocks);
+  const size_t o_sp_slots = o; o = round16(o + 4 * (size_t)kSpecSlot * (size_t)p->n_spec_blocks);
+  const size_t o_sp_flags = o; o = round16(o + 4 * (size_t)p->nt);
+  const size_t o_sp_status = o; o = round16(o + 4 * (size_t)p->nt);
   DeviceGuard g(p->device);
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   if (p->d_block) {
@@ -782,6 +1260,21 @@ static int upload_plan(omf_plan* p) {
   p->d_ring_t = reinterpret_cast<omf::ring::Tensor*>(base + o_ring_t);
   p->d_ring_gran = reinterpret_cast<uint64_t*>(base + o_ring_g);
   p->d_ring_prof = reinterpret_cast<unsigned long long*>(base + o_ring_p);
+  p->d_spec_br_items = reinterpret_cast<SpecBrItem*>(base + o_sp_bri);
+  p->d_spec_fold_items = reinterpret_cast<SpecFoldItem*>(base + o_sp_foi);
+  p->d_spec_br_part = reinterpret_cast<uint64_t*>(base + o_sp_brp);
+  p->d_spec_seg_part = reinterpret_cast<uint64_t*>(base + o_sp_segp);
+  p->d_spec_cnt = reinterpret_cast<uint32_t*>(base + o_sp_cnt);
+  p->d_spec_br = reinterpret_cast<SpecBracket*>(base + o_sp_br);
+  p->d_spec_part = reinterpret_cast<uint64_t*>(base + o_sp_part);
+  p->d_spec_slots = reinterpret_cast<uint32_t*>(base + o_sp_slots);
+  p->d_spec_flags = reinterpret_cast<uint32_t*>(base + o_sp_flags);
+  p->d_spec_status = reinterpret_cast<uint32_t*>(base + o_sp_status);
+  OMF_HIP(hipMemcpy(p->d_spec_br_items, br_items.data(), sizeof(SpecBrItem) * br_items.size(), hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_spec_fold_items, fold_items.data(), sizeof(SpecFoldItem) * fold_items.size(),
+                    hipMemcpyHostToDevice));
+  OMF_HIP(hipMemset(p->d_spec_cnt, 0, 8 * (size_t)p->nt + 4));
+  OMF_HIP(hipMemset(p->d_spec_flags, 0, 4 * (size_t)p->nt));
   OMF_HIP(hipMemset(p->d_ring_prof, 0, 8 * 16));
   OMF_HIP(hipMemcpy(p->d_enc[0], seq[0].data(), sizeof(Item) * seq[0].size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_enc[1], seq[1].data(), sizeof(Item) * seq[1].size(), hipMemcpyHostToDevice));
@@ -805,6 +1298,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
   if (!out) return fail(OMF_EINVAL, "omf_plan_create: out is NULL");
   *out = nullptr;
   if (ntensors <= 0 || !sizes || !offsets) return fail(OMF_EINVAL, "omf_plan_create: need >= 1 tensor");
+  if (ntensors >= (1 << 24)) return fail(OMF_EINVAL, "omf_plan_create: at most 2^24 - 1 tensors");
   if (chunk_elems == 0) chunk_elems = 2 * kSub;  // two-pass encode items: 128 KiB of fp32 (32 Ki: 0.579 vs
                                                  // 0.595 ms at 64 Ki on Llama-400M, scripts/exp/ab_chunk.py)
   if (chunk_elems < kSub || chunk_elems % kSub != 0)
@@ -861,7 +1355,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     // Infinity Cache and beats the ring on Llama-400M (401 M elements: 0.604 vs 0.624 ms);
     // the ring wins below (Llama-150M 0.349 vs 0.359, ResNet-18 0.033 vs 0.058 ms).
     p->strategy = p->arena_end >= ((int64_t)1 << 28) ? 1 : 2;
-    if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 2));
+    if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 3));
     p->ring_grid = omf::ring::grid_size(p->ring_cfg, device);
     if (p->ring_grid <= 0) {
       delete p;
@@ -888,6 +1382,7 @@ int omf_plan_destroy(omf_plan* plan) {
 
 int64_t omf_plan_encode_items(const omf_plan* plan) {
   if (!plan) return -1;
+  if (plan->strategy == 3) return plan->n_spec_blocks;
   return plan->strategy == 2 ? plan->n_ring : plan->n_enc[plan->strategy];
 }
 
@@ -895,8 +1390,8 @@ int32_t omf_plan_encode_strategy(const omf_plan* plan) { return plan ? plan->str
 
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
-  if (strategy < 0 || strategy > 2)
-    return fail(OMF_EINVAL, "strategy must be 0 (resident), 1 (two-pass) or 2 (single-read ring)");
+  if (strategy < 0 || strategy > 3)
+    return fail(OMF_EINVAL, "strategy must be 0 (resident), 1 (two-pass), 2 (single-read ring) or 3 (bracketed single-read)");
   plan->strategy = strategy;
   return OMF_OK;
 }
@@ -947,6 +1442,33 @@ int omf_plan_set_resident_capacity(omf_plan* plan, int64_t cap, int64_t wait_us)
   if (cap > 0) plan->cap = cap;
   plan->wait_ticks = wait_us > 0 ? (uint64_t)wait_us * 100ull : kWaitTicks;
   if (cap > 0) return upload_plan(plan);
+  return OMF_OK;
+}
+
+int omf_plan_spec_stats(omf_plan* plan, void* stream, int64_t* out4) {
+  if (!plan || !out4) return fail(OMF_EINVAL, "omf_plan_spec_stats: NULL argument");
+  DeviceGuard g(plan->device);
+  OMF_HIP(hipStreamSynchronize((hipStream_t)stream));
+  std::vector<uint32_t> status(plan->nt), slots((size_t)kSpecSlot * (size_t)plan->n_spec_blocks);
+  std::vector<SpecBracket> br(plan->nt);
+  OMF_HIP(hipMemcpy(status.data(), plan->d_spec_status, 4 * (size_t)plan->nt, hipMemcpyDeviceToHost));
+  OMF_HIP(hipMemcpy(br.data(), plan->d_spec_br, sizeof(SpecBracket) * (size_t)plan->nt, hipMemcpyDeviceToHost));
+  OMF_HIP(hipMemcpy(slots.data(), plan->d_spec_slots, 4 * slots.size(), hipMemcpyDeviceToHost));
+  int64_t whole = 0, deferred = 0, listed = 0, full = 0;
+  for (int32_t t = 0; t < plan->nt; ++t) {
+    whole += status[t] != 0u;
+    deferred += br[t].mode != 0u;
+  }
+  for (int64_t blk = 0; blk < plan->n_spec_blocks; ++blk)
+    for (int w = 0; w < kWaves; ++w) {
+      const uint32_t c = slots[(size_t)blk * kSpecSlot + w] & 0xffu;
+      listed += c;
+      full += c == (uint32_t)kSpecPerWave;
+    }
+  out4[0] = whole;
+  out4[1] = deferred;
+  out4[2] = listed;
+  out4[3] = full;
   return OMF_OK;
 }
 
@@ -1057,9 +1579,44 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }
+  // Bracketed single-read encoder: fp32 values with on-device draws (other formats and
+  // caller uniforms take the two-pass encoder).  Four launches, no host interaction.
+  if (p->strategy == 3 && !norm_only && !u && fmt == 0 && s >= kSpecMinBits && s <= kSpecMaxBits) {
+    SpecArgs sa;
+    a.items = p->d_flat;
+    a.tinfo = p->d_tinfo[1];
+    sa.e = a;
+    sa.begins = p->d_begins;
+    sa.sizes = p->d_sizes;
+    sa.br_items = p->d_spec_br_items;
+    sa.fold_items = p->d_spec_fold_items;
+    sa.br_part = p->d_spec_br_part;
+    sa.seg_part = p->d_spec_seg_part;
+    sa.br_cnt = p->d_spec_cnt;
+    sa.fold_cnt = p->d_spec_cnt + p->nt;
+    sa.any_whole = p->d_spec_cnt + 2 * p->nt;
+    if (++p->spec_epoch == 0) ++p->spec_epoch;
+    sa.epoch = p->spec_epoch;
+    sa.br = p->d_spec_br;
+    sa.partials = p->d_spec_part;
+    sa.slots = p->d_spec_slots;
+    sa.flags = p->d_spec_flags;
+    sa.status = p->d_spec_status;
+    sa.nblocks = p->n_spec_blocks;
+    const dim3 gbr((unsigned)p->n_spec_br), gfo((unsigned)p->n_spec_fold), gb((unsigned)p->n_spec_blocks),
+        gf((unsigned)((p->n_spec_blocks + kThreads / kWaves - 1) / (kThreads / kWaves)));
+    hipLaunchKernelGGL(qsgd_spec_bracket, gbr, blk, 0, st, sa);
+    if (width == 1) hipLaunchKernelGGL(qsgd_spec_quant<1>, gb, blk, 0, st, sa);
+    else hipLaunchKernelGGL(qsgd_spec_quant<4>, gb, blk, 0, st, sa);
+    hipLaunchKernelGGL(qsgd_spec_fold, gfo, blk, 0, st, sa);
+    if (width == 1) hipLaunchKernelGGL(qsgd_spec_fix<1>, gf, blk, 0, st, sa);
+    else hipLaunchKernelGGL(qsgd_spec_fix<4>, gf, blk, 0, st, sa);
+    OMF_HIP(hipGetLastError());
+    return OMF_OK;
+  }
   // No per-call memset: tickets and arrival counters are reset in-kernel by their last
   // user, and granules carry this launch's epoch.
-  const int strat = p->strategy == 2 ? 1 : p->strategy;  // norms-only passes use the two-pass tables
+  const int strat = p->strategy >= 2 ? 1 : p->strategy;  // norms-only passes use the two-pass tables
   if (++p->epoch == 0) ++p->epoch;
   a.epoch = p->epoch;
   a.n_items = (uint32_t)p->n_enc[strat];

@@ -48,3 +48,6 @@ for rnd in range(6):
 for sn in strats:
     v = sorted(res[sn])
     print(f"{MODEL} {sn:8s}: median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f}", flush=True)
+if "bracket" in plans:
+    plans["bracket"].qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1, offset=99)
+    print(f"{MODEL} bracket stats: {plans['bracket'].spec_stats()}", flush=True)

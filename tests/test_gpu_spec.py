@@ -1,0 +1,164 @@
+"""Bracketed single-read encoder (strategy 3, omf_qsgd.hip qsgd_spec_*) against the oracle.
+
+Every payload is compared bit for bit with the oracle's QSGD quantiser given the encoder's own
+norm (checked against fp64 at NORM_RTOL) and the Philox uniforms of oracle/philox.py — the bar
+of every other strategy.  The inputs exercise each path of the encoder: levels decided for the
+whole bracket, undecided quads fixed exactly, tensors whose norm falls outside the sampled
+bracket (a few huge elements the sample misses), slot overflows (heavy tails), deferred tensors
+(all zero, single non-zero, sub-normal scale) and non-finite tensors.
+"""
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from inputs import exact_input
+from omnifed_amd import codec, shapes
+
+pytestmark = pytest.mark.gpu
+
+NORM_RTOL = 2e-6
+
+
+def _check_against_oracle(plan, x_host, q, norms, s, seed, offset, alpha=1.0, finite=True):
+    qh, nh = q.cpu().numpy(), norms.cpu().numpy()
+    for t, (o, n) in enumerate(zip(plan.offsets, plan.sizes)):
+        p = x_host[o:o + n]
+        if alpha != 1.0:
+            p = (torch.from_numpy(p) * np.float32(alpha)).numpy()
+        if finite:
+            ref = float(np.sqrt(np.sum(p.astype(np.float64) ** 2)))
+            if ref > 1e-18:  # smaller: fp32 squares underflow (every strategy's norm does)
+                assert nh[t] == pytest.approx(ref, rel=NORM_RTOL), (t, n)
+        if nh[t] == 0:  # zero norm: all-zero payload (the Python layer sends the tensor dense)
+            assert not qh[o:o + n].any(), (t, n)
+            continue
+        u = oracle.philox_uniforms(seed, offset, t, n)
+        want, *_ = oracle.qsgd_quantize(torch.from_numpy(np.ascontiguousarray(p)), s, norm=float(nh[t]),
+                                        u=torch.from_numpy(u))
+        assert qh[o:o + n].tobytes() == want.numpy().tobytes(), (t, n, s)
+
+
+def _bracket_plan(gpu, sizes):
+    plan = codec.Plan(sizes, device=gpu)
+    plan.set_encode_strategy("bracket")
+    return plan
+
+
+@pytest.mark.parametrize("s", [1, 3, 4, 8])
+def test_bracket_mixed_sizes(gpu, s):
+    sizes = [1, 7, 1000, 4096, 4097, 16384, 16385, 40000, 65536, 65537, 100003, 262149, 1 << 20, 3 << 20]
+    plan = _bracket_plan(gpu, sizes)
+    x = np.zeros(plan.arena_end, np.float32)
+    for i, (o, n) in enumerate(zip(plan.offsets, sizes)):
+        x[o:o + n] = exact_input(100 + i, n, -9)
+    xd = torch.from_numpy(x).to(gpu)
+    q, norms = plan.qsgd_encode(xd, s, seed=21, offset=3)
+    assert plan.check()
+    if s <= 4:  # bracketed path (wider payloads take the two-pass encoder)
+        st = plan.spec_stats()
+        # at most the mid-size tensors (a wide sampled bracket) can overflow a slot and be redone
+        assert st["deferred"] == 0 and st["whole"] <= sum(16384 < n < 300000 for n in sizes), st
+        assert s > 1 or st["whole"] == 0, st
+    _check_against_oracle(plan, x, q, norms, s, 21, 3)
+    # deterministic, and the payload does not depend on what the buffer held before
+    q2 = torch.full_like(q, 0x55)
+    q2, n2 = plan.qsgd_encode(xd, s, q_out=q2, seed=21, offset=3)
+    assert torch.equal(n2, norms)
+    for o, n in zip(plan.offsets, plan.sizes):  # the gaps between tensors are padding, never written
+        assert torch.equal(q2[o:o + n], q[o:o + n])
+
+
+def test_bracket_weighted(gpu):
+    sizes = [5000, 300000, 1 << 20]
+    plan = _bracket_plan(gpu, sizes)
+    g = torch.Generator().manual_seed(4)
+    x = (torch.randn(plan.arena_end, generator=g) * 1e-3).numpy()
+    q, norms = plan.qsgd_encode(torch.from_numpy(x).to(gpu), 4, alpha=3.0, seed=8)
+    _check_against_oracle(plan, x, q, norms, 4, 8, 0, alpha=3.0)
+
+
+def test_bracket_adversarial_distributions(gpu):
+    """Inputs whose sampled bracket misses the norm or overflows the slots: exact anyway."""
+    n = 1 << 20
+    rng = np.random.default_rng(7)
+    cases = []
+    spikes = rng.standard_normal(n).astype(np.float32) * 1e-3
+    spikes[rng.choice(n, 3, replace=False)] = 50.0           # norm dominated by 3 unsampled elements
+    cases.append(spikes)
+    cases.append(rng.standard_cauchy(n).astype(np.float32))  # heavy tails: wide bracket
+    sparse = np.zeros(n, np.float32)
+    sparse[rng.choice(n, 500, replace=False)] = rng.standard_normal(500).astype(np.float32)
+    cases.append(sparse)                                        # 0.05 % non-zero
+    cases.append(np.full(n, 0.125, np.float32))                 # every element the same level point
+    cases.append(np.zeros(n, np.float32))                       # deferred: zero norm
+    one = np.zeros(n, np.float32)
+    one[n // 3] = -2.5
+    cases.append(one)                                           # single non-zero
+    cases.append((rng.standard_normal(n) * 1e-41).astype(np.float32))  # sub-normal scale
+    cases.append((rng.standard_normal(n) * 1e15).astype(np.float32))   # large scale
+    ramp = np.linspace(-1, 1, n, dtype=np.float32)
+    cases.append(ramp)                                          # smooth structure (strata alias)
+    sizes = [c.size for c in cases]
+    plan = _bracket_plan(gpu, sizes)
+    x = np.zeros(plan.arena_end, np.float32)
+    for o, c in zip(plan.offsets, cases):
+        x[o:o + c.size] = c
+    for s in (2, 4, 8):
+        q, norms = plan.qsgd_encode(torch.from_numpy(x).to(gpu), s, seed=s, offset=1)
+        assert plan.check()
+        if s <= 4:
+            st = plan.spec_stats()
+            # the spiked, zero and single-element tensors cannot keep their sampled bracket
+            assert st["whole"] >= 3 and st["deferred"] >= 2, st
+        _check_against_oracle(plan, x, q, norms, s, s, 1)
+
+
+def test_bracket_non_finite_matches_two_pass(gpu):
+    """NaN / inf tensors (norm NaN / inf): the same payload as the two-pass encoder."""
+    n = 70000
+    a = np.linspace(-1, 1, n, dtype=np.float32)
+    b = a.copy()
+    b[123] = np.nan
+    c = a.copy()
+    c[4567] = np.inf
+    plan = _bracket_plan(gpu, [n, n, n])
+    x = np.zeros(plan.arena_end, np.float32)
+    for o, v in zip(plan.offsets, (a, b, c)):
+        x[o:o + n] = v
+    xd = torch.from_numpy(x).to(gpu)
+    q3, n3 = plan.qsgd_encode(xd, 4, seed=2)
+    plan.set_encode_strategy("ordered")
+    q1, n1 = plan.qsgd_encode(xd, 4, seed=2)
+    torch.testing.assert_close(n3[:1], n1[:1], rtol=2e-6, atol=0)
+    assert torch.isnan(n3[1]) and torch.isinf(n3[2]) and torch.isnan(n1[1]) and torch.isinf(n1[2])
+    for o in plan.offsets[1:]:
+        assert torch.equal(q3[o:o + n], q1[o:o + n])
+
+
+def test_bracket_resnet18_full_arena(gpu):
+    """Every tensor of the ResNet-18 update (BASELINE config 1) at s = 3, 4 and 8."""
+    sizes = [shapes.numel(sh) for _, sh in shapes.resnet18()]
+    plan = _bracket_plan(gpu, sizes)
+    g = torch.Generator().manual_seed(18)
+    x = (torch.randn(plan.arena_end, generator=g) * 1e-3).numpy()
+    xd = torch.from_numpy(x).to(gpu)
+    for s in (3, 4, 8):
+        q, norms = plan.qsgd_encode(xd, s, seed=77, offset=s)
+        if s <= 4:
+            assert plan.spec_stats()["listed"] > 0
+        _check_against_oracle(plan, x, q, norms, s, 77, s)
+
+
+def test_bracket_large_tensors_sampled(gpu):
+    """Llama-sized tensors (16 Mi and 2^25 + 13 elements): whole-tensor parity."""
+    sizes = [1 << 24, (1 << 25) + 13, 4096]
+    plan = _bracket_plan(gpu, sizes)
+    g = torch.Generator(device=gpu).manual_seed(3)
+    xd = torch.randn(plan.arena_end, device=gpu, generator=g) * 2e-3
+    q, norms = plan.qsgd_encode(xd, 4, seed=5, offset=9)
+    st = plan.spec_stats()
+    assert st["whole"] == 0 and st["listed"] > 0, st
+    x = xd.cpu().numpy()
+    _check_against_oracle(plan, x, q, norms, 4, 5, 9)
