@@ -90,9 +90,10 @@ int omf_plan_check(omf_plan* plan, void* stream);
  * few undecided quads.  Identical payloads given the norm; the norms fold
  * partials over different chunk sizes, so strategies agree to rounding. */
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy);
-/* The plan's encode strategy (0/1/2 as above).  A new plan picks 1 (two-pass, whose second
- * read is served by the Infinity Cache) for arenas of >= 2^28 elements and 2 (the ring)
- * below: the measured crossover; OMF_ENCODE_STRATEGY overrides. */
+/* The plan's encode strategy (0-3 as above).  A new plan picks 3 (bracketed single-read) for
+ * arenas of >= 2^25 elements and 2 (the ring) below: the measured crossover;
+ * OMF_ENCODE_STRATEGY overrides.  Strategy 3 serves fp32 values with on-device draws at
+ * bit_width 1-4; other encodes of such a plan take the two-pass encoder (1). */
 int32_t omf_plan_encode_strategy(const omf_plan* plan);
 /* Diagnostics of the last bracketed single-read encode (strategy 3; synchronises `stream`,
  * not for the hot path): out[0] tensors requantised whole (norm outside the sampled bracket,

@@ -402,11 +402,11 @@ __global__ __launch_bounds__(kThreads) void qsgd_quant_sub(EncArgs a) {
 // Payload bits equal every other strategy's for the same norm.
 constexpr int kSpecV = 4;                                    // float4 rows per thread
 constexpr int64_t kSpecBlk = (int64_t)kSpecV * kThreads * 4;  // 4096 elements per block
-constexpr int kSpecSlot = 32;                                 // words per block: 4 wave counts + 4 x 7 quads
+constexpr int kSpecSlot = 32;                                 // words per block: 4 waves x 7 quads (+ 4 spare)
 constexpr int kSpecPerWave = 7;                               // listed quads per wave
 constexpr int64_t kSpecExact = 16384;                         // tensors read whole by the bracket
-constexpr int kSpecRuns = 2048;                               // sampled 16-element runs otherwise (at most)
-constexpr int kSpecRunsPerPart = 512;                         // runs per bracket workgroup (2 per thread)
+constexpr int kSpecRun = 64;                                  // elements per sampled run (256 B: DRAM-friendly)
+constexpr int kSpecRuns = 512;                                // sampled runs per larger tensor (at most)
 constexpr int kSpecSeg = 2048;                                // wave partials per fold workgroup
 // Widest level count the bracket serves: the undecided fraction grows with L (a level step is
 // norm / L wide), and at L = 32 a 1 Mi-element tensor's sampled bracket already leaves ~1.3
@@ -423,9 +423,10 @@ struct SpecBracket {
 // Bracket work item: part `part` of `nparts` of tensor `tensor` (a sampled tensor's runs are
 // split over up to 4 workgroups; a small tensor is one exact part).
 struct SpecBrItem {
-  int64_t base;  // stratum length n / R (R = runs of the tensor); rem = n % R strata are one longer
+  int64_t begin, n;  // the tensor's arena range
+  int64_t base;      // stratum length n / R (R = runs of the tensor); rem = n % R strata are one longer
   int32_t R, rem;
-  int32_t tensor, part, nparts, pbase;
+  int32_t tensor, pad;
 };
 // Fold work item: wave partials [p_begin, p_end) of tensor `tensor`, segment `seg` of `nsegs`.
 struct SpecFoldItem {
@@ -440,12 +441,12 @@ struct SpecArgs {
   const SpecBrItem* br_items;
   const SpecFoldItem* fold_items;
   SpecBracket* br;
-  uint64_t* br_part;       // per bracket item: {S1, S2} fp64 bits
   uint64_t* seg_part;      // per fold item: fp64 bits
-  uint32_t* br_cnt;        // per tensor arrival counters (reset by the last arriver)
-  uint32_t* fold_cnt;
+  uint32_t* fold_cnt;      // per tensor arrival counters of the fold segments (reset by the last arriver)
   uint64_t* partials;      // fp64 bits, one per wave (kWaves per block)
-  uint32_t* slots;         // kSpecSlot words per block; word w < kWaves: (tensor << 8) | count of wave w
+  uint32_t* heads;         // per wave (dense, kWaves per block): (tensor << 8) | count of listed quads
+  uint32_t* slots;         // kSpecSlot words per block: kSpecPerWave quad indices per wave
+  float4* recs;            // per listed quad: its scaled x and its uniforms (2 float4), kWaves x kSpecPerWave per block
   uint32_t* flags;         // per tensor: a wave's slot overflowed (set by quant, cleared by fold)
   uint32_t* status;        // per tensor: 0 = listed quads only, 1 = requantise whole
   uint32_t* any_whole;     // = epoch when some tensor of this launch is requantised whole
@@ -472,32 +473,52 @@ __device__ __forceinline__ float sq4(float4 v, float s) {
   s = fmaf(v.z, v.z, s); return fmaf(v.w, v.w, s);
 }
 
-__global__ __launch_bounds__(kThreads) void qsgd_spec_bracket(SpecArgs a) {
-  __shared__ double red[kWaves];
-  __shared__ uint32_t s_last;
-  const SpecBrItem bi = a.br_items[blockIdx.x];
+constexpr int kBrThreads = 1024;  // one bracket workgroup per tensor
+constexpr int kBrWaves = kBrThreads / 64;
+
+// Deterministic sum over a 1024-thread workgroup (wave butterflies, then the waves in order).
+__device__ __forceinline__ double br_sum(double v, double* lds) {
+  v = wave_sum_f64(v);
+  if ((threadIdx.x & 63) == 0) lds[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int w = 0; w < kBrWaves; ++w) s += lds[w];
+  __syncthreads();
+  return s;
+}
+
+__global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, const SpecBrItem* __restrict__ items) {
+  __shared__ double red[kBrWaves];
+  const SpecBrItem bi = items[blockIdx.x];  // one scalar load: the tensor's range and strata
   const int32_t t = bi.tensor;
-  const int64_t tb = a.begins[t], n = a.sizes[t];
+  const int64_t tb = bi.begin, n = bi.n;
   const float* __restrict__ x = a.e.x + tb;
   const float alpha = a.e.alpha;
   double s1 = 0.0, s2 = 0.0;
   const bool exact = n <= kSpecExact;
-  // runs of 16 elements: one at a hashed position inside each of R balanced strata (strata of
-  // >= 32 elements); this part takes runs [part * 512, part * 512 + 512)
   const int64_t R = bi.R;
-  if (exact) {  // 16 float4 per thread, all loads in flight
-    constexpr int PER = (int)(kSpecExact / (4 * kThreads));
+  // Loads are unconditional (a clamped address, the value masked after): a load under a
+  // branch is waited for at the branch's end, which would serialise the round trips.
+  if (exact) {  // 4 float4 per thread, all loads in flight
+    constexpr int PER = (int)(kSpecExact / (4 * kBrThreads));
     float4 v[PER];
+    const int64_t nq = n & ~(int64_t)3;  // whole quads
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int64_t e = 4 * ((int64_t)i * kThreads + threadIdx.x);
-      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (e + 4 <= n) {
-        v[i] = *reinterpret_cast<const float4*>(x + e);
-      } else if (e < n) {
-        v[i].x = x[e];
-        if (e + 1 < n) v[i].y = x[e + 1];
-        if (e + 2 < n) v[i].z = x[e + 2];
+      const int64_t e = 4 * ((int64_t)i * kBrThreads + threadIdx.x);
+      v[i] = nq ? *reinterpret_cast<const float4*>(x + (e < nq ? e : 0)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int64_t e = 4 * ((int64_t)i * kBrThreads + threadIdx.x);
+      if (e >= nq) {
+        v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < n) {  // the tensor's partial last quad (one thread)
+          v[i].x = x[e];
+          if (e + 1 < n) v[i].y = x[e + 1];
+          if (e + 2 < n) v[i].z = x[e + 2];
+        }
       }
     }
     float acc = 0.0f;
@@ -505,58 +526,36 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_bracket(SpecArgs a) {
     for (int i = 0; i < PER; ++i) acc = sq4(scale_alpha(v[i], alpha), acc);
     s1 = acc;
   } else {
-    constexpr int PER = kSpecRunsPerPart / kThreads;
+    // runs of 64 elements at a hashed position inside each of R <= 512 balanced strata (of
+    // >= 128 elements); a run is 16 float4 loaded by 16 consecutive lanes, 64 runs per pass
+    constexpr int LPR = kSpecRun / 4, RPP = kBrThreads / LPR, PASSES = kSpecRuns / RPP;
     const int64_t base = bi.base, rem = bi.rem;
-    float4 v[PER][4];
-    bool live[PER];
+    const int j = threadIdx.x & (LPR - 1);
+    float4 v[PASSES];
+    bool live[PASSES];
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      const int64_t r = (int64_t)bi.part * kSpecRunsPerPart + threadIdx.x + (int64_t)i * kThreads;
-      live[i] = r < R;
-      if (live[i]) {
-        const int64_t lo = r * base + min(r, rem), len = base + (r < rem ? 1 : 0);
-        const int64_t pos = (lo + (int64_t)(spec_hash((uint32_t)r, (uint32_t)t) % (uint32_t)(len - 15))) & ~(int64_t)3;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[i][j] = *reinterpret_cast<const float4*>(x + pos + 4 * j);
-      }
+    for (int i = 0; i < PASSES; ++i) {
+      const int64_t r0 = (int64_t)i * RPP + (threadIdx.x / LPR);
+      live[i] = r0 < R;
+      const int64_t r = live[i] ? r0 : 0;  // a dead lane re-reads run 0 (masked below)
+      const int64_t lo = r * base + min(r, rem), len = base + (r < rem ? 1 : 0);
+      const int64_t pos = (lo + (int64_t)(spec_hash((uint32_t)r, (uint32_t)t) % (uint32_t)(len - (kSpecRun - 1)))) &
+                          ~(int64_t)3;
+      v[i] = *reinterpret_cast<const float4*>(x + pos + 4 * j);
     }
 #pragma unroll
-    for (int i = 0; i < PER; ++i) {
-      if (live[i]) {
-        float sr = 0.0f;
+    for (int i = 0; i < PASSES; ++i) {
+      float sr = live[i] ? sq4(scale_alpha(v[i], alpha), 0.0f) : 0.0f;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) sr = sq4(scale_alpha(v[i][j], alpha), sr);
+      for (int o = LPR / 2; o > 0; o >>= 1) sr += __shfl_xor(sr, o, LPR);  // the run's sum in every lane
+      if (live[i] && j == 0) {
         s1 += (double)sr;
         s2 += (double)sr * (double)sr;
       }
     }
   }
-  const double S1p = block_sum_f64(s1, red);
-  const double S2p = block_sum_f64(s2, red);
-  // publish this part; the last arriver of the tensor folds the parts in order (cdna_hip_
-  // programming.md §6 G16: sc1 stores drained before the agent-scope counter add)
-  if (threadIdx.x == 0) {
-    uint32_t last = 1u;
-    if (bi.nparts > 1) {
-      st_agent(&a.br_part[2 * (bi.pbase + bi.part)], (uint64_t)__double_as_longlong(S1p));
-      st_agent(&a.br_part[2 * (bi.pbase + bi.part) + 1], (uint64_t)__double_as_longlong(S2p));
-      drain_vmem();
-      last = add_agent(&a.br_cnt[t], 1u) == (uint32_t)(bi.nparts - 1) ? 1u : 0u;
-      if (last) __hip_atomic_store(&a.br_cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_last = last;
-  }
-  __syncthreads();
-  if (!s_last) return;
-  double S1 = S1p, S2 = S2p;
-  if (bi.nparts > 1) {  // the parts in order (one per thread, a fixed reduction)
-    const bool mine = (int)threadIdx.x < bi.nparts;
-    const int pi = 2 * (bi.pbase + (mine ? (int)threadIdx.x : 0));
-    const double p1 = mine ? __longlong_as_double((long long)ld_agent(&a.br_part[pi])) : 0.0;
-    const double p2 = mine ? __longlong_as_double((long long)ld_agent(&a.br_part[pi + 1])) : 0.0;
-    S1 = block_sum_f64(p1, red);
-    S2 = block_sum_f64(p2, red);
-  }
+  const double S1 = br_sum(s1, red);
+  const double S2 = br_sum(s2, red);
   if (threadIdx.x != 0) return;
   double ss, k;
   if (exact) {
@@ -565,10 +564,10 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_bracket(SpecArgs a) {
   } else {
     const double Rd = (double)R, m = S1 / Rd;
     const double var = fmax(0.0, (S2 - Rd * m * m) / (Rd - 1.0));
-    ss = S1 * ((double)n / (16.0 * Rd));
+    ss = S1 * ((double)n / ((double)kSpecRun * Rd));
     k = 6.0 * sqrt(var / Rd) / m + 0x1p-10;  // 6 sigma of the run-sum estimate + 0.1 %
   }
-  SpecBracket o{0.f, 0.f, 0.f, 0.f, 1u, {0u, 0u, 0u}};
+  SpecBracket o{0.f, 0.f, 0.f, 0.f, 1u, {0u, 0u, 0u}};  // deferred: c = 0 decides every level as 0
   if (ss > 0.0 && ss < 1e300 && k < 0.5) {
     const float n_lo = nextafterf((float)sqrt(ss * (1.0 - k)), 0.0f);
     const float n_hi = nextafterf((float)sqrt(ss * (1.0 + k)), INFINITY);
@@ -623,50 +622,50 @@ __device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t 
   }
 }
 
-template <int WIDTH>
-__global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a) {
+// One block's pass: loads issued first, the Philox draws (independent of x) computed while
+// they are in flight, then the partial, the levels and the undecided list.  FULL: a whole
+// 4 Ki block (straight-line code, no bounds checks).
+template <int WIDTH, bool FULL>
+__device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t end, int32_t t, int64_t tb,
+                                           const SpecBracket& br, uint32_t* slot, uint64_t* part) {
   const EncArgs& e = a.e;
-  const int64_t blk = blockIdx.x;
-  const Item it = e.items[blk >> 2];
-  const int64_t b = it.begin + (blk & 3) * kSpecBlk;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t* slot = a.slots + blk * kSpecSlot;
-  uint64_t* part = a.partials + blk * kWaves + wave;
-  if (b >= it.end) {  // past the tensor's end: an empty block still reports (stale values otherwise)
-    if (lane == 0) {
-      *part = 0ull;
-      slot[wave] = (uint32_t)it.tensor << 8;
-    }
-    return;
-  }
-  const int64_t end = min(b + kSpecBlk, it.end);
-  const bool full = end - b == kSpecBlk;
   float4 v[kSpecV];
-  if (full) load_f4<kSpecV, true>(e.x, b, end, v);
-  else load_f4<kSpecV, false>(e.x, b, end, v);
-  scale_f4<kSpecV>(v, e);
-  const float acc = sumsq_f4<kSpecV>(v, 0.0f);
-  const SpecBracket br = a.br[it.tensor];
+  load_f4<kSpecV, FULL>(e.x, b, end, v);
+  float4 uu[4];
+  philox_rows(e, b, tb, t, 0, uu);
+  // Branch-free from the loads to the stores, so that the scheduler can place the Philox
+  // arithmetic under the load latency: x * alpha unconditionally (x * 1 = x; fp32 only, the
+  // product is not rounded further), and levels computed for a deferred tensor too (its
+  // multipliers are 0: every level 0, none undecided; the fix pass requantises it).
+  const float alpha = e.alpha;
+  float acc = 0.0f;
+#pragma unroll
+  for (int k = 0; k < kSpecV; ++k) {
+    v[k].x = __fmul_rn(v[k].x, alpha); v[k].y = __fmul_rn(v[k].y, alpha);
+    v[k].z = __fmul_rn(v[k].z, alpha); v[k].w = __fmul_rn(v[k].w, alpha);
+    acc = sq4(v[k], acc);
+  }
   uint32_t cnt = 0;  // wave-uniform
-  if (br.mode == 0u) {
-    float4 uu[4];
-    philox_rows(e, b, a.begins[it.tensor], it.tensor, 0, uu);
-    uint32_t* list = slot + kWaves + kSpecPerWave * wave;
+  {
+    uint32_t* list = slot + kSpecPerWave * wave;
 #pragma unroll
     for (int k = 0; k < kSpecV; ++k) {
       const int64_t el = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
-      const bool live = full || el < end;
+      const bool live = FULL || el < end;
       int32_t qq[4];
       bool und = false;
       spec_quad(v[k], uu[k], br.c_lo, br.c_hi, qq, und);
-      if (live) {
-        if (full) store_quad<WIDTH>(e, el, el + 4, qq);
-        else store_quad<WIDTH>(e, el, end, qq);
-      }
+      if (live) store_quad<WIDTH>(e, el, FULL ? el + 4 : end, qq);
       const uint64_t m = __ballot(live && und);
       if (m) {  // rare: list this wave's undecided quads
         const uint32_t pos = cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (live && und && pos < (uint32_t)kSpecPerWave) list[pos] = (uint32_t)(el >> 2);
+        if (live && und && pos < (uint32_t)kSpecPerWave) {  // the quad, its x and its draws: no re-read
+          list[pos] = (uint32_t)(el >> 2);
+          float4* rec = a.recs + 2 * ((blockIdx.x * kWaves + wave) * kSpecPerWave + pos);
+          rec[0] = v[k];
+          rec[1] = uu[k];
+        }
         cnt += (uint32_t)__popcll(m);
       }
     }
@@ -674,10 +673,35 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a) {
   const double s = wave_sum_f64((double)acc);
   if (lane == 0) {
     *part = (uint64_t)__double_as_longlong(s);
-    slot[wave] = ((uint32_t)it.tensor << 8) | min(cnt, (uint32_t)kSpecPerWave);
+    a.heads[blockIdx.x * kWaves + wave] = ((uint32_t)t << 8) | min(cnt, (uint32_t)kSpecPerWave);
     if (cnt > (uint32_t)kSpecPerWave)
-      __hip_atomic_fetch_or(&a.flags[it.tensor], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_or(&a.flags[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// The per-tensor tables are __restrict__ const kernel arguments so that they are read with
+// scalar loads (a vector load there is waited for before the x loads are issued).
+template <int WIDTH>
+__global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
+                                                            const int64_t* __restrict__ begins) {
+  const int64_t blk = blockIdx.x;
+  const Item it = a.e.items[blk >> 2];
+  const SpecBracket br = brs[it.tensor];
+  const int64_t tb = begins[it.tensor];
+  const int64_t b = it.begin + (blk & 3) * kSpecBlk;
+  const int wave = threadIdx.x >> 6;
+  uint32_t* slot = a.slots + blk * kSpecSlot;
+  uint64_t* part = a.partials + blk * kWaves + wave;
+  if (b >= it.end) {  // past the tensor's end: an empty block still reports (stale values otherwise)
+    if ((threadIdx.x & 63) == 0) {
+      *part = 0ull;
+      a.heads[blk * kWaves + wave] = (uint32_t)it.tensor << 8;
+    }
+    return;
+  }
+  const int64_t end = min(b + kSpecBlk, it.end);
+  if (end - b == kSpecBlk) spec_block<WIDTH, true>(a, b, end, it.tensor, tb, br, slot, part);
+  else spec_block<WIDTH, false>(a, b, end, it.tensor, tb, br, slot, part);
 }
 
 __global__ __launch_bounds__(kThreads) void qsgd_spec_fold(SpecArgs a) {
@@ -691,7 +715,8 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_fold(SpecArgs a) {
 #pragma unroll
   for (int i = 0; i < U; ++i) {
     const int64_t j = fi.p_begin + threadIdx.x + (int64_t)i * kThreads;
-    v[i] = j < fi.p_end ? __longlong_as_double((long long)a.partials[j]) : 0.0;
+    const double d = __longlong_as_double((long long)a.partials[j < fi.p_end ? j : fi.p_begin]);  // unconditional load
+    v[i] = j < fi.p_end ? d : 0.0;
   }
   double p = 0.0;
 #pragma unroll
@@ -723,41 +748,25 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_fold(SpecArgs a) {
   if (!ok) *a.any_whole = a.epoch;
 }
 
-// Uniforms of the quad at tensor-relative element rel (the Philox layout of philox_rows).
-__device__ __forceinline__ float4 spec_quad_uniforms(const EncArgs& a, int64_t rel, int32_t t) {
-  const uint64_t G = (uint64_t)(rel >> 12) * (uint64_t)kThreads + (uint64_t)((rel >> 2) & (kThreads - 1));
-  const int sl = (int)((rel >> 10) & 3);
-  uint32_t w[12];
-#pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    const uint64_t ctr = 3 * G + c;
-    const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)t, a.offset),
-                                  a.seed_lo, a.seed_hi);
-    w[4 * c] = r.x; w[4 * c + 1] = r.y; w[4 * c + 2] = r.z; w[4 * c + 3] = r.w;
-  }
-  float4 u = u24x4(w[0], w[1], w[2]);
-#pragma unroll
-  for (int s = 1; s < 4; ++s)
-    if (s == sl) u = u24x4(w[3 * s], w[3 * s + 1], w[3 * s + 2]);
-  return u;
-}
-
-__device__ __forceinline__ float4 load_quad(const float* __restrict__ x, int64_t e, int64_t end) {
-  if (e + 4 <= end) return *reinterpret_cast<const float4*>(x + e);
-  float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-  v.x = x[e];
-  if (e + 1 < end) v.y = x[e + 1];
-  if (e + 2 < end) v.z = x[e + 2];
-  return v;
-}
-
+// Two dependent rounds of memory: (slot header, the wave's list and records, the block's item),
+// then the tensor's norm; then the exact levels of the listed quads from their recorded x and
+// draws.  Listed quads are fixed whatever the tensor's status (exact for the final norm either
+// way); whole-tensor requantisation runs only in launches whose fold flagged a tensor
+// (any_whole == epoch).
 template <int WIDTH>
-__global__ __launch_bounds__(kThreads) void qsgd_spec_fix(SpecArgs a) {
+__global__ __launch_bounds__(kThreads) void qsgd_spec_fix(SpecArgs a, const Item* __restrict__ items,
+                                                          const int64_t* __restrict__ begins,
+                                                          const float* __restrict__ norms,
+                                                          const uint32_t* __restrict__ slots,
+                                                          const uint32_t* __restrict__ status,
+                                                          const uint32_t* __restrict__ any_whole,
+                                                          const float4* __restrict__ recs,
+                                                          const uint32_t* __restrict__ heads) {
   constexpr int BPW = kThreads / kWaves;  // blocks per workgroup (one thread per wave slot)
   __shared__ uint32_t s_rep[BPW];
   __shared__ uint32_t s_nrep;
   const EncArgs& e = a.e;
-  const bool whole = *a.any_whole == a.epoch;  // uniform: some tensor is requantised whole
+  const bool whole = *any_whole == a.epoch;  // uniform: some tensor is requantised whole
   if (whole) {
     if (threadIdx.x == 0) s_nrep = 0u;
     __syncthreads();
@@ -765,49 +774,43 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_fix(SpecArgs a) {
   const int64_t blk = (int64_t)blockIdx.x * BPW + (threadIdx.x >> 2);
   const int w = threadIdx.x & 3;
   if (blk < a.nblocks) {
-    const uint32_t* slot = a.slots + blk * kSpecSlot;
-    const uint32_t head = slot[w];
-    const int32_t t = (int32_t)(head >> 8);
+    const uint32_t* slot = slots + blk * kSpecSlot;
+    const uint32_t head = heads[blk * kWaves + w];
     const uint32_t cnt = head & 0xffu;
-    if (!whole || a.status[t] == 0u) {
-      if (cnt) {
-        const Item it = e.items[blk >> 2];
-        const int64_t b = it.begin + (blk & 3) * kSpecBlk;
-        {
-          const int64_t end = min(b + kSpecBlk, it.end), tb = a.begins[it.tensor];
-          int64_t el[kSpecPerWave];
-          float4 xv[kSpecPerWave];
+    const Item it = items[blk >> 2];
+    if (cnt) {
+      const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
+      const float norm = norms[head >> 8];
+      uint32_t ent[kSpecPerWave];
+      float4 xr[kSpecPerWave], ur[kSpecPerWave];
+      const float4* rec = recs + 2 * ((blk * kWaves + w) * kSpecPerWave);
 #pragma unroll
-          for (int j = 0; j < kSpecPerWave; ++j) {  // every load in flight before any arithmetic
-            el[j] = (uint32_t)j < cnt ? 4 * (int64_t)slot[kWaves + kSpecPerWave * w + j] : b;
-            xv[j] = (uint32_t)j < cnt ? load_quad(e.x, el[j], end) : make_float4(0.f, 0.f, 0.f, 0.f);
-          }
-          const Divisor dv(e.norm_out[it.tensor]);
-#pragma unroll
-          for (int j = 0; j < kSpecPerWave; ++j) {
-            if ((uint32_t)j >= cnt) break;
-            float4 x1[1] = {xv[j]};
-            scale_f4<1>(x1, e);
-            int32_t qq[4];
-            qsgd_quad<false>(x1[0], spec_quad_uniforms(e, el[j] - tb, it.tensor), dv, e.levels, false, qq);
-            store_quad<WIDTH>(e, el[j], end, qq);
-          }
-        }
+      for (int j = 0; j < kSpecPerWave; ++j) {  // only the listed records (unconditional loads of all 7 measured 2x slower)
+        const bool on = (uint32_t)j < cnt;
+        ent[j] = on ? slot[kSpecPerWave * w + j] : 0u;
+        xr[j] = on ? rec[2 * j] : make_float4(0.f, 0.f, 0.f, 0.f);
+        ur[j] = on ? rec[2 * j + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-    } else if (w == 0) {
-      s_rep[atomicAdd(&s_nrep, 1u)] = (uint32_t)(threadIdx.x >> 2);
+      const Divisor dv(norm);
+#pragma unroll
+      for (int j = 0; j < kSpecPerWave; ++j) {
+        if ((uint32_t)j >= cnt) break;
+        int32_t qq[4];
+        qsgd_quad<false>(xr[j], ur[j], dv, e.levels, false, qq);
+        store_quad<WIDTH>(e, 4 * (int64_t)ent[j], end, qq);
+      }
     }
+    if (whole && w == 0 && status[it.tensor] != 0u) s_rep[atomicAdd(&s_nrep, 1u)] = (uint32_t)(threadIdx.x >> 2);
   }
   if (!whole) return;
   __syncthreads();
   const uint32_t nrep = s_nrep;
   for (uint32_t r = 0; r < nrep; ++r) {  // whole blocks of requantised tensors, all 256 threads
     const int64_t rb = (int64_t)blockIdx.x * BPW + s_rep[r];
-    const Item it = e.items[rb >> 2];
+    const Item it = items[rb >> 2];
     const int64_t b = it.begin + (rb & 3) * kSpecBlk;
     if (b < it.end)
-      quant_sub<WIDTH, false, kSpecV>(e, b, min(b + kSpecBlk, it.end), a.begins[it.tensor], it.tensor,
-                                      e.norm_out[it.tensor]);
+      quant_sub<WIDTH, false, kSpecV>(e, b, min(b + kSpecBlk, it.end), begins[it.tensor], it.tensor, norms[it.tensor]);
   }
 }
 
@@ -950,13 +953,15 @@ struct omf_plan {
   int64_t n_spec_blocks = 0, n_spec_br = 0, n_spec_fold = 0;
   SpecBrItem* d_spec_br_items = nullptr;
   SpecFoldItem* d_spec_fold_items = nullptr;
-  uint64_t* d_spec_br_part = nullptr;
   uint64_t* d_spec_seg_part = nullptr;
-  uint32_t* d_spec_cnt = nullptr;  // [br_cnt x nt][fold_cnt x nt][any_whole]
+  uint32_t* d_spec_cnt = nullptr;  // [fold_cnt x nt][any_whole]
   uint32_t spec_epoch = 0;
+  uint32_t spec_skip = 0;  // experiment switch (OMF_SPEC_SKIP)
   SpecBracket* d_spec_br = nullptr;
   uint64_t* d_spec_part = nullptr;
   uint32_t* d_spec_slots = nullptr;
+  uint32_t* d_spec_heads = nullptr;
+  float4* d_spec_recs = nullptr;  // listed quads' x and draws (32 B each)
   uint32_t* d_spec_flags = nullptr;
   uint32_t* d_spec_status = nullptr;
   // Launches that use the sync block / granules are ordered across streams: a launch on a
@@ -1182,7 +1187,7 @@ static int upload_plan(omf_plan* p) {
   // kSpecSeg wave partials (4 per 4 Ki block, kSub / kSpecBlk = 4 blocks per flat item).
   std::vector<SpecBrItem> br_items;
   std::vector<SpecFoldItem> fold_items;
-  int32_t br_pbase = 0, seg_base = 0;
+  int32_t seg_base = 0;
   for (int32_t t = 0; t < p->nt; ++t) {
     const int64_t n = p->sizes[t], b = p->offsets[t];
     const int64_t p_begin = (int64_t)kWaves * 4 * (int64_t)flat.size();
@@ -1191,11 +1196,8 @@ static int upload_plan(omf_plan* p) {
       flat.push_back(Item{cb, std::min(b + n, cb + kSub), t, kQuant, (int32_t)c, 0});
     }
     const int64_t p_end = (int64_t)kWaves * 4 * (int64_t)flat.size();
-    const int64_t R = std::max<int64_t>(1, std::min<int64_t>(kSpecRuns, n / 32));
-    const int32_t nparts = n <= kSpecExact ? 1 : (int32_t)((R + kSpecRunsPerPart - 1) / kSpecRunsPerPart);
-    for (int32_t q = 0; q < nparts; ++q)
-      br_items.push_back(SpecBrItem{n / R, (int32_t)R, (int32_t)(n % R), t, q, nparts, br_pbase});
-    br_pbase += nparts;
+    const int64_t R = std::max<int64_t>(1, std::min<int64_t>(kSpecRuns, n / (2 * kSpecRun)));
+    br_items.push_back(SpecBrItem{b, n, n / R, (int32_t)R, (int32_t)(n % R), t});
     const int32_t nsegs = (int32_t)((p_end - p_begin + kSpecSeg - 1) / kSpecSeg);
     for (int32_t q = 0; q < nsegs; ++q)
       fold_items.push_back(SpecFoldItem{p_begin + (int64_t)q * kSpecSeg, std::min(p_end, p_begin + (int64_t)(q + 1) * kSpecSeg),
@@ -1230,12 +1232,13 @@ static int upload_plan(omf_plan* p) {
   const size_t o_ring_p = o; o = round16(o + 8 * 16);
   const size_t o_sp_bri = o; o = round16(o + sizeof(SpecBrItem) * br_items.size());
   const size_t o_sp_foi = o; o = round16(o + sizeof(SpecFoldItem) * fold_items.size());
-  const size_t o_sp_brp = o; o = round16(o + 16 * br_items.size());
   const size_t o_sp_segp = o; o = round16(o + 8 * fold_items.size());
-  const size_t o_sp_cnt = o; o = round16(o + 8 * (size_t)p->nt + 4);
+  const size_t o_sp_cnt = o; o = round16(o + 4 * (size_t)p->nt + 4);
   const size_t o_sp_br = o; o = round16(o + sizeof(SpecBracket) * (size_t)p->nt);
   const size_t o_sp_part = o; o = round16(o + 8 * (size_t)kWaves * (size_t)p->n_spec_blocks);
   const size_t o_sp_slots = o; o = round16(o + 4 * (size_t)kSpecSlot * (size_t)p->n_spec_blocks);
+  const size_t o_sp_heads = o; o = round16(o + 4 * (size_t)kWaves * (size_t)p->n_spec_blocks);
+  const size_t o_sp_recs = o; o = round16(o + 32 * (size_t)kWaves * kSpecPerWave * (size_t)p->n_spec_blocks);
   const size_t o_sp_flags = o; o = round16(o + 4 * (size_t)p->nt);
   const size_t o_sp_status = o; o = round16(o + 4 * (size_t)p->nt);
   DeviceGuard g(p->device);
@@ -1262,18 +1265,19 @@ static int upload_plan(omf_plan* p) {
   p->d_ring_prof = reinterpret_cast<unsigned long long*>(base + o_ring_p);
   p->d_spec_br_items = reinterpret_cast<SpecBrItem*>(base + o_sp_bri);
   p->d_spec_fold_items = reinterpret_cast<SpecFoldItem*>(base + o_sp_foi);
-  p->d_spec_br_part = reinterpret_cast<uint64_t*>(base + o_sp_brp);
   p->d_spec_seg_part = reinterpret_cast<uint64_t*>(base + o_sp_segp);
   p->d_spec_cnt = reinterpret_cast<uint32_t*>(base + o_sp_cnt);
   p->d_spec_br = reinterpret_cast<SpecBracket*>(base + o_sp_br);
   p->d_spec_part = reinterpret_cast<uint64_t*>(base + o_sp_part);
   p->d_spec_slots = reinterpret_cast<uint32_t*>(base + o_sp_slots);
+  p->d_spec_heads = reinterpret_cast<uint32_t*>(base + o_sp_heads);
+  p->d_spec_recs = reinterpret_cast<float4*>(base + o_sp_recs);
   p->d_spec_flags = reinterpret_cast<uint32_t*>(base + o_sp_flags);
   p->d_spec_status = reinterpret_cast<uint32_t*>(base + o_sp_status);
   OMF_HIP(hipMemcpy(p->d_spec_br_items, br_items.data(), sizeof(SpecBrItem) * br_items.size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_spec_fold_items, fold_items.data(), sizeof(SpecFoldItem) * fold_items.size(),
                     hipMemcpyHostToDevice));
-  OMF_HIP(hipMemset(p->d_spec_cnt, 0, 8 * (size_t)p->nt + 4));
+  OMF_HIP(hipMemset(p->d_spec_cnt, 0, 4 * (size_t)p->nt + 4));
   OMF_HIP(hipMemset(p->d_spec_flags, 0, 4 * (size_t)p->nt));
   OMF_HIP(hipMemset(p->d_ring_prof, 0, 8 * 16));
   OMF_HIP(hipMemcpy(p->d_enc[0], seq[0].data(), sizeof(Item) * seq[0].size(), hipMemcpyHostToDevice));
@@ -1351,10 +1355,11 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     if (const char* bm = getenv("OMF_RING_BIG")) p->ring_big_mode = atoi(bm) == 1 ? 1 : 0;
     if (const char* gp = getenv("OMF_RING_GAP")) p->ring_gap = atoll(gp);
     if (const char* dg = getenv("OMF_RING_DBG")) p->ring_dbg = (uint32_t)atoi(dg);
-    // Default strategy by arena size: the two-pass encoder's second read comes from the
-    // Infinity Cache and beats the ring on Llama-400M (401 M elements: 0.604 vs 0.624 ms);
-    // the ring wins below (Llama-150M 0.349 vs 0.359, ResNet-18 0.033 vs 0.058 ms).
-    p->strategy = p->arena_end >= ((int64_t)1 << 28) ? 1 : 2;
+    if (const char* sk = getenv("OMF_SPEC_SKIP")) p->spec_skip = (uint32_t)atoi(sk);
+    // Default strategy by arena size: the bracketed single-read encoder from 2^25 elements
+    // (Llama-400M 0.386 ms against the two-pass 0.59 and the ring 0.63; Llama-150M 0.25 against
+    // 0.35), the ring below (ResNet-18: 0.032 ms against 0.08 for the bracket's four launches).
+    p->strategy = p->arena_end >= ((int64_t)1 << 25) ? 3 : 2;
     if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 3));
     p->ring_grid = omf::ring::grid_size(p->ring_cfg, device);
     if (p->ring_grid <= 0) {
@@ -1449,11 +1454,11 @@ int omf_plan_spec_stats(omf_plan* plan, void* stream, int64_t* out4) {
   if (!plan || !out4) return fail(OMF_EINVAL, "omf_plan_spec_stats: NULL argument");
   DeviceGuard g(plan->device);
   OMF_HIP(hipStreamSynchronize((hipStream_t)stream));
-  std::vector<uint32_t> status(plan->nt), slots((size_t)kSpecSlot * (size_t)plan->n_spec_blocks);
+  std::vector<uint32_t> status(plan->nt), heads((size_t)kWaves * (size_t)plan->n_spec_blocks);
   std::vector<SpecBracket> br(plan->nt);
   OMF_HIP(hipMemcpy(status.data(), plan->d_spec_status, 4 * (size_t)plan->nt, hipMemcpyDeviceToHost));
   OMF_HIP(hipMemcpy(br.data(), plan->d_spec_br, sizeof(SpecBracket) * (size_t)plan->nt, hipMemcpyDeviceToHost));
-  OMF_HIP(hipMemcpy(slots.data(), plan->d_spec_slots, 4 * slots.size(), hipMemcpyDeviceToHost));
+  OMF_HIP(hipMemcpy(heads.data(), plan->d_spec_heads, 4 * heads.size(), hipMemcpyDeviceToHost));
   int64_t whole = 0, deferred = 0, listed = 0, full = 0;
   for (int32_t t = 0; t < plan->nt; ++t) {
     whole += status[t] != 0u;
@@ -1461,7 +1466,7 @@ int omf_plan_spec_stats(omf_plan* plan, void* stream, int64_t* out4) {
   }
   for (int64_t blk = 0; blk < plan->n_spec_blocks; ++blk)
     for (int w = 0; w < kWaves; ++w) {
-      const uint32_t c = slots[(size_t)blk * kSpecSlot + w] & 0xffu;
+      const uint32_t c = heads[(size_t)blk * kWaves + w] & 0xffu;
       listed += c;
       full += c == (uint32_t)kSpecPerWave;
     }
@@ -1590,27 +1595,41 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.sizes = p->d_sizes;
     sa.br_items = p->d_spec_br_items;
     sa.fold_items = p->d_spec_fold_items;
-    sa.br_part = p->d_spec_br_part;
     sa.seg_part = p->d_spec_seg_part;
-    sa.br_cnt = p->d_spec_cnt;
-    sa.fold_cnt = p->d_spec_cnt + p->nt;
-    sa.any_whole = p->d_spec_cnt + 2 * p->nt;
+    sa.fold_cnt = p->d_spec_cnt;
+    sa.any_whole = p->d_spec_cnt + p->nt;
     if (++p->spec_epoch == 0) ++p->spec_epoch;
     sa.epoch = p->spec_epoch;
     sa.br = p->d_spec_br;
     sa.partials = p->d_spec_part;
     sa.slots = p->d_spec_slots;
+    sa.heads = p->d_spec_heads;
+    sa.recs = p->d_spec_recs;
     sa.flags = p->d_spec_flags;
     sa.status = p->d_spec_status;
     sa.nblocks = p->n_spec_blocks;
     const dim3 gbr((unsigned)p->n_spec_br), gfo((unsigned)p->n_spec_fold), gb((unsigned)p->n_spec_blocks),
         gf((unsigned)((p->n_spec_blocks + kThreads / kWaves - 1) / (kThreads / kWaves)));
-    hipLaunchKernelGGL(qsgd_spec_bracket, gbr, blk, 0, st, sa);
-    if (width == 1) hipLaunchKernelGGL(qsgd_spec_quant<1>, gb, blk, 0, st, sa);
-    else hipLaunchKernelGGL(qsgd_spec_quant<4>, gb, blk, 0, st, sa);
-    hipLaunchKernelGGL(qsgd_spec_fold, gfo, blk, 0, st, sa);
-    if (width == 1) hipLaunchKernelGGL(qsgd_spec_fix<1>, gf, blk, 0, st, sa);
-    else hipLaunchKernelGGL(qsgd_spec_fix<4>, gf, blk, 0, st, sa);
+    // p->spec_skip: experiment switch (OMF_SPEC_SKIP, read at plan creation; never set in
+    // production): bit 0 skips the bracket launch (the previous brackets stay), bit 1 the fold,
+    // bit 2 the fix — timings only, the payload is then not the encoder's.
+    if (!(p->spec_skip & 1u)) hipLaunchKernelGGL(qsgd_spec_bracket, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
+    if (width == 1) hipLaunchKernelGGL(qsgd_spec_quant<1>, gb, blk, 0, st, sa, sa.br, sa.begins);
+    else hipLaunchKernelGGL(qsgd_spec_quant<4>, gb, blk, 0, st, sa, sa.br, sa.begins);
+    if (!(p->spec_skip & 2u)) hipLaunchKernelGGL(qsgd_spec_fold, gfo, blk, 0, st, sa);
+    const uint32_t* cst = sa.status;
+    if (p->spec_skip & 4u) {
+      OMF_HIP(hipGetLastError());
+      return OMF_OK;
+    }
+    if (width == 1)
+      hipLaunchKernelGGL(qsgd_spec_fix<1>, gf, blk, 0, st, sa, (const Item*)a.items, (const int64_t*)sa.begins,
+                         (const float*)a.norm_out, (const uint32_t*)sa.slots, cst, (const uint32_t*)sa.any_whole,
+                         (const float4*)sa.recs, (const uint32_t*)sa.heads);
+    else
+      hipLaunchKernelGGL(qsgd_spec_fix<4>, gf, blk, 0, st, sa, (const Item*)a.items, (const int64_t*)sa.begins,
+                         (const float*)a.norm_out, (const uint32_t*)sa.slots, cst, (const uint32_t*)sa.any_whole,
+                         (const float4*)sa.recs, (const uint32_t*)sa.heads);
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }

@@ -1,0 +1,41 @@
+"""Marginal cost of each bracketed-encoder launch: encode timings with OMF_SPEC_SKIP bits
+(experiment; each setting in its own plan, interleaved)."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from omnifed_amd import codec, shapes  # noqa: E402
+
+dev = torch.device("cuda", 0)
+sizes = [shapes.numel(s) for _, s in shapes.model_shapes(os.environ.get("MODEL", "llama400m"))]
+settings = [0, 1, 2, 4, 6, 7]
+plans = {}
+for sk in settings:
+    os.environ["OMF_SPEC_SKIP"] = str(sk)
+    p = codec.Plan(sizes, device=dev)
+    p.set_encode_strategy("bracket")
+    plans[sk] = p
+os.environ.pop("OMF_SPEC_SKIP")
+x = torch.randn(plans[0].arena_end, device=dev) * 1e-3
+q = torch.empty(plans[0].payload_elems(8), dtype=torch.int8, device=dev)
+nr = torch.empty(len(sizes), device=dev)
+for p in plans.values():
+    p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1)  # brackets exist before skipping them
+res = {sk: [] for sk in settings}
+for rnd in range(7):
+    for sk in settings:
+        p = plans[sk]
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for i in range(20):
+            p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1, offset=i)
+        e1.record()
+        torch.cuda.synchronize()
+        res[sk].append(e0.elapsed_time(e1) / 20)
+names = {0: "all four", 1: "no bracket", 2: "no fold", 4: "no fix", 6: "quant+bracket", 7: "quant only"}
+for sk in settings:
+    v = sorted(res[sk])
+    print(f"{names[sk]:14s}: median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f}", flush=True)

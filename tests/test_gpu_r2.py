@@ -398,9 +398,9 @@ def test_layer_states_belong_to_the_callers_pb2(gpu, monkeypatch):
 
 
 def test_default_encode_strategy_by_arena_size(gpu):
-    """A new plan takes the two-pass encoder for arenas of >= 2^28 elements (its second read is
-    served by the Infinity Cache) and the single-read ring below."""
+    """A new plan takes the bracketed single-read encoder for arenas of >= 2^25 elements and the
+    single-read ring below."""
     small = codec.Plan([1 << 20, 5000], device=gpu)
     assert small.strategy == "ring"
-    big = codec.Plan([1 << 27, 1 << 27, 1000], device=gpu)
-    assert big.strategy == "ordered"
+    big = codec.Plan([1 << 24, 1 << 24, 1000], device=gpu)
+    assert big.strategy == "bracket"
