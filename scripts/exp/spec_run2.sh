@@ -1,0 +1,10 @@
+#!/usr/bin/env bash
+# Spec encoder GPU tests, the marginal-cost timings, then strategy timings + kernel trace.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_spec.py -x -q --timeout 120 --timeout-method thread > gpurun_out/spec_tests.log 2>&1 || { tail -40 gpurun_out/spec_tests.log; exit 1; }
+tail -2 gpurun_out/spec_tests.log
+timeout -k 10 200 python scripts/exp/spec_skip.py || exit 1
+rm -f gpurun_out/spec_perf.log
+bash scripts/exp/spec_perf.sh
