@@ -748,11 +748,12 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_fold(SpecArgs a) {
   if (!ok) *a.any_whole = a.epoch;
 }
 
-// Two dependent rounds of memory: (slot header, the wave's list and records, the block's item),
-// then the tensor's norm; then the exact levels of the listed quads from their recorded x and
-// draws.  Listed quads are fixed whatever the tensor's status (exact for the final norm either
-// way); whole-tensor requantisation runs only in launches whose fold flagged a tensor
-// (any_whole == epoch).
+// One thread per listed-quad position (8 per wave slot, 7 used): two dependent rounds of
+// memory — (the slot header), then (the quad's index, recorded x and draws, the tensor's norm
+// and the block's item) — then the exact level from the shared element math (Markstein
+// division) and its store.  Listed quads are fixed whatever the tensor's status (exact for
+// the final norm either way); whole-tensor requantisation runs only in launches whose fold
+// flagged a tensor (any_whole == epoch), by the workgroup that holds the block's slots.
 template <int WIDTH>
 __global__ __launch_bounds__(kThreads) void qsgd_spec_fix(SpecArgs a, const Item* __restrict__ items,
                                                           const int64_t* __restrict__ begins,
@@ -762,7 +763,9 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_fix(SpecArgs a, const Item
                                                           const uint32_t* __restrict__ any_whole,
                                                           const float4* __restrict__ recs,
                                                           const uint32_t* __restrict__ heads) {
-  constexpr int BPW = kThreads / kWaves;  // blocks per workgroup (one thread per wave slot)
+  constexpr int LPS = 8;                          // threads per wave slot
+  constexpr int SPW = kThreads / LPS;             // wave slots per workgroup (32)
+  constexpr int BPW = SPW / kWaves;               // blocks per workgroup (8)
   __shared__ uint32_t s_rep[BPW];
   __shared__ uint32_t s_nrep;
   const EncArgs& e = a.e;
@@ -771,36 +774,26 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_fix(SpecArgs a, const Item
     if (threadIdx.x == 0) s_nrep = 0u;
     __syncthreads();
   }
-  const int64_t blk = (int64_t)blockIdx.x * BPW + (threadIdx.x >> 2);
-  const int w = threadIdx.x & 3;
+  const int64_t ws = (int64_t)blockIdx.x * SPW + threadIdx.x / LPS;  // global wave slot
+  const int j = threadIdx.x & (LPS - 1);
+  const int64_t blk = ws / kWaves;
+  const int w = (int)(ws % kWaves);
   if (blk < a.nblocks) {
-    const uint32_t* slot = slots + blk * kSpecSlot;
-    const uint32_t head = heads[blk * kWaves + w];
+    const uint32_t head = heads[ws];
     const uint32_t cnt = head & 0xffu;
-    const Item it = items[blk >> 2];
-    if (cnt) {
-      const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
+    if ((uint32_t)j < cnt) {
+      const uint32_t q = slots[blk * kSpecSlot + kSpecPerWave * w + j];
+      const float4* rec = recs + 2 * (ws * kSpecPerWave + j);
+      const float4 xr = rec[0], ur = rec[1];
       const float norm = norms[head >> 8];
-      uint32_t ent[kSpecPerWave];
-      float4 xr[kSpecPerWave], ur[kSpecPerWave];
-      const float4* rec = recs + 2 * ((blk * kWaves + w) * kSpecPerWave);
-#pragma unroll
-      for (int j = 0; j < kSpecPerWave; ++j) {  // only the listed records (unconditional loads of all 7 measured 2x slower)
-        const bool on = (uint32_t)j < cnt;
-        ent[j] = on ? slot[kSpecPerWave * w + j] : 0u;
-        xr[j] = on ? rec[2 * j] : make_float4(0.f, 0.f, 0.f, 0.f);
-        ur[j] = on ? rec[2 * j + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-      }
-      const Divisor dv(norm);
-#pragma unroll
-      for (int j = 0; j < kSpecPerWave; ++j) {
-        if ((uint32_t)j >= cnt) break;
-        int32_t qq[4];
-        qsgd_quad<false>(xr[j], ur[j], dv, e.levels, false, qq);
-        store_quad<WIDTH>(e, 4 * (int64_t)ent[j], end, qq);
-      }
+      const Item it = items[blk >> 2];
+      const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
+      int32_t qq[4];
+      qsgd_quad<false>(xr, ur, Divisor(norm), e.levels, false, qq);
+      store_quad<WIDTH>(e, 4 * (int64_t)q, end, qq);
     }
-    if (whole && w == 0 && status[it.tensor] != 0u) s_rep[atomicAdd(&s_nrep, 1u)] = (uint32_t)(threadIdx.x >> 2);
+    if (whole && w == 0 && j == 0 && status[head >> 8] != 0u)
+      s_rep[atomicAdd(&s_nrep, 1u)] = (uint32_t)(blk - (int64_t)blockIdx.x * BPW);
   }
   if (!whole) return;
   __syncthreads();
@@ -1609,7 +1602,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.status = p->d_spec_status;
     sa.nblocks = p->n_spec_blocks;
     const dim3 gbr((unsigned)p->n_spec_br), gfo((unsigned)p->n_spec_fold), gb((unsigned)p->n_spec_blocks),
-        gf((unsigned)((p->n_spec_blocks + kThreads / kWaves - 1) / (kThreads / kWaves)));
+        gf((unsigned)((p->n_spec_blocks + 7) / 8));  // qsgd_spec_fix: 8 blocks (32 wave slots x 8 threads) per workgroup
     // p->spec_skip: experiment switch (OMF_SPEC_SKIP, read at plan creation; never set in
     // production): bit 0 skips the bracket launch (the previous brackets stay), bit 1 the fold,
     // bit 2 the fix — timings only, the payload is then not the encoder's.
