@@ -393,12 +393,13 @@ __global__ __launch_bounds__(kThreads) void qsgd_quant_sub(EncArgs a) {
 //                      "undecided" and listed in the wave's slot (scripts/exp/spec_check.c
 //                      checks the rule: 0 mismatches at brackets' end points and at decision
 //                      points j + u; u == 0 with x != 0 is always undecided).
-//   qsgd_spec_fold     one workgroup per tensor: folds its wave partials in a fixed order
-//                      (the norm), checks it lies in the bracket.
-//   qsgd_spec_fix      one thread per wave slot: the listed quads exactly (Markstein division,
-//                      the shared element math); a tensor whose norm fell outside its bracket,
-//                      whose slots overflowed or whose sample was degenerate is requantised
-//                      whole from x (exact; the rare path).
+//   qsgd_spec_finish   its first workgroups fold the wave partials in segments (the last
+//                      arriver folds the segments in order: the deterministic norm), check it
+//                      lies in the bracket and publish {epoch, bad, norm}; the rest fix the
+//                      listed quads exactly from their records (Markstein division, the shared
+//                      element math), one thread per quad, polling their tensor's granule; a
+//                      tensor whose norm fell outside its bracket, whose slots overflowed or
+//                      whose sample was degenerate is requantised whole from x (the rare path).
 // Payload bits equal every other strategy's for the same norm.
 constexpr int kSpecV = 4;                                    // float4 rows per thread
 constexpr int64_t kSpecBlk = (int64_t)kSpecV * kThreads * 4;  // 4096 elements per block
@@ -407,7 +408,8 @@ constexpr int kSpecPerWave = 7;                               // listed quads pe
 constexpr int64_t kSpecExact = 16384;                         // tensors read whole by the bracket
 constexpr int kSpecRun = 64;                                  // elements per sampled run (256 B: DRAM-friendly)
 constexpr int kSpecRuns = 512;                                // sampled runs per larger tensor (at most)
-constexpr int kSpecSeg = 2048;                                // wave partials per fold workgroup
+constexpr int kSpecSeg = 4096;                                // wave partials per fold workgroup (16 loads per thread
+                                                              // in flight: a 4 Mi-element tensor is one segment)
 // Widest level count the bracket serves: the undecided fraction grows with L (a level step is
 // norm / L wide), and at L = 32 a 1 Mi-element tensor's sampled bracket already leaves ~1.3
 // undecided quads per wave; wider payloads take the two-pass encoder.
@@ -449,7 +451,11 @@ struct SpecArgs {
   float4* recs;            // per listed quad: its scaled x and its uniforms (2 float4), kWaves x kSpecPerWave per block
   uint32_t* flags;         // per tensor: a wave's slot overflowed (set by quant, cleared by fold)
   uint32_t* status;        // per tensor: 0 = listed quads only, 1 = requantise whole
-  uint32_t* any_whole;     // = epoch when some tensor of this launch is requantised whole
+  uint64_t* ngran;         // per tensor: {epoch << 1 | bad, norm} published by the fold
+  uint64_t wait_ticks;     // bound of a fix thread's wait for its tensor's norm (100 MHz ticks)
+  uint32_t dbg;            // experiment switches (OMF_SPEC_SKIP bits 2-3), 0 in production
+  float divisor;           // fused PS step: x := x / divisor (IEEE), written to xout; 0 = none
+  float* xout;
   uint32_t epoch;          // per-launch tag (never 0)
   int64_t nblocks;
 };
@@ -464,6 +470,16 @@ __device__ __forceinline__ float4 scale_alpha(float4 v, float alpha) {
   if (alpha != 1.0f) {
     v.x = __fmul_rn(v.x, alpha); v.y = __fmul_rn(v.y, alpha);
     v.z = __fmul_rn(v.z, alpha); v.w = __fmul_rn(v.w, alpha);
+  }
+  return v;
+}
+
+// x * alpha, then / divisor for the fused PS step (divisor 0: none) — the pass's arithmetic.
+__device__ __forceinline__ float4 spec_prologue(float4 v, float alpha, float divisor) {
+  v = scale_alpha(v, alpha);
+  if (divisor != 0.0f) {
+    v.x = __fdiv_rn(v.x, divisor); v.y = __fdiv_rn(v.y, divisor);
+    v.z = __fdiv_rn(v.z, divisor); v.w = __fdiv_rn(v.w, divisor);
   }
   return v;
 }
@@ -523,7 +539,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     }
     float acc = 0.0f;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) acc = sq4(scale_alpha(v[i], alpha), acc);
+    for (int i = 0; i < PER; ++i) acc = sq4(spec_prologue(v[i], alpha, a.divisor), acc);
     s1 = acc;
   } else {
     // runs of 64 elements at a hashed position inside each of R <= 512 balanced strata (of
@@ -545,7 +561,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     }
 #pragma unroll
     for (int i = 0; i < PASSES; ++i) {
-      float sr = live[i] ? sq4(scale_alpha(v[i], alpha), 0.0f) : 0.0f;
+      float sr = live[i] ? sq4(spec_prologue(v[i], alpha, a.divisor), 0.0f) : 0.0f;
 #pragma unroll
       for (int o = LPR / 2; o > 0; o >>= 1) sr += __shfl_xor(sr, o, LPR);  // the run's sum in every lane
       if (live[i] && j == 0) {
@@ -625,13 +641,13 @@ __device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t 
 // One block's pass: loads issued first, the Philox draws (independent of x) computed while
 // they are in flight, then the partial, the levels and the undecided list.  FULL: a whole
 // 4 Ki block (straight-line code, no bounds checks).
-template <int WIDTH, bool FULL>
+template <int WIDTH, bool FULL, bool DIV>
 __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t end, int32_t t, int64_t tb,
                                            const SpecBracket& br, uint32_t* slot, uint64_t* part) {
   const EncArgs& e = a.e;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float4 v[kSpecV];
-  load_f4<kSpecV, FULL>(e.x, b, end, v);
+  load_f4<kSpecV, FULL, true>(e.x, b, end, v);  // x is read once: nontemporal (the fix uses the records)
   float4 uu[4];
   philox_rows(e, b, tb, t, 0, uu);
   // Branch-free from the loads to the stores, so that the scheduler can place the Philox
@@ -644,6 +660,19 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
   for (int k = 0; k < kSpecV; ++k) {
     v[k].x = __fmul_rn(v[k].x, alpha); v[k].y = __fmul_rn(v[k].y, alpha);
     v[k].z = __fmul_rn(v[k].z, alpha); v[k].w = __fmul_rn(v[k].w, alpha);
+    if (DIV) {  // fused PS step: the average, stored once (nontemporal) and quantised from registers
+      const float d = a.divisor;
+      v[k].x = __fdiv_rn(v[k].x, d); v[k].y = __fdiv_rn(v[k].y, d);
+      v[k].z = __fdiv_rn(v[k].z, d); v[k].w = __fdiv_rn(v[k].w, d);
+      const int64_t el = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+      if (FULL || el + 4 <= end) {
+        store_nt(a.xout + el, v[k]);
+      } else if (el < end) {
+        a.xout[el] = v[k].x;
+        if (el + 1 < end) a.xout[el + 1] = v[k].y;
+        if (el + 2 < end) a.xout[el + 2] = v[k].z;
+      }
+    }
     acc = sq4(v[k], acc);
   }
   uint32_t cnt = 0;  // wave-uniform
@@ -681,7 +710,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
 
 // The per-tensor tables are __restrict__ const kernel arguments so that they are read with
 // scalar loads (a vector load there is waited for before the x loads are issued).
-template <int WIDTH>
+template <int WIDTH, bool DIV>
 __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
                                                             const int64_t* __restrict__ begins) {
   const int64_t blk = blockIdx.x;
@@ -700,16 +729,17 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const Sp
     return;
   }
   const int64_t end = min(b + kSpecBlk, it.end);
-  if (end - b == kSpecBlk) spec_block<WIDTH, true>(a, b, end, it.tensor, tb, br, slot, part);
-  else spec_block<WIDTH, false>(a, b, end, it.tensor, tb, br, slot, part);
+  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV>(a, b, end, it.tensor, tb, br, slot, part);
+  else spec_block<WIDTH, false, DIV>(a, b, end, it.tensor, tb, br, slot, part);
 }
 
-__global__ __launch_bounds__(kThreads) void qsgd_spec_fold(SpecArgs a) {
+// One fold segment (a workgroup of the finish launch); the last arriver of the tensor folds the
+// segments in order, checks the bracket and publishes {epoch, bad, norm} in the tensor's granule.
+__device__ void spec_fold(const SpecArgs& a, const SpecFoldItem& fi) {
   __shared__ double red[kWaves];
   __shared__ uint32_t s_last;
-  const SpecFoldItem fi = a.fold_items[blockIdx.x];
   const int32_t t = fi.tensor;
-  // up to kSpecSeg partials: 8 loads in flight per thread, a fixed order
+  // up to kSpecSeg partials: 16 loads in flight per thread, a fixed order
   constexpr int U = kSpecSeg / kThreads;
   double v[U];
 #pragma unroll
@@ -745,65 +775,110 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_fold(SpecArgs a) {
   const bool ok = br.mode == 0u && fl == 0u && norm >= br.n_lo && norm <= br.n_hi;
   a.status[t] = ok ? 0u : 1u;
   if (fl) a.flags[t] = 0u;
-  if (!ok) *a.any_whole = a.epoch;
+  st_agent(&a.ngran[t], ((uint64_t)((a.epoch << 1) | (ok ? 0u : 1u)) << 32) | __float_as_uint(norm));
 }
 
-// One thread per listed-quad position (8 per wave slot, 7 used): two dependent rounds of
-// memory — (the slot header), then (the quad's index, recorded x and draws, the tensor's norm
-// and the block's item) — then the exact level from the shared element math (Markstein
-// division) and its store.  Listed quads are fixed whatever the tensor's status (exact for
-// the final norm either way); whole-tensor requantisation runs only in launches whose fold
-// flagged a tensor (any_whole == epoch), by the workgroup that holds the block's slots.
+// The tensor's norm and status as its fold published them in this launch (bounded; the fold
+// workgroups are dispatched before every fix workgroup).  false: timed out (err bit 4 set,
+// reported as OMF_ETIMEOUT by omf_plan_check).
+__device__ __forceinline__ bool spec_norm_wait(const SpecArgs& a, int32_t t, float& norm, bool& bad) {
+  uint64_t g = ld_agent(&a.ngran[t]);
+  if ((uint32_t)(g >> 33) != a.epoch) {
+    // exponential back-off: every polling wave reads one of 183-odd granules, and tight
+    // polling of a few lines by tens of thousands of waves congests them
+    const uint64_t t0 = wall_clock64();
+    for (int k = 0;; k = min(k + 1, 6)) {
+      if (k < 2) __builtin_amdgcn_s_sleep(4);
+      else if (k < 4) __builtin_amdgcn_s_sleep(16);
+      else __builtin_amdgcn_s_sleep(64);
+      g = ld_agent(&a.ngran[t]);
+      if ((uint32_t)(g >> 33) == a.epoch) break;
+      if (wall_clock64() - t0 > a.wait_ticks) {
+        __hip_atomic_fetch_or(a.e.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+  }
+  norm = __uint_as_float((uint32_t)g);
+  bad = ((g >> 32) & 1u) != 0u;
+  return true;
+}
+
+// The finish launch: its first nfold workgroups fold the partials (spec_fold); the rest fix the
+// listed quads, one thread per listed-quad position (8 per wave slot, 7 used): (the slot
+// header), then (the quad's index, recorded x and draws, the block's item) with the tensor's
+// norm granule, then the exact level from the shared element math (Markstein division) and
+// its store.  A block whose tensor the fold marked bad (norm outside the bracket, a slot
+// overflow, a deferred tensor) is requantised whole from x by its workgroup (the rare path).
 template <int WIDTH>
-__global__ __launch_bounds__(kThreads) void qsgd_spec_fix(SpecArgs a, const Item* __restrict__ items,
-                                                          const int64_t* __restrict__ begins,
-                                                          const float* __restrict__ norms,
-                                                          const uint32_t* __restrict__ slots,
-                                                          const uint32_t* __restrict__ status,
-                                                          const uint32_t* __restrict__ any_whole,
-                                                          const float4* __restrict__ recs,
-                                                          const uint32_t* __restrict__ heads) {
+__global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const SpecFoldItem* __restrict__ fold_items,
+                                                             int32_t nfold, const Item* __restrict__ items,
+                                                             const int64_t* __restrict__ begins,
+                                                             const uint32_t* __restrict__ slots,
+                                                             const float4* __restrict__ recs,
+                                                             const uint32_t* __restrict__ heads) {
+  if ((int32_t)blockIdx.x < nfold) {
+    spec_fold(a, fold_items[blockIdx.x]);
+    return;
+  }
   constexpr int LPS = 8;                          // threads per wave slot
   constexpr int SPW = kThreads / LPS;             // wave slots per workgroup (32)
   constexpr int BPW = SPW / kWaves;               // blocks per workgroup (8)
   __shared__ uint32_t s_rep[BPW];
+  __shared__ float s_rep_norm[BPW];  // the granule's norm (norm_out is written in this launch)
   __shared__ uint32_t s_nrep;
   const EncArgs& e = a.e;
-  const bool whole = *any_whole == a.epoch;  // uniform: some tensor is requantised whole
-  if (whole) {
-    if (threadIdx.x == 0) s_nrep = 0u;
-    __syncthreads();
-  }
-  const int64_t ws = (int64_t)blockIdx.x * SPW + threadIdx.x / LPS;  // global wave slot
+  const int64_t fb = (int64_t)blockIdx.x - nfold;
+  if (threadIdx.x == 0) s_nrep = 0u;
+  const int64_t ws = fb * SPW + threadIdx.x / LPS;  // global wave slot
   const int j = threadIdx.x & (LPS - 1);
   const int64_t blk = ws / kWaves;
   const int w = (int)(ws % kWaves);
+  bool rep = false;
+  float rep_norm = 0.0f;
   if (blk < a.nblocks) {
     const uint32_t head = heads[ws];
     const uint32_t cnt = head & 0xffu;
-    if ((uint32_t)j < cnt) {
+    const int32_t t = (int32_t)(head >> 8);
+    const bool leader = w == 0 && j == 0;  // one status check per block
+    if (((uint32_t)j < cnt || leader) && !(a.dbg & 8u)) {
       const uint32_t q = slots[blk * kSpecSlot + kSpecPerWave * w + j];
       const float4* rec = recs + 2 * (ws * kSpecPerWave + j);
       const float4 xr = rec[0], ur = rec[1];
-      const float norm = norms[head >> 8];
       const Item it = items[blk >> 2];
-      const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
-      int32_t qq[4];
-      qsgd_quad<false>(xr, ur, Divisor(norm), e.levels, false, qq);
-      store_quad<WIDTH>(e, 4 * (int64_t)q, end, qq);
+      float norm;
+      bool bad;
+      if (spec_norm_wait(a, t, norm, bad)) {
+        if ((uint32_t)j < cnt) {
+          const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
+          int32_t qq[4];
+          qsgd_quad<false>(xr, ur, Divisor(norm), e.levels, false, qq);
+          if (!(a.dbg & 4u)) store_quad<WIDTH>(e, 4 * (int64_t)q, end, qq);
+        }
+        rep = leader && bad;
+        rep_norm = norm;
+      }
     }
-    if (whole && w == 0 && j == 0 && status[head >> 8] != 0u)
-      s_rep[atomicAdd(&s_nrep, 1u)] = (uint32_t)(blk - (int64_t)blockIdx.x * BPW);
   }
-  if (!whole) return;
-  __syncthreads();
+  __syncthreads();  // s_nrep initialised
+  if (rep) {
+    const uint32_t i = atomicAdd(&s_nrep, 1u);
+    s_rep[i] = (uint32_t)(blk - fb * BPW);
+    s_rep_norm[i] = rep_norm;
+  }
+  if (!__syncthreads_or(rep)) return;
   const uint32_t nrep = s_nrep;
+  EncArgs er = e;  // the fused PS step requantises from the average the pass wrote
+  if (a.divisor != 0.0f) {
+    er.x = a.xout;
+    er.alpha = 1.0f;
+  }
   for (uint32_t r = 0; r < nrep; ++r) {  // whole blocks of requantised tensors, all 256 threads
-    const int64_t rb = (int64_t)blockIdx.x * BPW + s_rep[r];
+    const int64_t rb = fb * BPW + s_rep[r];
     const Item it = items[rb >> 2];
     const int64_t b = it.begin + (rb & 3) * kSpecBlk;
     if (b < it.end)
-      quant_sub<WIDTH, false, kSpecV>(e, b, min(b + kSpecBlk, it.end), begins[it.tensor], it.tensor, norms[it.tensor]);
+      quant_sub<WIDTH, false, kSpecV>(er, b, min(b + kSpecBlk, it.end), begins[it.tensor], it.tensor, s_rep_norm[r]);
   }
 }
 
@@ -947,10 +1022,11 @@ struct omf_plan {
   SpecBrItem* d_spec_br_items = nullptr;
   SpecFoldItem* d_spec_fold_items = nullptr;
   uint64_t* d_spec_seg_part = nullptr;
-  uint32_t* d_spec_cnt = nullptr;  // [fold_cnt x nt][any_whole]
+  uint32_t* d_spec_cnt = nullptr;  // fold_cnt x nt
   uint32_t spec_epoch = 0;
   uint32_t spec_skip = 0;  // experiment switch (OMF_SPEC_SKIP)
   SpecBracket* d_spec_br = nullptr;
+  uint64_t* d_spec_ngran = nullptr;  // per tensor {epoch << 1 | bad, norm} granules of the fold
   uint64_t* d_spec_part = nullptr;
   uint32_t* d_spec_slots = nullptr;
   uint32_t* d_spec_heads = nullptr;
@@ -1228,6 +1304,7 @@ static int upload_plan(omf_plan* p) {
   const size_t o_sp_segp = o; o = round16(o + 8 * fold_items.size());
   const size_t o_sp_cnt = o; o = round16(o + 4 * (size_t)p->nt + 4);
   const size_t o_sp_br = o; o = round16(o + sizeof(SpecBracket) * (size_t)p->nt);
+  const size_t o_sp_ngran = o; o = round16(o + 8 * (size_t)p->nt);
   const size_t o_sp_part = o; o = round16(o + 8 * (size_t)kWaves * (size_t)p->n_spec_blocks);
   const size_t o_sp_slots = o; o = round16(o + 4 * (size_t)kSpecSlot * (size_t)p->n_spec_blocks);
   const size_t o_sp_heads = o; o = round16(o + 4 * (size_t)kWaves * (size_t)p->n_spec_blocks);
@@ -1261,6 +1338,7 @@ static int upload_plan(omf_plan* p) {
   p->d_spec_seg_part = reinterpret_cast<uint64_t*>(base + o_sp_segp);
   p->d_spec_cnt = reinterpret_cast<uint32_t*>(base + o_sp_cnt);
   p->d_spec_br = reinterpret_cast<SpecBracket*>(base + o_sp_br);
+  p->d_spec_ngran = reinterpret_cast<uint64_t*>(base + o_sp_ngran);
   p->d_spec_part = reinterpret_cast<uint64_t*>(base + o_sp_part);
   p->d_spec_slots = reinterpret_cast<uint32_t*>(base + o_sp_slots);
   p->d_spec_heads = reinterpret_cast<uint32_t*>(base + o_sp_heads);
@@ -1272,6 +1350,7 @@ static int upload_plan(omf_plan* p) {
                     hipMemcpyHostToDevice));
   OMF_HIP(hipMemset(p->d_spec_cnt, 0, 4 * (size_t)p->nt + 4));
   OMF_HIP(hipMemset(p->d_spec_flags, 0, 4 * (size_t)p->nt));
+  OMF_HIP(hipMemset(p->d_spec_ngran, 0, 8 * (size_t)p->nt));  // epoch 0 is never a launch's tag
   OMF_HIP(hipMemset(p->d_ring_prof, 0, 8 * 16));
   OMF_HIP(hipMemcpy(p->d_enc[0], seq[0].data(), sizeof(Item) * seq[0].size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_enc[1], seq[1].data(), sizeof(Item) * seq[1].size(), hipMemcpyHostToDevice));
@@ -1550,6 +1629,62 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }
+  // Bracketed single-read encoder: fp32 values with on-device draws (other formats and
+  // caller uniforms take the two-pass encoder).  Four launches, no host interaction.
+  if (p->strategy == 3 && !norm_only && !u && fmt == 0 && s >= kSpecMinBits && s <= kSpecMaxBits) {
+    // (the fused PS step too: the pass divides, stores the average and quantises it)
+    SpecArgs sa;
+    a.items = p->d_flat;
+    a.tinfo = p->d_tinfo[1];
+    sa.e = a;
+    sa.begins = p->d_begins;
+    sa.sizes = p->d_sizes;
+    sa.br_items = p->d_spec_br_items;
+    sa.fold_items = p->d_spec_fold_items;
+    sa.seg_part = p->d_spec_seg_part;
+    sa.fold_cnt = p->d_spec_cnt;
+    if (++p->spec_epoch >= 0x80000000u) p->spec_epoch = 1;  // 31-bit tags (the norm granule keeps a status bit)
+    sa.epoch = p->spec_epoch;
+    sa.ngran = p->d_spec_ngran;
+    sa.dbg = p->spec_skip;
+    sa.divisor = divisor;
+    sa.xout = xout;
+    sa.wait_ticks = p->wait_ticks;
+    sa.br = p->d_spec_br;
+    sa.partials = p->d_spec_part;
+    sa.slots = p->d_spec_slots;
+    sa.heads = p->d_spec_heads;
+    sa.recs = p->d_spec_recs;
+    sa.flags = p->d_spec_flags;
+    sa.status = p->d_spec_status;
+    sa.nblocks = p->n_spec_blocks;
+    const dim3 gbr((unsigned)p->n_spec_br), gb((unsigned)p->n_spec_blocks);
+    // p->spec_skip: experiment switch (OMF_SPEC_SKIP, read at plan creation; never set in
+    // production): bit 0 skips the bracket launch (the previous brackets stay), bit 1 the fold,
+    // bit 2 the fix — timings only, the payload is then not the encoder's.
+    if (!(p->spec_skip & 1u)) hipLaunchKernelGGL(qsgd_spec_bracket, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
+    const bool div = divisor != 0.0f;
+    if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    else hipLaunchKernelGGL((qsgd_spec_quant<4, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    if (p->spec_skip & 2u) {  // experiment: no finish launch (timings only)
+      OMF_HIP(hipGetLastError());
+      return OMF_OK;
+    }
+    const int32_t nfold = (int32_t)p->n_spec_fold;
+    const dim3 gfin((unsigned)(nfold + (p->n_spec_blocks + 7) / 8));  // fix: 8 blocks per workgroup
+    if (width == 1)
+      hipLaunchKernelGGL(qsgd_spec_finish<1>, gfin, blk, 0, st, sa, (const SpecFoldItem*)sa.fold_items, nfold,
+                         (const Item*)a.items, (const int64_t*)sa.begins, (const uint32_t*)sa.slots,
+                         (const float4*)sa.recs, (const uint32_t*)sa.heads);
+    else
+      hipLaunchKernelGGL(qsgd_spec_finish<4>, gfin, blk, 0, st, sa, (const SpecFoldItem*)sa.fold_items, nfold,
+                         (const Item*)a.items, (const int64_t*)sa.begins, (const uint32_t*)sa.slots,
+                         (const float4*)sa.recs, (const uint32_t*)sa.heads);
+    OMF_HIP(hipGetLastError());
+    return OMF_OK;
+  }
   // The ring also serves the fused PS step (divide + encode in one launch) under any strategy.
   if ((p->strategy == 2 || divisor != 0.0f) && !norm_only) {
     omf::ring::Args r;
@@ -1574,55 +1709,6 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     const int grid = (int)std::min<int64_t>(p->ring_grid, std::max<int64_t>(p->n_ring, 1));
     if (omf::ring::launch(p->ring_cfg, width, u != nullptr, r, grid, st) != 0)
       return fail(OMF_EHIP, "ring encoder launch failed");
-    OMF_HIP(hipGetLastError());
-    return OMF_OK;
-  }
-  // Bracketed single-read encoder: fp32 values with on-device draws (other formats and
-  // caller uniforms take the two-pass encoder).  Four launches, no host interaction.
-  if (p->strategy == 3 && !norm_only && !u && fmt == 0 && s >= kSpecMinBits && s <= kSpecMaxBits) {
-    SpecArgs sa;
-    a.items = p->d_flat;
-    a.tinfo = p->d_tinfo[1];
-    sa.e = a;
-    sa.begins = p->d_begins;
-    sa.sizes = p->d_sizes;
-    sa.br_items = p->d_spec_br_items;
-    sa.fold_items = p->d_spec_fold_items;
-    sa.seg_part = p->d_spec_seg_part;
-    sa.fold_cnt = p->d_spec_cnt;
-    sa.any_whole = p->d_spec_cnt + p->nt;
-    if (++p->spec_epoch == 0) ++p->spec_epoch;
-    sa.epoch = p->spec_epoch;
-    sa.br = p->d_spec_br;
-    sa.partials = p->d_spec_part;
-    sa.slots = p->d_spec_slots;
-    sa.heads = p->d_spec_heads;
-    sa.recs = p->d_spec_recs;
-    sa.flags = p->d_spec_flags;
-    sa.status = p->d_spec_status;
-    sa.nblocks = p->n_spec_blocks;
-    const dim3 gbr((unsigned)p->n_spec_br), gfo((unsigned)p->n_spec_fold), gb((unsigned)p->n_spec_blocks),
-        gf((unsigned)((p->n_spec_blocks + 7) / 8));  // qsgd_spec_fix: 8 blocks (32 wave slots x 8 threads) per workgroup
-    // p->spec_skip: experiment switch (OMF_SPEC_SKIP, read at plan creation; never set in
-    // production): bit 0 skips the bracket launch (the previous brackets stay), bit 1 the fold,
-    // bit 2 the fix — timings only, the payload is then not the encoder's.
-    if (!(p->spec_skip & 1u)) hipLaunchKernelGGL(qsgd_spec_bracket, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
-    if (width == 1) hipLaunchKernelGGL(qsgd_spec_quant<1>, gb, blk, 0, st, sa, sa.br, sa.begins);
-    else hipLaunchKernelGGL(qsgd_spec_quant<4>, gb, blk, 0, st, sa, sa.br, sa.begins);
-    if (!(p->spec_skip & 2u)) hipLaunchKernelGGL(qsgd_spec_fold, gfo, blk, 0, st, sa);
-    const uint32_t* cst = sa.status;
-    if (p->spec_skip & 4u) {
-      OMF_HIP(hipGetLastError());
-      return OMF_OK;
-    }
-    if (width == 1)
-      hipLaunchKernelGGL(qsgd_spec_fix<1>, gf, blk, 0, st, sa, (const Item*)a.items, (const int64_t*)sa.begins,
-                         (const float*)a.norm_out, (const uint32_t*)sa.slots, cst, (const uint32_t*)sa.any_whole,
-                         (const float4*)sa.recs, (const uint32_t*)sa.heads);
-    else
-      hipLaunchKernelGGL(qsgd_spec_fix<4>, gf, blk, 0, st, sa, (const Item*)a.items, (const int64_t*)sa.begins,
-                         (const float*)a.norm_out, (const uint32_t*)sa.slots, cst, (const uint32_t*)sa.any_whole,
-                         (const float4*)sa.recs, (const uint32_t*)sa.heads);
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }

@@ -10,7 +10,7 @@ from omnifed_amd import codec, shapes  # noqa: E402
 
 dev = torch.device("cuda", 0)
 sizes = [shapes.numel(s) for _, s in shapes.model_shapes(os.environ.get("MODEL", "llama400m"))]
-settings = [0, 1, 2, 4, 6, 7]
+settings = [0, 2, 4, 8]
 plans = {}
 for sk in settings:
     os.environ["OMF_SPEC_SKIP"] = str(sk)
@@ -35,7 +35,7 @@ for rnd in range(7):
         e1.record()
         torch.cuda.synchronize()
         res[sk].append(e0.elapsed_time(e1) / 20)
-names = {0: "all four", 1: "no bracket", 2: "no fold", 4: "no fix", 6: "quant+bracket", 7: "quant only"}
+names = {0: "all three", 2: "bracket+quant", 4: "fix: no stores", 8: "fix: heads only"}
 for sk in settings:
     v = sorted(res[sk])
     print(f"{names[sk]:14s}: median {v[len(v) // 2]:.4f} ms  min {v[0]:.4f}", flush=True)

@@ -93,7 +93,7 @@ def test_batched_decode_errors_in_message_order(gpu):
         decode_updates_dict([odd])
 
 
-@pytest.mark.parametrize("strategy,hold", [("ring", 0), ("ring", 1), ("ordered", 0)])
+@pytest.mark.parametrize("strategy,hold", [("ring", 0), ("ring", 1), ("ordered", 0), ("bracket", 0)])
 def test_fused_ps_apply_encode(gpu, strategy, hold):
     """avg = acc / total (numpy fp32 division, bit for bit) and its payload = encode(avg) with the
     same draws — in one launch (ring) or divide + encode (other strategies).  hold=1: every
