@@ -318,7 +318,7 @@ def main():
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(dom_name, args.config, s)
         if dom_name == "qsgd_spec_all":  # the whole bracketed encode call, timed as one unit
-            dom_name = "omf_qsgd_encode = qsgd_spec_bracket + qsgd_spec_quant + qsgd_spec_fold + qsgd_spec_fix"
+            dom_name = "omf_qsgd_encode = qsgd_spec_bracket + qsgd_spec_quant + qsgd_spec_finish"
         qsgd = {
             "value": world * alg_bytes_step * args.steps / dt / 1e9, "ms_per_step": dt / args.steps * 1e3,
             "alg_bytes_step": alg_bytes_step,

@@ -168,7 +168,7 @@ class Plan:
     @property
     def encoder_kernel(self) -> str:
         """Name of the kernel one encode launch runs (profiling / roofline bookkeeping)."""
-        # the bracketed encoder is four launches (qsgd_spec_bracket, _quant, _fold, _fix): "qsgd_spec_all"
+        # the bracketed encoder is three launches (qsgd_spec_bracket, _quant, _finish): "qsgd_spec_all"
         return {"ring": "qsgd_encode_pc", "bracket": "qsgd_spec_all"}.get(self.strategy, "qsgd_encode_ordered")
 
     def set_ring(self, cfg: int = -1, big_mode: int = -1, gap: int = -2, hold_max: int = -1) -> None:

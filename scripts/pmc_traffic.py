@@ -28,7 +28,7 @@ def load(d, counter):
 
 def short(name):
     for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_decode_flat", "qsgd_quant_sub",
-              "qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_fold", "qsgd_spec_fix",
+              "qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_finish",
               "topk_fused", "topk_prep_hist", "topk_collect", "topk_gather", "topk_scatter_arena"):
         if k in name:
             return k
@@ -48,7 +48,7 @@ def main():
         f = 2 * 1024 * sum(vals) / len(vals)
         w = 1024 * sum(write[name]) / len(write[name])
         res[k] = {"fetch_bytes_corrected": f, "write_bytes": w, "launches": len(vals)}
-    spec = ("qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_fold", "qsgd_spec_fix")
+    spec = ("qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_finish")
     if all(k in res for k in spec):  # the bracketed encoder: one launch of each per encode
         res["qsgd_spec_all"] = {kk: sum(res[k][kk] for k in spec) for kk in ("fetch_bytes_corrected", "write_bytes")}
         res["qsgd_spec_all"]["launches"] = res["qsgd_spec_quant"]["launches"]
