@@ -162,3 +162,27 @@ def test_bracket_large_tensors_sampled(gpu):
     assert st["whole"] == 0 and st["listed"] > 0, st
     x = xd.cpu().numpy()
     _check_against_oracle(plan, x, q, norms, 4, 5, 9)
+
+
+def test_bracket_llama400m_equals_quantiser_given_its_norms(gpu):
+    """Full Llama-400M arena (183 tensors, 401 M elements), s = 4 and s = 3, client weight 3:
+    the bracketed encoder's payload equals the flat quantiser's given the same norms (exact
+    division, the same Philox draws: the element math of every strategy), and its norms agree
+    with the two-pass encoder's to rounding."""
+    sizes = [shapes.numel(sh) for _, sh in shapes.model_shapes("llama400m")]
+    plan = _bracket_plan(gpu, sizes)
+    g = torch.Generator(device=gpu).manual_seed(400)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    for s in (4, 3):
+        q, norms = plan.qsgd_encode(x, s, alpha=3.0, seed=17, offset=s)
+        st = plan.spec_stats()
+        assert st["whole"] == 0 and st["listed"] > 0, st
+        q2, n2 = plan.qsgd_encode(x, s, alpha=3.0, seed=17, offset=s, norm_in=norms)
+        assert torch.equal(n2, norms)
+        for o, n in zip(plan.offsets, plan.sizes):
+            assert torch.equal(q[o:o + n], q2[o:o + n]), (o, n, s)
+        plan.set_encode_strategy("ordered")
+        _, n3 = plan.qsgd_encode(x, s, alpha=3.0, seed=17, offset=s)
+        plan.set_encode_strategy("bracket")
+        torch.testing.assert_close(n3, norms, rtol=2e-6, atol=0)
+        del q, q2
