@@ -167,12 +167,13 @@ int omf_qsgd_norms_ex(omf_plan* plan, const float* x, float alpha, int32_t value
  * Fused PS step: avg_out = acc / divisor (IEEE fp32 division, as the reference's
  * `acc / total_samples` in CentralServerServicer._apply_model_updates,
  * src/omnifed/hybrid/communicator/global_grpc_server.py:155-171) and the QSGD encode of avg
- * for the downlink (_send_current_model, :213-234 -> encode_layer_state) in ONE launch
- * with the ring encoder (acc read once); other strategies run divide + encode.
- * Arguments after avg_out as omf_qsgd_encode (no alpha, no norm_in).  avg_out must be
- * disjoint from acc for the one-launch path (the launch re-reads acc for tensors larger
- * than the on-chip ring); avg_out == acc is accepted and runs as divide (in place) +
- * encode; a partial overlap is OMF_EINVAL.
+ * for the downlink (_send_current_model, :213-234 -> encode_layer_state), acc read once:
+ * the bracketed encoder's pass divides, stores the average and quantises it (strategy 3 at
+ * bit_width 1-4; its rare whole-tensor requantisation reads the average back), or one ring
+ * launch (other plans; tensors larger than the on-chip ring re-read acc); the two-pass
+ * strategies run divide + encode.  Arguments after avg_out as omf_qsgd_encode (no alpha,
+ * no norm_in).  avg_out must be disjoint from acc for the one-launch paths; avg_out == acc
+ * is accepted and runs as divide (in place) + encode; a partial overlap is OMF_EINVAL.
  */
 int omf_ps_apply_encode(omf_plan* plan, const float* acc, float divisor, float* avg_out, int32_t bit_width,
                         const float* u, uint64_t seed, uint64_t offset, void* q_out, float* norm_out, void* stream);
