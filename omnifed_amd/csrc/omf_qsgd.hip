@@ -962,6 +962,100 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_flat(DecArgs a) {
   }
 }
 
+// Decoder over arena-aligned 4 Ki-element blocks: the payload loads depend on blockIdx only,
+// so they go out at once; the block's tensor (binfo: tensor id, bit 31 = the block lies inside
+// it) and its norm are scalar loads in flight with them.  A block that crosses a tensor
+// boundary or padding (at most nt + 1 of them) finds each quad's tensor and writes only its
+// elements.  The streaming shape of scripts/exp/dec_probe.hip (4 rows of 1 Ki elements per
+// block); the item-indexed decoder waited for its item and norm loads before its payload loads.
+constexpr int kDecV = 4;
+constexpr int64_t kDecBlk = (int64_t)kDecV * kThreads * 4;  // 4096 elements
+
+template <int WIDTH, bool ACC, bool POW2>
+__device__ __forceinline__ void dec_quad(const DecArgs& a, int32_t raw[4], float norm, float (&yv)[4]) {
+  int32_t qi[4];
+  if (WIDTH == 1) {
+    qi[0] = (int32_t)(int8_t)(raw[0] & 0xff);
+    qi[1] = (int32_t)(int8_t)((raw[0] >> 8) & 0xff);
+    qi[2] = (int32_t)(int8_t)((raw[0] >> 16) & 0xff);
+    qi[3] = (int32_t)(int8_t)((raw[0] >> 24) & 0xff);
+  } else {
+    qi[0] = raw[0]; qi[1] = raw[1]; qi[2] = raw[2]; qi[3] = raw[3];
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float nq = __fmul_rn(norm, (float)qi[c]);
+    yv[c] = POW2 ? __fmul_rn(nq, a.inv_levels) : nq / a.levels;
+  }
+}
+
+template <int WIDTH, bool ACC, bool POW2>
+__global__ __launch_bounds__(kThreads) void qsgd_decode_arena(DecArgs a, const uint32_t* __restrict__ binfo,
+                                                              const float* __restrict__ norms,
+                                                              const int64_t* __restrict__ begins,
+                                                              const int64_t* __restrict__ sizes, int32_t nt,
+                                                              int64_t qlast) {
+  const int64_t base = (int64_t)blockIdx.x * kDecBlk;
+  int32_t raw[kDecV][WIDTH == 1 ? 1 : 4];
+#pragma unroll
+  for (int k = 0; k < kDecV; ++k) {  // unconditional (clamped) nontemporal loads
+    const int64_t e = min(base + 4 * ((int64_t)k * kThreads + threadIdx.x), qlast);
+    if (WIDTH == 1) {
+      raw[k][0] = __builtin_nontemporal_load(reinterpret_cast<const int32_t*>(reinterpret_cast<const int8_t*>(a.q) + e));
+    } else {
+      const i32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(reinterpret_cast<const int32_t*>(a.q) + e));
+      raw[k][0] = t[0]; raw[k][1] = t[1]; raw[k][2] = t[2]; raw[k][3] = t[3];
+    }
+  }
+  const uint32_t info = binfo[blockIdx.x];
+  const int32_t t0 = (int32_t)(info & 0x7fffffffu);
+  if (info >> 31) {  // the whole block lies inside tensor t0
+    const float norm = norms[t0];
+#pragma unroll
+    for (int k = 0; k < kDecV; ++k) {
+      const int64_t e = base + 4 * ((int64_t)k * kThreads + threadIdx.x);
+      float yv[4];
+      dec_quad<WIDTH, ACC, POW2>(a, raw[k], norm, yv);
+      float4 o = make_float4(yv[0], yv[1], yv[2], yv[3]);
+      if (ACC) {
+        const f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(a.y + e));
+        o.x = __fadd_rn(pv[0], o.x); o.y = __fadd_rn(pv[1], o.y);
+        o.z = __fadd_rn(pv[2], o.z); o.w = __fadd_rn(pv[3], o.w);
+      }
+      store_nt(a.y + e, o);
+    }
+    return;
+  }
+  // boundary block: each quad's tensor, element by element
+#pragma unroll
+  for (int k = 0; k < kDecV; ++k) {
+    const int64_t e = base + 4 * ((int64_t)k * kThreads + threadIdx.x);
+    int32_t t = t0;
+    while (t + 1 < nt && e >= begins[t + 1]) ++t;
+    const int64_t tb = begins[t], te = tb + sizes[t];
+    if (e + 3 < tb || e >= te) continue;  // padding (offsets are multiples of 4: a quad never
+                                          // starts before its tensor and ends inside it)
+    int32_t rr[4] = {raw[k][0], WIDTH == 1 ? 0 : raw[k][1], WIDTH == 1 ? 0 : raw[k][2], WIDTH == 1 ? 0 : raw[k][3]};
+    if (e + 4 > te) {  // the tensor's partial last quad: its bytes only (the payload may end here)
+      if (WIDTH == 1) {
+        const int8_t* q8 = reinterpret_cast<const int8_t*>(a.q);
+        uint32_t w = 0;
+        for (int c = 0; c < 3; ++c)
+          if (e + c < te) w |= (uint32_t)(uint8_t)q8[e + c] << (8 * c);
+        rr[0] = (int32_t)w;
+      } else {
+        const int32_t* q32 = reinterpret_cast<const int32_t*>(a.q);
+        for (int c = 0; c < 3; ++c) rr[c] = e + c < te ? q32[e + c] : 0;
+        rr[3] = 0;
+      }
+    }
+    float yv[4];
+    dec_quad<WIDTH, ACC, POW2>(a, rr, norms[t], yv);
+    for (int c = 0; c < 4; ++c)
+      if (e + c < te) a.y[e + c] = ACC ? __fadd_rn(a.y[e + c], yv[c]) : yv[c];
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void div_f32_kernel(float* __restrict__ y, int64_t n, float d) {
   const int64_t stride = (int64_t)gridDim.x * kThreads * 4;
   for (int64_t e = 4 * ((int64_t)blockIdx.x * kThreads + threadIdx.x); e < n; e += stride) {
@@ -1031,6 +1125,9 @@ struct omf_plan {
   uint32_t* d_spec_slots = nullptr;
   uint32_t* d_spec_heads = nullptr;
   float4* d_spec_recs = nullptr;  // listed quads' x and draws (32 B each)
+  // arena-aligned decoder: per 4 Ki block, tensor id | (1 << 31 when inside it)
+  int64_t n_dec_blocks = 0;
+  uint32_t* d_dec_binfo = nullptr;
   uint32_t* d_spec_flags = nullptr;
   uint32_t* d_spec_status = nullptr;
   // Launches that use the sync block / granules are ordered across streams: a launch on a
@@ -1274,6 +1371,19 @@ static int upload_plan(omf_plan* p) {
     seg_base += nsegs;
   }
   static_assert(kSub == 4 * kSpecBlk, "four spec blocks per flat item");
+  // decoder block table: the last tensor starting at or before the block, and whether the
+  // block lies entirely inside it
+  std::vector<uint32_t> binfo((size_t)((p->arena_end + kDecBlk - 1) / kDecBlk));
+  {
+    int32_t t = 0;
+    for (size_t k = 0; k < binfo.size(); ++k) {
+      const int64_t base = (int64_t)k * kDecBlk;
+      while (t + 1 < p->nt && p->offsets[t + 1] <= base) ++t;
+      const bool inside = p->offsets[t] <= base && base + kDecBlk <= p->offsets[t] + p->sizes[t];
+      binfo[k] = (uint32_t)t | (inside ? 0x80000000u : 0u);
+    }
+  }
+  p->n_dec_blocks = (int64_t)binfo.size();
   p->n_spec_blocks = 4 * (int64_t)flat.size();
   p->n_spec_br = (int64_t)br_items.size();
   p->n_spec_fold = (int64_t)fold_items.size();
@@ -1308,6 +1418,7 @@ static int upload_plan(omf_plan* p) {
   const size_t o_sp_part = o; o = round16(o + 8 * (size_t)kWaves * (size_t)p->n_spec_blocks);
   const size_t o_sp_slots = o; o = round16(o + 4 * (size_t)kSpecSlot * (size_t)p->n_spec_blocks);
   const size_t o_sp_heads = o; o = round16(o + 4 * (size_t)kWaves * (size_t)p->n_spec_blocks);
+  const size_t o_binfo = o; o = round16(o + 4 * binfo.size());
   const size_t o_sp_recs = o; o = round16(o + 32 * (size_t)kWaves * kSpecPerWave * (size_t)p->n_spec_blocks);
   const size_t o_sp_flags = o; o = round16(o + 4 * (size_t)p->nt);
   const size_t o_sp_status = o; o = round16(o + 4 * (size_t)p->nt);
@@ -1342,6 +1453,8 @@ static int upload_plan(omf_plan* p) {
   p->d_spec_part = reinterpret_cast<uint64_t*>(base + o_sp_part);
   p->d_spec_slots = reinterpret_cast<uint32_t*>(base + o_sp_slots);
   p->d_spec_heads = reinterpret_cast<uint32_t*>(base + o_sp_heads);
+  p->d_dec_binfo = reinterpret_cast<uint32_t*>(base + o_binfo);
+  OMF_HIP(hipMemcpy(p->d_dec_binfo, binfo.data(), 4 * binfo.size(), hipMemcpyHostToDevice));
   p->d_spec_recs = reinterpret_cast<float4*>(base + o_sp_recs);
   p->d_spec_flags = reinterpret_cast<uint32_t*>(base + o_sp_flags);
   p->d_spec_status = reinterpret_cast<uint32_t*>(base + o_sp_status);
@@ -1803,9 +1916,19 @@ int omf_qsgd_decode(omf_plan* p, const void* q, int32_t width, int32_t levels, c
   a.levels = (float)levels;
   const bool pow2 = (levels & (levels - 1)) == 0;
   a.inv_levels = pow2 ? 1.0f / (float)levels : 0.0f;  // exact for a power of two
-  const dim3 grid((unsigned)p->n_flat), blk(kThreads);
+  const dim3 grid((unsigned)p->n_dec_blocks), blk(kThreads);
   hipStream_t st = (hipStream_t)stream;
-#define OMF_DEC(W, A, P) hipLaunchKernelGGL((qsgd_decode_flat<W, A, P>), grid, blk, 0, st, a)
+  // the last whole quad of the payload the caller holds (width 8: round_up(arena_end, 4) bytes
+  // are not promised, so a clamped load never passes the last full quad)
+  const int64_t qlast = (p->arena_end & ~(int64_t)3) - 4;  // < 0 only for arenas of < 4 elements
+#define OMF_DEC(W, A, P)                                                                                         \
+  do {                                                                                                           \
+    if (qlast >= 0)                                                                                              \
+      hipLaunchKernelGGL((qsgd_decode_arena<W, A, P>), grid, blk, 0, st, a, (const uint32_t*)p->d_dec_binfo,     \
+                         norm, (const int64_t*)p->d_begins, (const int64_t*)p->d_sizes, p->nt, qlast);           \
+    else /* a payload of < 4 elements: the item decoder's byte loads */                                          \
+      hipLaunchKernelGGL((qsgd_decode_flat<W, A, P>), dim3((unsigned)p->n_flat), blk, 0, st, a);                \
+  } while (0)
   if (width == 8) {
     if (accumulate) { if (pow2) OMF_DEC(1, true, true); else OMF_DEC(1, true, false); }
     else { if (pow2) OMF_DEC(1, false, true); else OMF_DEC(1, false, false); }
