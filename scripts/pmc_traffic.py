@@ -27,7 +27,8 @@ def load(d, counter):
 
 
 def short(name):
-    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_decode_flat", "qsgd_quant_sub",
+    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_decode_flat", "qsgd_decode_arena",
+              "qsgd_quant_sub",
               "qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_finish",
               "topk_fused", "topk_prep_hist", "topk_collect", "topk_gather", "topk_scatter_arena"):
         if k in name:
