@@ -186,3 +186,45 @@ def test_bracket_llama400m_equals_quantiser_given_its_norms(gpu):
         plan.set_encode_strategy("bracket")
         torch.testing.assert_close(n3, norms, rtol=2e-6, atol=0)
         del q, q2
+
+
+@pytest.mark.parametrize("s", [4, 8])
+def test_arena_decoder_boundaries_and_padding(gpu, s):
+    """qsgd_decode_arena on a layout with tiny tensors, odd sizes and caller-chosen gaps: every
+    tensor element equals the oracle's decode (and the accumulate mode adds it), and padding
+    between tensors is never written (a canary survives)."""
+    rng = np.random.default_rng(11 + s)
+    sizes = [1, 3, 5, 64, 1000, 4095, 4097, 10, 70001, 2, 16384, 9]
+    offsets, cur = [], 0
+    for n in sizes:
+        cur = (cur + 3) // 4 * 4 + 4 * int(rng.integers(0, 600))  # starts: multiples of 4, random gaps
+        offsets.append(cur)
+        cur += n
+    plan = codec.Plan(sizes, offsets=offsets, device=gpu)
+    L = 2 ** s
+    w = 8 if L <= 127 else 32
+    qdt = np.int8 if w == 8 else np.int32
+    q = np.zeros(plan.payload_elems(w), qdt)
+    norms = rng.random(len(sizes)).astype(np.float32) + 0.5
+    want = {}
+    for t, (o, n) in enumerate(zip(offsets, sizes)):
+        q[o:o + n] = rng.integers(-L, L + 1, n).astype(qdt)
+        want[t] = oracle.qsgd_dequantize(torch.from_numpy(q[o:o + n].astype(np.int64)), float(norms[t]), L,
+                                         (n,)).numpy()
+    qd = torch.from_numpy(q).to(gpu)
+    nd = torch.from_numpy(norms).to(gpu)
+    canary = -12345.5
+    y = torch.full((plan.arena_end,), canary, dtype=torch.float32, device=gpu)
+    plan.qsgd_decode(qd, w, L, nd, y_out=y)
+    yh = y.cpu().numpy()
+    mask = np.ones(plan.arena_end, bool)
+    for t, (o, n) in enumerate(zip(offsets, sizes)):
+        assert yh[o:o + n].tobytes() == want[t].astype(np.float32).tobytes(), t
+        mask[o:o + n] = False
+    assert (yh[mask] == canary).all()  # padding untouched
+    # accumulate: y += decode, padding still untouched
+    plan.qsgd_decode(qd, w, L, nd, y_out=y, accumulate=True)
+    yh2 = y.cpu().numpy()
+    for t, (o, n) in enumerate(zip(offsets, sizes)):
+        assert yh2[o:o + n].tobytes() == (want[t].astype(np.float32) + want[t].astype(np.float32)).tobytes(), t
+    assert (yh2[mask] == canary).all()
