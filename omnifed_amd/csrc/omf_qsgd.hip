@@ -455,6 +455,7 @@ struct SpecArgs {
   uint64_t wait_ticks;     // bound of a fix thread's wait for its tensor's norm (100 MHz ticks)
   uint32_t dbg;            // experiment switches (OMF_SPEC_SKIP bits 2-3), 0 in production
   float divisor;           // fused PS step: x := x / divisor (IEEE), written to xout; 0 = none
+  float zsig;              // bracket half-width in standard deviations of the sample estimate (6)
   float* xout;
   uint32_t epoch;          // per-launch tag (never 0)
   int64_t nblocks;
@@ -581,7 +582,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     const double Rd = (double)R, m = S1 / Rd;
     const double var = fmax(0.0, (S2 - Rd * m * m) / (Rd - 1.0));
     ss = S1 * ((double)n / ((double)kSpecRun * Rd));
-    k = 6.0 * sqrt(var / Rd) / m + 0x1p-10;  // 6 sigma of the run-sum estimate + 0.1 %
+    k = (double)a.zsig * sqrt(var / Rd) / m + 0x1p-10;  // 6 sigma of the run-sum estimate + 0.1 %
   }
   SpecBracket o{0.f, 0.f, 0.f, 0.f, 1u, {0u, 0u, 0u}};  // deferred: c = 0 decides every level as 0
   if (ss > 0.0 && ss < 1e300 && k < 0.5) {
@@ -1119,6 +1120,7 @@ struct omf_plan {
   uint32_t* d_spec_cnt = nullptr;  // fold_cnt x nt
   uint32_t spec_epoch = 0;
   uint32_t spec_skip = 0;  // experiment switch (OMF_SPEC_SKIP)
+  float spec_zsig = 6.0f;  // experiment switch (OMF_SPEC_ZSIG): the bracket's width in sigmas
   SpecBracket* d_spec_br = nullptr;
   uint64_t* d_spec_ngran = nullptr;  // per tensor {epoch << 1 | bad, norm} granules of the fold
   uint64_t* d_spec_part = nullptr;
@@ -1541,6 +1543,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     if (const char* gp = getenv("OMF_RING_GAP")) p->ring_gap = atoll(gp);
     if (const char* dg = getenv("OMF_RING_DBG")) p->ring_dbg = (uint32_t)atoi(dg);
     if (const char* sk = getenv("OMF_SPEC_SKIP")) p->spec_skip = (uint32_t)atoi(sk);
+    if (const char* zs = getenv("OMF_SPEC_ZSIG")) p->spec_zsig = std::max(1.0f, (float)atof(zs));
     // Default strategy by arena size: the bracketed single-read encoder from 2^25 elements
     // (Llama-400M 0.386 ms against the two-pass 0.59 and the ring 0.63; Llama-150M 0.25 against
     // 0.35), the ring below (ResNet-18: 0.032 ms against 0.08 for the bracket's four launches).
@@ -1760,6 +1763,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.epoch = p->spec_epoch;
     sa.ngran = p->d_spec_ngran;
     sa.dbg = p->spec_skip;
+    sa.zsig = p->spec_zsig;
     sa.divisor = divisor;
     sa.xout = xout;
     sa.wait_ticks = p->wait_ticks;
