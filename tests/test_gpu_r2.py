@@ -82,7 +82,7 @@ def test_ring_debug_timing_modes_complete(gpu, dbg, monkeypatch):
             assert torch.equal(nd, n_ref) if hold == 0 else torch.allclose(nd, n_ref, rtol=2e-6, atol=0)
 
 
-@pytest.mark.parametrize("strategy", ["ordered", "ring"])
+@pytest.mark.parametrize("strategy", ["ordered", "ring", "bracket"])
 def test_encodes_on_two_streams_are_ordered(gpu, strategy):
     """One plan, launches alternating between two streams with no host synchronisation: each
     result equals the sequential one (the plan orders a launch after the previous stream's)."""
