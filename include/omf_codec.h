@@ -51,7 +51,7 @@ extern "C" {
 
 typedef struct omf_plan omf_plan;
 
-/* ABI version (major*100 + minor): 103. */
+/* ABI version (major*100 + minor): 104. */
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -73,10 +73,25 @@ int omf_plan_destroy(omf_plan* plan);
 /* Number of workgroups one encode launch uses (diagnostics / roofline bookkeeping). */
 int64_t omf_plan_encode_items(const omf_plan* plan);
 /* Synchronise `stream` and report what the plan's launches since the previous check hit:
- * OMF_ETIMEOUT when an on-chip hand-off wait of the ring encoder exceeded its bound (that
- * workgroup aborted and drained: the payload is invalid); 1 (results still exact) when an
- * encoder recomputed a norm after a bounded wait; 0 otherwise.  Clears what it reports. */
+ * OMF_ETIMEOUT when an on-chip wait exceeded its bound (a ring encoder hand-off: that
+ * workgroup aborted and drained; a bracketed-encoder fix thread waiting for its tensor's norm:
+ * the quad kept its guess) — the payload of that launch is invalid; 1 (results still exact)
+ * when an encoder recomputed a norm after a bounded wait; 0 otherwise.  Clears what it
+ * reports.  The Python layer calls it at the synchronisation each product path already makes
+ * (the norms' device-to-host copy) and raises RuntimeError on OMF_ETIMEOUT, so the PS turns
+ * it into UpdateResponse(success=False) like any codec exception
+ * (src/omnifed/hybrid/communicator/global_grpc_server.py:138-145).  Every bound needs both
+ * its wall-clock time (20 ms) and a minimum number of polls, so a queue context switch does
+ * not fake an expiry. */
 int omf_plan_check(omf_plan* plan, void* stream);
+/* Test / experiment hook, never set in production (all 0): switches that change what an
+ * encode writes.  ring_dbg (ring encoder): 1 no norm wait (norm := 1), 2 no quantisation,
+ * 4 phase cycle counters, 8 slots never marked loaded (every hand-off wait of the poller
+ * expires: OMF_ETIMEOUT).  spec_dbg (bracketed encoder): 1 no bracket launch, 2 no finish
+ * launch, 4 no fix stores, 8 no fix, 16 no fold (every fix wait expires: OMF_ETIMEOUT).
+ * lds_wait_us > 0 replaces the ring's 20 ms hand-off bound (0 restores it); the norm-wait
+ * bound is omf_plan_set_resident_capacity's wait_us. */
+int omf_plan_set_debug(omf_plan* plan, uint32_t ring_dbg, uint32_t spec_dbg, int64_t lds_wait_us);
 /* Encoder strategy: 0 = register-resident items for tensors of at most
  * omf_plan_resident_capacity() items (x read once; the workgroup holds its 16 Ki elements
  * while the tensor norm is published) and two-pass items for larger tensors;
@@ -109,8 +124,8 @@ int omf_plan_set_ring(omf_plan* plan, int32_t cfg, int32_t big_mode, int64_t gap
 /* Ring encoder facts: out[0] grid, out[1] chunk elements, out[2] items, out[3] hold limit
  * (chunks), out[4] tensors taking two passes, out[5] configuration. */
 int omf_plan_ring_info(const omf_plan* plan, int64_t* out6);
-/* Experiment hook: per-phase cycle totals of ring launches made with OMF_RING_DBG bit 4
- * set in the environment at plan creation (zeros otherwise); read and reset. */
+/* Experiment hook: per-phase cycle totals of ring launches made with omf_plan_set_debug
+ * ring bit 4 (zeros otherwise); read and reset. */
 int omf_plan_ring_profile(omf_plan* plan, int64_t* out16);
 /* Largest tensor (in 16 Ki-element items) that takes the register-resident path: half the
  * encoder's co-resident workgroups (occupancy x CUs). */

@@ -42,6 +42,7 @@ SIGNATURES = {
     "omf_plan_resident_capacity": (_c_i64, [_c_p]),
     "omf_plan_set_resident_capacity": (ctypes.c_int, [_c_p, _c_i64, _c_i64]),
     "omf_plan_set_ring": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i64, _c_i64]),
+    "omf_plan_set_debug": (ctypes.c_int, [_c_p, ctypes.c_uint32, ctypes.c_uint32, _c_i64]),
     "omf_plan_ring_info": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64)]),
     "omf_plan_spec_stats": (ctypes.c_int, [_c_p, _c_p, ctypes.POINTER(_c_i64)]),
     "omf_plan_ring_profile": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64)]),

@@ -18,7 +18,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
-from ._lib import check, lib
+from ._lib import CodecError, check, lib  # noqa: F401  (CodecError: raised by check())
 
 ALIGN_ELEMS = 64
 
@@ -142,13 +142,20 @@ class Plan:
         return int(lib().omf_plan_encode_items(self._h))
 
     def check(self, stream: Optional[int] = None) -> bool:
-        """Synchronise; raise on an in-kernel timeout.  Returns False if the resident encoder
-        had to recompute a norm (results exact, but the grid was not co-resident)."""
+        """Synchronise; raise ``CodecError`` (a ``RuntimeError``) on an in-kernel timeout (the
+        payload of that launch is invalid).  Returns False if an encoder had to recompute a
+        norm (results exact, but the grid was not co-resident).  Every product entry point
+        calls it at the synchronisation it already makes."""
         rc = lib().omf_plan_check(self._h, ctypes.c_void_p(stream if stream is not None else _stream(self.device)))
         if rc == 1:
             return False
         check(rc, "omf_plan_check")
         return True
+
+    def set_debug(self, ring: int = 0, spec: int = 0, lds_wait_us: int = 0) -> None:
+        """Test / experiment hook (omf_plan_set_debug): switches that change what an encode
+        writes (never set in production); all zero restores the production behaviour."""
+        check(lib().omf_plan_set_debug(self._h, int(ring), int(spec), int(lds_wait_us)), "omf_plan_set_debug")
 
     @property
     def resident_capacity(self) -> int:
@@ -176,7 +183,7 @@ class Plan:
         check(lib().omf_plan_set_ring(self._h, int(cfg), int(big_mode), int(gap), int(hold_max)), "omf_plan_set_ring")
 
     def ring_profile(self) -> List[int]:
-        """Experiment hook: per-phase cycle totals (OMF_RING_DBG bit 4), read and reset."""
+        """Experiment hook: per-phase cycle totals (set_debug ring bit 4), read and reset."""
         out = (ctypes.c_int64 * 16)()
         check(lib().omf_plan_ring_profile(self._h, out), "omf_plan_ring_profile")
         return [int(v) for v in out]

@@ -422,8 +422,8 @@ struct SpecBracket {
   uint32_t pad[3];
 };
 
-// Bracket work item: part `part` of `nparts` of tensor `tensor` (a sampled tensor's runs are
-// split over up to 4 workgroups; a small tensor is one exact part).
+// Bracket work item: one per tensor, one workgroup each (qsgd_spec_bracket writes the
+// tensor's bracket from that workgroup's sums alone; upload_plan builds exactly one).
 struct SpecBrItem {
   int64_t begin, n;  // the tensor's arena range
   int64_t base;      // stratum length n / R (R = runs of the tensor); rem = n % R strata are one longer
@@ -453,7 +453,7 @@ struct SpecArgs {
   uint32_t* status;        // per tensor: 0 = listed quads only, 1 = requantise whole
   uint64_t* ngran;         // per tensor: {epoch << 1 | bad, norm} published by the fold
   uint64_t wait_ticks;     // bound of a fix thread's wait for its tensor's norm (100 MHz ticks)
-  uint32_t dbg;            // experiment switches (OMF_SPEC_SKIP bits 2-3), 0 in production
+  uint32_t dbg;            // test / experiment switches (omf_plan_set_debug spec bits 2-4), 0 in production
   float divisor;           // fused PS step: x := x / divisor (IEEE), written to xout; 0 = none
   float zsig;              // bracket half-width in standard deviations of the sample estimate (6)
   float* xout;
@@ -780,21 +780,26 @@ __device__ void spec_fold(const SpecArgs& a, const SpecFoldItem& fi) {
 }
 
 // The tensor's norm and status as its fold published them in this launch (bounded; the fold
-// workgroups are dispatched before every fix workgroup).  false: timed out (err bit 4 set,
-// reported as OMF_ETIMEOUT by omf_plan_check).
+// workgroups are dispatched before every fix workgroup and never wait, so the bound is only a
+// guard against a logic error).  false: timed out (err bit 4 set, reported as OMF_ETIMEOUT by
+// omf_plan_check, which every product entry point calls).  The bound needs the wall-clock
+// time AND a minimum number of polls, so a context switch of the queue (the clock runs on
+// while the wave is saved) cannot fake an expiry.
 __device__ __forceinline__ bool spec_norm_wait(const SpecArgs& a, int32_t t, float& norm, bool& bad) {
   uint64_t g = ld_agent(&a.ngran[t]);
   if ((uint32_t)(g >> 33) != a.epoch) {
     // exponential back-off: every polling wave reads one of 183-odd granules, and tight
     // polling of a few lines by tens of thousands of waves congests them
     const uint64_t t0 = wall_clock64();
+    const uint64_t min_polls = a.wait_ticks >> 10;  // a back-off poll is <= ~200 ticks
+    uint64_t polls = 0;
     for (int k = 0;; k = min(k + 1, 6)) {
       if (k < 2) __builtin_amdgcn_s_sleep(4);
       else if (k < 4) __builtin_amdgcn_s_sleep(16);
       else __builtin_amdgcn_s_sleep(64);
       g = ld_agent(&a.ngran[t]);
       if ((uint32_t)(g >> 33) == a.epoch) break;
-      if (wall_clock64() - t0 > a.wait_ticks) {
+      if (++polls > min_polls && wall_clock64() - t0 > a.wait_ticks) {
         __hip_atomic_fetch_or(a.e.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return false;
       }
@@ -819,7 +824,7 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
                                                              const float4* __restrict__ recs,
                                                              const uint32_t* __restrict__ heads) {
   if ((int32_t)blockIdx.x < nfold) {
-    spec_fold(a, fold_items[blockIdx.x]);
+    if (!(a.dbg & 16u)) spec_fold(a, fold_items[blockIdx.x]);  // test hook: no fold, the fix waits expire
     return;
   }
   constexpr int LPS = 8;                          // threads per wave slot
@@ -1083,7 +1088,8 @@ struct omf_plan {
   int64_t cap = 0;               // tensors of <= cap items take the register-resident path
   int32_t strategy = 2;          // 0 register-resident + two-pass, 1 ticket-ordered two-pass, 2 single-read ring,
                                  // 3 bracketed single-read (default by size: omf_plan_create)
-  uint64_t wait_ticks = kWaitTicks;
+  uint64_t wait_ticks = kWaitTicks;      // norm waits (ring: expiry recomputes; bracketed fix: expiry fails)
+  uint64_t lds_wait_ticks = kWaitTicks;  // the ring's on-chip hand-off waits (expiry aborts the workgroup)
   uint32_t epoch = 0;            // last granule tag used (host-side launch counter)
   int32_t ev = 8;                // encode rows per thread (sub-chunk = ev * 1024 elements): 8 measured
                                  // faster than 16 for the two-pass encoder (0.596 vs 0.606 ms, Llama-400M)
@@ -1104,7 +1110,7 @@ struct omf_plan {
   int32_t ring_big_mode = 1;     // 0: QUANT chunks of a large tensor ring_gap items after its NORM chunks; 1: NORM first, QUANT last
   int64_t ring_gap = -1;         // items (-1: one grid)
   int64_t ring_hold_override = 0;  // > 0: hold limit in chunks (tests)
-  uint32_t ring_dbg = 0;           // experiment switches (OMF_RING_DBG), never set in production
+  uint32_t ring_dbg = 0;           // test / experiment switches (omf_plan_set_debug), 0 in production
   uint32_t ring_epoch = 0;
   int64_t n_ring = 0, n_ring_gran = 0, ring_hold_max = 0, ring_two_pass = 0;
   omf::ring::Item* d_ring = nullptr;
@@ -1119,7 +1125,7 @@ struct omf_plan {
   uint64_t* d_spec_seg_part = nullptr;
   uint32_t* d_spec_cnt = nullptr;  // fold_cnt x nt
   uint32_t spec_epoch = 0;
-  uint32_t spec_skip = 0;  // experiment switch (OMF_SPEC_SKIP)
+  uint32_t spec_skip = 0;  // test / experiment switches (omf_plan_set_debug), 0 in production
   float spec_zsig = 6.0f;  // experiment switch (OMF_SPEC_ZSIG): the bracket's width in sigmas
   SpecBracket* d_spec_br = nullptr;
   uint64_t* d_spec_ngran = nullptr;  // per tensor {epoch << 1 | bad, norm} granules of the fold
@@ -1351,8 +1357,9 @@ static int upload_plan(omf_plan* p) {
   p->n_ring = (int64_t)rseq.size();
   // Flat items (decode, norm-supplied quantise, Top-K passes): one 16 Ki sub-chunk each,
   // the fastest decode granularity measured (profiles/r01_notes.md).
-  // Bracketed encoder tables: bracket parts (up to 4 per sampled tensor) and fold segments of
-  // kSpecSeg wave partials (4 per 4 Ki block, kSub / kSpecBlk = 4 blocks per flat item).
+  // Bracketed encoder tables: one bracket item per tensor (one workgroup writes its bracket)
+  // and fold segments of kSpecSeg wave partials (4 per 4 Ki block, kSub / kSpecBlk = 4 blocks
+  // per flat item).
   std::vector<SpecBrItem> br_items;
   std::vector<SpecFoldItem> fold_items;
   int32_t seg_base = 0;
@@ -1541,8 +1548,13 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     if (const char* rc = getenv("OMF_RING_CFG")) p->ring_cfg = std::max(0, std::min(atoi(rc), omf::ring::num_configs() - 1));
     if (const char* bm = getenv("OMF_RING_BIG")) p->ring_big_mode = atoi(bm) == 1 ? 1 : 0;
     if (const char* gp = getenv("OMF_RING_GAP")) p->ring_gap = atoll(gp);
+    // Switches that change what an encode writes (skipped launches, no quantisation) are never
+    // read from the environment of a release build: tests set them per plan (omf_plan_set_debug);
+    // experiment builds (-DOMF_EXPERIMENTS, scripts/exp/build_variants.sh) also take them here.
+#ifdef OMF_EXPERIMENTS
     if (const char* dg = getenv("OMF_RING_DBG")) p->ring_dbg = (uint32_t)atoi(dg);
     if (const char* sk = getenv("OMF_SPEC_SKIP")) p->spec_skip = (uint32_t)atoi(sk);
+#endif
     if (const char* zs = getenv("OMF_SPEC_ZSIG")) p->spec_zsig = std::max(1.0f, (float)atof(zs));
     // Default strategy by arena size: the bracketed single-read encoder from 2^25 elements
     // (Llama-400M 0.386 ms against the two-pass 0.59 and the ring 0.63; Llama-150M 0.25 against
@@ -1638,6 +1650,16 @@ int omf_plan_set_resident_capacity(omf_plan* plan, int64_t cap, int64_t wait_us)
   return OMF_OK;
 }
 
+int omf_plan_set_debug(omf_plan* plan, uint32_t ring_dbg, uint32_t spec_dbg, int64_t lds_wait_us) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (lds_wait_us < 0) return fail(OMF_EINVAL, "lds_wait_us must be >= 0");
+  if ((ring_dbg & ~15u) || (spec_dbg & ~31u)) return fail(OMF_EINVAL, "omf_plan_set_debug: unknown switch bits");
+  plan->ring_dbg = ring_dbg;
+  plan->spec_skip = spec_dbg;
+  plan->lds_wait_ticks = lds_wait_us > 0 ? (uint64_t)lds_wait_us * 100ull : kWaitTicks;
+  return OMF_OK;
+}
+
 int omf_plan_spec_stats(omf_plan* plan, void* stream, int64_t* out4) {
   if (!plan || !out4) return fail(OMF_EINVAL, "omf_plan_spec_stats: NULL argument");
   DeviceGuard g(plan->device);
@@ -1673,8 +1695,9 @@ int omf_plan_check(omf_plan* plan, void* stream) {
   OMF_HIP(hipMemcpy(&err, plan->d_sync + 4, 4, hipMemcpyDeviceToHost));
   if (err) OMF_HIP(hipMemset(plan->d_sync + 4, 0, 4));  // report each event once
   if (err & 4u)
-    return fail(OMF_ETIMEOUT, "ring encoder: an on-chip hand-off wait exceeded its bound and the workgroup "
-                              "aborted; the payload of that launch is invalid");
+    return fail(OMF_ETIMEOUT, "QSGD encoder: an on-chip wait exceeded its bound (a ring hand-off, or a "
+                              "bracketed-encoder fix waiting for its tensor's norm) and was abandoned; the "
+                              "payload of that launch is invalid");
   if (err & 2u) {
     set_error("encoder recomputed a norm after a bounded wait (items not co-resident); results are exact");
     return 1;
@@ -1776,9 +1799,9 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.status = p->d_spec_status;
     sa.nblocks = p->n_spec_blocks;
     const dim3 gbr((unsigned)p->n_spec_br), gb((unsigned)p->n_spec_blocks);
-    // p->spec_skip: experiment switch (OMF_SPEC_SKIP, read at plan creation; never set in
-    // production): bit 0 skips the bracket launch (the previous brackets stay), bit 1 the fold,
-    // bit 2 the fix — timings only, the payload is then not the encoder's.
+    // p->spec_skip: test / experiment switches (omf_plan_set_debug; 0 in production): bit 0
+    // skips the bracket launch (the previous brackets stay), bit 1 the finish launch, bits 2/3
+    // the fix stores / the fix, bit 4 the fold — the payload is then not the encoder's.
     if (!(p->spec_skip & 1u)) hipLaunchKernelGGL(qsgd_spec_bracket, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
     const bool div = divisor != 0.0f;
     if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
@@ -1820,7 +1843,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     if (++p->ring_epoch == 0) ++p->ring_epoch;
     r.epoch = p->ring_epoch;
     r.wait_ticks = p->wait_ticks;
-    r.lds_wait_ticks = kWaitTicks;
+    r.lds_wait_ticks = p->lds_wait_ticks;
     r.dbg = p->ring_dbg;
     r.prof = p->d_ring_prof;
     const int grid = (int)std::min<int64_t>(p->ring_grid, std::max<int64_t>(p->n_ring, 1));

@@ -261,12 +261,15 @@ __shared__ uint32_t g_wg_abort;
 __device__ __forceinline__ bool wg_aborted() { return ufirst((int)lds_ld(&g_wg_abort)) != 0; }
 
 // Wait until the LDS word *p >= v.  Bounded: the clock is read only every 64 sleeps, so
-// the common short wait costs one LDS load per poll; past a.wait_ticks (20 ms) the
+// the common short wait costs one LDS load per poll; past a.lds_wait_ticks (20 ms) the
 // workgroup aborts instead of hanging the GPU (a hand-off logic error, never expected).
-// a.lds_wait_ticks is fixed (20 ms); the tunable a.wait_ticks bounds only norm waits.
+// The bound needs both the wall-clock time AND a minimum number of polls (about a quarter
+// of the bound spent polling): a context switch of the queue (CWSR) advances the clock
+// while the wave is saved, and must not look like a stuck hand-off.
 __device__ __forceinline__ void lds_wait_ge(const Args& a, const uint32_t* p, uint32_t v) {
   if (ufirst((int)lds_ld(p)) < (int)v) {
     uint64_t t0 = 0;
+    const uint64_t min_polls = a.lds_wait_ticks >> 5;  // a poll is >= ~7 ticks (s_sleep 1 + an LDS load)
     for (uint32_t i = 1;; ++i) {
       __builtin_amdgcn_s_sleep(1);
       if (ufirst((int)lds_ld(p)) >= (int)v) break;
@@ -275,7 +278,7 @@ __device__ __forceinline__ void lds_wait_ge(const Args& a, const uint32_t* p, ui
         const uint64_t now = wall_clock64();
         if (t0 == 0) {
           t0 = now;
-        } else if (now - t0 > a.lds_wait_ticks) {
+        } else if (now - t0 > a.lds_wait_ticks && i > min_polls) {
           lds_st(&g_wg_abort, 1u);
           if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(a.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           break;
@@ -569,7 +572,9 @@ __global__ __launch_bounds__(1024, 4) void qsgd_encode_pc(Args a, const Item* __
         if (old == LW - 1 && lane == 0) {
           lds_st(&fill[s], 0u);
           lds_drain();
-          lds_st(&loaded[s], (uint32_t)(k + 1));
+          // test hook (omf_plan_set_debug ring bit 8): the slot is never marked loaded, so the
+          // poller's hand-off wait expires and the workgroup aborts (err bit 4, OMF_ETIMEOUT)
+          if (!(a.dbg & 8)) lds_st(&loaded[s], (uint32_t)(k + 1));
         }
       } else if (w == 0 && lane == 0) {
         lds_st(&freed[s], (uint32_t)(k + 1));  // NORM chunk: the slot stays free

@@ -52,8 +52,10 @@ struct Args {
   uint32_t round_in;  // fmt != F32 and alpha != 1: the weighted input is rounded to fmt
   uint32_t epoch;  // per-launch granule tag (never 0)
   uint64_t wait_ticks;      // bound of a norm wait (tunable: tests force the recompute fallback)
-  uint64_t lds_wait_ticks;  // bound of an on-chip LDS hand-off wait (fixed 20 ms; expiry aborts)
-  uint32_t dbg;  // experiment switches: 1 = no norm wait (norm := 1), 2 = no quantisation, 4 = time phases
+  uint64_t lds_wait_ticks;  // bound of an on-chip LDS hand-off wait (20 ms; expiry aborts)
+  // test / experiment switches (omf_plan_set_debug, 0 in production): 1 = no norm wait
+  // (norm := 1), 2 = no quantisation, 4 = time phases, 8 = slots never marked loaded
+  uint32_t dbg;
   unsigned long long* prof;  // dbg & 4: per-phase cycle totals (omf_plan_ring_profile)
 };
 

@@ -383,6 +383,7 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
             if compressor.packed_wire:  # pack on the GPU; (b/8) bytes per element cross PCIe
                 p_host = _packed_host(plan, q, width, levels)
                 host_norms = norms.cpu().tolist()
+                plan.check()  # an in-kernel timeout raises: the payload would be invalid
                 for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, host_norms):
                     if nv != 0:
                         results[i] = (_packed_slice(p_host, o, n, levels), nv)
@@ -390,6 +391,7 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
                 staged = _STAGING.get("encode", q.numel() * q.element_size()).view(q.dtype)
                 staged.copy_(q, non_blocking=True)  # one D2H of the payload arena (w bytes per element)
                 host_norms = norms.cpu().tolist()  # synchronises the stream: the payload copy has landed
+                plan.check()  # an in-kernel timeout raises: the payload would be invalid
                 q_host = staged.numpy()
                 for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, host_norms):
                     if nv != 0:

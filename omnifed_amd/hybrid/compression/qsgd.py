@@ -9,7 +9,8 @@ GPU and its payload returned on the CPU, as ``_do_compress`` returns it on
 
 Random draws (``rng``):
   * ``"philox"`` (default): on-device Philox4x32-10 keyed by (``torch.initial_seed()``,
-    the compressor's creation index) with the per-compressor call counter as the
+    the compressor's creation index, the client identity — the process's rank, or
+    ``client_id`` when set) with the per-compressor call counter as the
     stream offset — so ``torch.manual_seed`` makes runs reproducible, as in the
     reference, and the caller's CPU generator is never advanced (the reference's
     ``rand_like`` consumes n of its draws per tensor; this codec consumes none, so
@@ -30,7 +31,7 @@ value formats); float64 tensors raise ``ValueError`` (no fp64 encoder).
 from __future__ import annotations
 
 import itertools
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -144,9 +145,29 @@ def encode_many(flats: Sequence[torch.Tensor], bit_width: int, dev: torch.device
 _INSTANCES = itertools.count()
 
 
-def philox_key(instance: int) -> int:
-    """64-bit Philox key of a compressor: splitmix64 of (torch.initial_seed(), creation index)."""
-    z = (int(torch.initial_seed()) * 0x9E3779B97F4A7C15 + int(instance) * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB)
+def client_identity() -> int:
+    """This process's client identity: its rank in the default process group when one is
+    initialised, else the launcher's ``RANK`` environment variable, else 0."""
+    import os
+
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        return int(dist.get_rank())
+    try:
+        return int(os.environ.get("RANK", "0"))
+    except ValueError:
+        return 0
+
+
+def philox_key(instance: int, client: int = 0) -> int:
+    """64-bit Philox key of a compressor: splitmix64 of (torch.initial_seed(), creation index,
+    client identity).  The identity keeps clients that share a seed (every process calling the
+    reference's ``set_seed(1234)``, omnifed/data/utils.py:22) from drawing the same uniforms at
+    every arena position, which would correlate their rounding errors and void the 1/N variance
+    reduction of averaging N clients."""
+    z = (int(torch.initial_seed()) * 0x9E3779B97F4A7C15 + int(instance) * 0xBF58476D1CE4E5B9 + 0x94D049BB133111EB
+         + int(client) * 0xD1B54A32D192ED03)
     z &= 2**64 - 1
     z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
     z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
@@ -166,10 +187,12 @@ class QSGDQuantCompression(Compression):
         self.rng = rng
         self._calls = 0
         self._instance = next(_INSTANCES)
+        self.client_id: Optional[int] = None  # None: client_identity() (the process's rank)
 
     def philox_key(self) -> int:
         """The Philox key of this compressor (see the module docstring)."""
-        return philox_key(self._instance)
+        cid = client_identity() if self.client_id is None else int(self.client_id)
+        return philox_key(self._instance, cid)
 
     def _next_call(self) -> int:
         c = self._calls
@@ -203,7 +226,9 @@ class QSGDQuantCompression(Compression):
         width, _ = choose_qsgd_storage_width(levels)
         out: List[Tuple] = [None] * len(flats)
         for plan, q, norms, idx in groups:
-            for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, norms.cpu().tolist()):
+            host_norms = norms.cpu().tolist()  # synchronises the stream
+            plan.check()  # an in-kernel timeout raises (the payload would be invalid)
+            for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, host_norms):
                 out[i] = (None, -1, -1, -1) if nv == 0 else (q[o:o + n], float(nv), width, levels)
         return out
 

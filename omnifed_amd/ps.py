@@ -38,16 +38,44 @@ from . import codec
 from .shapes import numel
 
 
-class GpuOps:
-    """The device operations the PS steps use (HIP C ABI)."""
+def rank_key(seed: int, rank: int) -> int:
+    """64-bit Philox key of one client: splitmix64 of (seed, rank).  Clients that share a seed
+    (every process calling the reference's ``set_seed(1234)``) still draw independent streams,
+    so averaging N clients keeps QSGD's 1/N variance reduction."""
+    z = (int(seed) * 0x9E3779B97F4A7C15 + (int(rank) + 1) * 0xD1B54A32D192ED03) & (2**64 - 1)
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & (2**64 - 1)
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & (2**64 - 1)
+    return z ^ (z >> 31)
 
-    def __init__(self, plan: "codec.Plan", seed: int = 0):
+
+def _rank(group=None) -> int:
+    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+
+
+class GpuOps:
+    """The device operations the PS steps use (HIP C ABI).
+
+    ``seed``: the Philox key is ``rank_key(seed, rank)`` (``rank`` defaults to this process's
+    rank in the default group), so ranks that pass one seed still draw independently."""
+
+    def __init__(self, plan: "codec.Plan", seed: int = 0, rank: Optional[int] = None):
         self.plan = plan
         self.seed = int(seed)
+        self.rank = _rank() if rank is None else int(rank)
+        self.key = rank_key(self.seed, self.rank)
 
     def encode(self, x, bit_width, alpha, call, q=None, norms=None):
-        """Q(fl32(alpha·x)) of the whole arena (Philox keyed by ``seed``, stream ``call``)."""
-        return self.plan.qsgd_encode(x, bit_width, q_out=q, norm_out=norms, alpha=alpha, seed=self.seed, offset=call)
+        """Q(fl32(alpha·x)) of the whole arena (Philox keyed by ``key``, stream ``call``)."""
+        return self.plan.qsgd_encode(x, bit_width, q_out=q, norm_out=norms, alpha=alpha, seed=self.key, offset=call)
+
+    def encode_status(self) -> int:
+        """1 if the plan's launches since the last check hit an in-kernel timeout (the payload is
+        invalid), else 0; synchronises the current stream."""
+        try:
+            self.plan.check()
+        except codec.CodecError:
+            return 1
+        return 0
 
     def decode(self, q, width, levels, norms, y, accumulate):
         return self.plan.qsgd_decode(q, width, levels, norms, y_out=y, accumulate=accumulate)
@@ -172,6 +200,10 @@ class DeviceAggregator:
                 q[o:o + m].copy_(qg[plan.offsets[k]:plan.offsets[k] + m])
                 norms[i] = ng[k]
         levels = 2**compressor.s
+        # An in-kernel encoder timeout raises here, before anything touches the accumulator (the
+        # reference decodes a whole update before it accumulates, global_grpc_server.py:108-111,
+        # so a failed SendUpdate leaves acc as it was and answers success=False).
+        self.plan.check()
         # absent tensors have q = 0 (x was zero there): acc += +0, as accumulate_layers
         self.plan.qsgd_decode(q, 8 if levels <= 127 else 32, levels, norms, y_out=self.acc, accumulate=True)
         self.update_count += 1
@@ -179,23 +211,28 @@ class DeviceAggregator:
 
     def apply_and_encode(self, compressor, total_samples: Optional[int] = None):
         """Fused ``_apply_model_updates`` + the first downlink ``_send_current_model``
-        (global_grpc_server.py:155-171, 213-234): one launch divides the accumulator by the
-        sample count (in place: it becomes the averaged model, as ``param.data = avg``) and
-        QSGD-encodes the average.  Returns ``(avg views by name, LayerState list)``; later
-        requests re-encode the average independently, as the reference does per request.
+        (global_grpc_server.py:155-171, 213-234): the average ``acc / total_samples`` is written
+        to ``self.avg`` (the accumulator keeps the sum) and QSGD-encoded — for a Philox QSGD
+        compressor in one launch that reads the accumulator once (omf_ps_apply_encode).
+        Returns ``(avg views by name, LayerState list)``; later requests re-encode the average
+        independently, as the reference does per request.  An in-kernel encoder timeout raises
+        ``RuntimeError``.
         """
         from .hybrid.compression.qsgd import QSGDQuantCompression, choose_qsgd_storage_width
         from .hybrid.communicator.global_grpc_compression import qsgd_layer_from_payload, _encode_dense_layer
 
-        if (not isinstance(compressor, QSGDQuantCompression) or not self.compute_mean
-                or compressor.rng != "philox"):  # parity mode draws MT19937 uniforms on the host
-            avg = self.apply(total_samples)
-            from .hybrid.communicator.global_grpc_compression import encode_updates_dict
-            return avg, encode_updates_dict(avg, compressor)
         total = self.total_samples if total_samples is None else int(total_samples)
-        s = compressor.s
         if self.avg is None:
             self.avg = torch.empty_like(self.acc)
+        if (not isinstance(compressor, QSGDQuantCompression) or not self.compute_mean
+                or compressor.rng != "philox"):  # parity mode draws MT19937 uniforms on the host
+            self.avg.copy_(self.acc)
+            if self.compute_mean:
+                codec.div_(self.avg, float(total))
+            avg = {n: self._avg_slice(n).view(self.shapes[n]) for n in self.names}
+            from .hybrid.communicator.global_grpc_compression import encode_updates_dict
+            return avg, encode_updates_dict(avg, compressor)
+        s = compressor.s
         # avg_out disjoint from acc: the one-launch path (omf_ps_apply_encode)
         _, q, norms = self.plan.ps_apply_encode(self.acc, float(total), s, avg_out=self.avg,
                                                 seed=compressor.philox_key(), offset=compressor._next_call())
@@ -203,6 +240,7 @@ class DeviceAggregator:
         width, _ = choose_qsgd_storage_width(levels)
         qh = q.cpu().numpy()
         nh = norms.cpu().tolist()
+        self.plan.check()  # an in-kernel timeout raises: the payload would be invalid
         avg = {n: self._avg_slice(n).view(self.shapes[n]) for n in self.names}
         layers = []
         for i, n in enumerate(self.names):
@@ -219,6 +257,24 @@ class DeviceAggregator:
         if self.compute_mean:
             codec.div_(self.acc, float(total))
         return {n: self._slice(n).view(self.shapes[n]) for n in self.names}
+
+
+def weighted_sum_error_bound(abs_sum: torch.Tensor, exact: torch.Tensor, n_terms: int, total: float) -> torch.Tensor:
+    """Element-wise bound on ``|reduce(SUM)/total − exact|`` for a sum of ``n_terms`` fp32 terms
+    added in ANY order (an RCCL ring or tree reduce picks its own), then one fp32 division.
+
+    ``abs_sum`` = Σ_i |x_i| and ``exact`` = (Σ_i x_i)/total, both in fp64.  Every order of
+    N−1 fp32 additions errs by at most γ_{N−1}·Σ|x_i| (γ_m = m·u/(1 − m·u), u = 2⁻²⁴; Higham,
+    *Accuracy and Stability of Numerical Algorithms*, §4.2), and the division adds u·|result|;
+    N·2⁻¹⁴⁹ covers subnormal rounding.  The reference PS sums in nondeterministic gRPC arrival
+    order (global_grpc_server.py:147-153), so this bound — not bit equality — is the parity bar
+    of the ``reduce`` mode; the ``gather`` mode is bit-exact in rank order."""
+    u = 2.0**-24
+    m = max(int(n_terms) - 1, 0)
+    gamma = m * u / (1.0 - m * u)
+    w = abs(float(total))
+    err_sum = gamma * abs_sum.double() / w
+    return err_sum + u * (exact.double().abs() + err_sum) + n_terms * 2.0**-149 / min(w, 1.0)
 
 
 def weighted_sum_reduce(y: torch.Tensor, total_weight: float, ops, group=None, dst: int = 0) -> torch.Tensor:
@@ -257,6 +313,19 @@ def total_weight(weight: float, device, group=None) -> float:
     return float(t.item())
 
 
+def _agree_encoded(ops, device, group=None) -> None:
+    """Every rank learns whether any rank's encode hit an in-kernel timeout (an 8-byte RCCL
+    all-reduce of the flags) before the payloads move, and all of them raise together: a
+    failed client never ships an invalid payload into the sum, and no rank is left waiting in
+    a collective the others abandoned."""
+    status = getattr(ops, "encode_status", None)
+    flag = torch.tensor([0 if status is None else int(status())], dtype=torch.int32, device=device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+    if int(flag.item()):
+        raise codec.CodecError("qsgd_weighted_round: a rank's QSGD encode hit an in-kernel timeout "
+                               "(omf_plan_check OMF_ETIMEOUT); the round is abandoned on every rank")
+
+
 def qsgd_weighted_round(x: torch.Tensor, weight: float, total: float, ops, bit_width: int, call: int,
                         mode: str = "gather", y: Optional[torch.Tensor] = None, acc: Optional[torch.Tensor] = None,
                         q: Optional[torch.Tensor] = None, norms: Optional[torch.Tensor] = None, group=None,
@@ -269,6 +338,7 @@ def qsgd_weighted_round(x: torch.Tensor, weight: float, total: float, ops, bit_w
     levels = 2**int(bit_width)
     width = 8 if levels <= 127 else 32
     q, norms = ops.encode(x, bit_width, float(weight), call, q, norms)
+    _agree_encoded(ops, x.device, group)
     if mode == "reduce":
         y = ops.decode(q, width, levels, norms, y, False)
         return weighted_sum_reduce(y, total, ops, group=group, dst=dst)

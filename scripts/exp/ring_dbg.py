@@ -1,4 +1,4 @@
-"""Ring encoder phase pricing (experiment): time with OMF_RING_DBG switches set by the caller."""
+"""Ring encoder phase pricing (experiment): time with OMF_RING_DBG switches set by the caller (applied with Plan.set_debug)."""
 import os
 import sys
 
@@ -15,6 +15,7 @@ x = torch.randn(p.arena_end, device=dev) * 1e-3
 q = torch.empty(p.arena_end, dtype=torch.int8, device=dev)
 nr = torch.empty(p.nt, device=dev)
 p.set_encode_strategy("ring")
+p.set_debug(ring=int(os.environ.get("OMF_RING_DBG", "0")))
 for cfg in cfgs:
     for bm in (1,):
         p.set_ring(cfg=cfg, big_mode=bm)

@@ -1,4 +1,4 @@
-"""Stress every ring configuration under the debug timing modes (OMF_RING_DBG set by the caller):
+"""Stress every ring configuration under the debug timing modes (OMF_RING_DBG set by the caller, applied with Plan.set_debug):
 20 launches each on Llama-400M and on a mixed small arena; prints one line per configuration."""
 import os
 import sys
@@ -15,6 +15,7 @@ arenas = {"llama400m": [shapes.numel(s) for _, s in shapes.model_shapes("llama40
 for name, sizes in arenas.items():
     p = codec.Plan(sizes, device=dev)
     p.set_encode_strategy("ring")
+    p.set_debug(ring=int(os.environ.get("OMF_RING_DBG", "0")))
     x = torch.randn(p.arena_end, device=dev) * 1e-3
     for cfg in cfgs:
         for hold in (0, 3):

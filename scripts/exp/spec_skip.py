@@ -1,4 +1,4 @@
-"""Marginal cost of each bracketed-encoder launch: encode timings with OMF_SPEC_SKIP bits
+"""Marginal cost of each bracketed-encoder launch: encode timings with spec debug bits (Plan.set_debug)
 (experiment; each setting in its own plan, interleaved)."""
 import os
 import sys
@@ -13,16 +13,15 @@ sizes = [shapes.numel(s) for _, s in shapes.model_shapes(os.environ.get("MODEL",
 settings = [0, 2, 4, 8]
 plans = {}
 for sk in settings:
-    os.environ["OMF_SPEC_SKIP"] = str(sk)
     p = codec.Plan(sizes, device=dev)
     p.set_encode_strategy("bracket")
     plans[sk] = p
-os.environ.pop("OMF_SPEC_SKIP")
 x = torch.randn(plans[0].arena_end, device=dev) * 1e-3
 q = torch.empty(plans[0].payload_elems(8), dtype=torch.int8, device=dev)
 nr = torch.empty(len(sizes), device=dev)
-for p in plans.values():
+for sk, p in plans.items():
     p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=1)  # brackets exist before skipping them
+    p.set_debug(spec=sk)
 res = {sk: [] for sk in settings}
 for rnd in range(7):
     for sk in settings:

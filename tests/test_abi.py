@@ -23,7 +23,7 @@ def test_build_and_load():
     path = build()
     assert os.path.exists(path)
     L = _lib.lib()
-    assert L.omf_abi_version() == 103
+    assert L.omf_abi_version() == 104
     assert L.omf_last_error() == b""
 
 

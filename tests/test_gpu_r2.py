@@ -62,8 +62,8 @@ def _layer(buf):
 # ---------------------------------------------------------------- ring robustness
 
 @pytest.mark.parametrize("dbg", [2, 3])
-def test_ring_debug_timing_modes_complete(gpu, dbg, monkeypatch):
-    """OMF_RING_DBG=2 (quantisation off: the timing that hung before the ticket fix) and 3
+def test_ring_debug_timing_modes_complete(gpu, dbg):
+    """Ring debug switches 2 (quantisation off: the timing that hung before the ticket fix) and 3
     (norm waits off too) finish, report no timeout, and publish the same norms."""
     sizes = [7, 1000, 16384, 40000, 70001, 3, 1 << 20, 300_000]
     ref = codec.Plan(sizes, device=gpu)
@@ -71,8 +71,8 @@ def test_ring_debug_timing_modes_complete(gpu, dbg, monkeypatch):
     x = torch.randn(ref.arena_end, device=gpu, generator=g)
     _, n_ref = ref.qsgd_encode(x, 4, seed=1)
     assert ref.check()
-    monkeypatch.setenv("OMF_RING_DBG", str(dbg))
-    p = codec.Plan(sizes, device=gpu)  # the debug switch is read at plan creation
+    p = codec.Plan(sizes, device=gpu)
+    p.set_debug(ring=dbg)  # test hook (omf_plan_set_debug); never read from the environment
     p.set_encode_strategy("ring")
     for hold in (0, 3):
         p.set_ring(hold_max=hold)

@@ -1,0 +1,287 @@
+"""Round-3 GPU tests, all through the HIP C ABI:
+
+* in-kernel timeouts surface as ``RuntimeError`` on every product entry point
+  (``encode_updates_dict``, ``DeviceAggregator.accumulate_updates`` / ``apply_and_encode``,
+  ``qsgd_weighted_round``), as the reference PS turns any codec exception into
+  ``UpdateResponse(success=False)`` (global_grpc_server.py:138-145);
+* the multi-GPU PS aggregates (omnifed_amd/ps.py) on a real RCCL group of world size 1
+  (``nccl`` in-process, ``device_id`` bound): the weighted QSGD round in both modes and the
+  Top-K sparse aggregate in both modes, against the oracle and the one-GPU aggregator;
+* oracle pins of the fused PS step (f2) and of a stratified Llama-400M sample on the
+  bracketed single-read encoder.
+"""
+
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+import oracle
+from omnifed_amd import codec, shapes
+from omnifed_amd.hybrid.communicator.global_grpc_compression import encode_updates_dict
+from omnifed_amd.hybrid.compression.qsgd import QSGDQuantCompression
+
+pytestmark = pytest.mark.gpu
+
+SPEC_NO_FOLD = 16  # omf_plan_set_debug spec bit: fold skipped, every fix wait expires
+RING_NO_LOADED = 8  # omf_plan_set_debug ring bit: slots never marked loaded, hand-off waits expire
+
+
+def _oracle_q(x_np, s, norm, u_np):
+    q, *_ = oracle.qsgd_quantize(torch.from_numpy(np.ascontiguousarray(x_np)), s, norm=norm,
+                                 u=torch.from_numpy(np.ascontiguousarray(u_np)))
+    return q.numpy()
+
+
+class _Forced:
+    """Force the plan's next encodes to time out in-kernel (test hooks), restore on exit."""
+
+    def __init__(self, plan, strategy):
+        self.plan, self.strategy = plan, strategy
+
+    def __enter__(self):
+        self.prev = self.plan.strategy
+        self.plan.set_encode_strategy(self.strategy)
+        if self.strategy == "bracket":
+            self.plan.set_debug(spec=SPEC_NO_FOLD)
+            self.plan.set_resident_capacity(0, wait_us=50)  # the fix threads' norm-wait bound
+        else:
+            self.plan.set_debug(ring=RING_NO_LOADED, lds_wait_us=200)
+        return self.plan
+
+    def __exit__(self, *exc):
+        torch.cuda.synchronize()
+        self.plan.set_debug()
+        self.plan.set_resident_capacity(0, wait_us=0)
+        try:
+            self.plan.check()  # drop whatever the forced launch left
+        except codec.CodecError:
+            pass
+        self.plan.set_encode_strategy(self.prev)
+        return False
+
+
+NAMED = [("w1", (256, 1024)), ("b1", (1000,)), ("w2", (70001,)), ("n", (4096,))]
+
+
+def _updates(gpu, seed=3):
+    g = torch.Generator().manual_seed(seed)
+    return {n: (torch.randn(s, generator=g) * 1e-2).to(gpu) for n, s in NAMED}
+
+
+@pytest.mark.parametrize("strategy", ["bracket", "ring"])
+def test_timeout_raises_on_the_drop_in(gpu, strategy):
+    """A forced in-kernel timeout makes encode_updates_dict and the PS aggregator raise
+    RuntimeError (never a silent invalid payload); the next encode is clean again."""
+    from omnifed_amd.ps import DeviceAggregator
+
+    upd = _updates(gpu)
+    plan = codec.Plan.get([shapes.numel(s) for _, s in NAMED], device=gpu)  # the plan the drop-in uses
+    comp = QSGDQuantCompression(bit_width=4, device=gpu)
+    with _Forced(plan, strategy):
+        with pytest.raises(RuntimeError, match="timeout|exceeded its bound"):
+            encode_updates_dict(upd, comp)
+    good = encode_updates_dict(upd, comp)  # no stale error, a valid payload
+    assert [L.compression_type for L in good] == ["QSGDQuantCompression"] * len(NAMED)
+
+    agg = DeviceAggregator(NAMED, device=gpu)
+    assert agg.plan is plan
+    with _Forced(plan, strategy):
+        with pytest.raises(RuntimeError):
+            agg.accumulate_updates(upd, comp, number_samples=5, weight=5)
+    assert agg.update_count == 0 and agg.total_samples == 0  # the failed client was not counted
+    assert not bool(agg.acc.any())  # and nothing reached the accumulator
+    agg.accumulate_updates(upd, comp, number_samples=5, weight=5)
+    agg.accumulate_updates(upd, comp, number_samples=7, weight=7)
+    with _Forced(plan, strategy):
+        with pytest.raises(RuntimeError):
+            agg.apply_and_encode(comp)
+    avg, layers = agg.apply_and_encode(comp)
+    assert len(layers) == len(NAMED) and all(L.compression_type == "QSGDQuantCompression" for L in layers)
+    # the accumulator keeps the sum; the average is acc / total (both branches alike)
+    want = agg.acc.cpu().numpy() / np.float32(12)
+    for i, (n, _) in enumerate(NAMED):
+        o, k = agg.plan.offsets[i], agg.plan.sizes[i]
+        assert avg[n].cpu().numpy().reshape(-1).tobytes() == want[o:o + k].tobytes(), n
+
+
+# ---------------------------------------------------------------- RCCL, world size 1
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def nccl1(gpu):
+    """A one-rank RCCL group in this process (loopback rendezvous, device bound)."""
+    if dist.is_initialized():
+        pytest.skip("a process group already exists")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    yield gpu
+    dist.destroy_process_group()
+
+
+def _r18_arena(gpu, seed):
+    named = shapes.model_shapes("resnet18")
+    sizes = [shapes.numel(s) for _, s in named]
+    plan = codec.Plan.get(sizes, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(seed)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    return plan, x
+
+
+@pytest.mark.parametrize("mode", ["gather", "reduce"])
+def test_qsgd_weighted_round_rccl_world1(nccl1, mode):
+    """qsgd_weighted_round over RCCL (world 1): Σ decode(Q(w·x)) / Σw equals the one-GPU path
+    byte for byte, and per tensor the oracle's levels / decode given the GPU norm and draws."""
+    from omnifed_amd.ps import DeviceAggregator, GpuOps, qsgd_weighted_round, total_weight, weighted_sum_error_bound
+
+    gpu = nccl1
+    plan, x = _r18_arena(gpu, 11)
+    ops = GpuOps(plan, seed=77)
+    assert ops.rank == 0
+    w = 37.0
+    total = total_weight(w, gpu)
+    assert total == w
+    s, call = 4, 5
+    out = qsgd_weighted_round(x, w, total, ops, s, call, mode=mode)
+    torch.cuda.synchronize()
+    # one-GPU reference: the same encode, decode-accumulate into zeros, divide
+    q, norms = plan.qsgd_encode(x, s, alpha=w, seed=ops.key, offset=call)
+    acc = torch.zeros(plan.arena_end, device=gpu)
+    plan.qsgd_decode(q, 8, 16, norms, y_out=acc, accumulate=True)
+    codec.div_(acc, total)
+    oh, ah, xh, qh, nh = (t.cpu().numpy() for t in (out, acc, x, q, norms))
+    for o, n in zip(plan.offsets, plan.sizes):
+        assert oh[o:o + n].tobytes() == ah[o:o + n].tobytes()
+    # oracle: levels of fl32(w·x) given the GPU norm and the Philox draws, decode, / total
+    for t in (0, 7, 20, len(plan.sizes) - 2, len(plan.sizes) - 1):
+        o, n = plan.offsets[t], plan.sizes[t]
+        xw = (xh[o:o + n] * np.float32(w)).astype(np.float32)
+        want_q = _oracle_q(xw, s, float(nh[t]), oracle.philox_uniforms(ops.key, call, t, n))
+        assert qh[o:o + n].tobytes() == want_q.tobytes(), t
+        dec = oracle.qsgd_dequantize(torch.from_numpy(want_q), float(nh[t]), 16, (n,))
+        want = (dec / np.float32(total)).numpy()
+        got = oh[o:o + n]
+        if mode == "gather":
+            assert got.tobytes() == want.tobytes(), t
+        bound = weighted_sum_error_bound(dec.double().abs(), torch.from_numpy(want).double(), 1, total).numpy()
+        assert np.all(np.abs(got.astype(np.float64) - want.astype(np.float64)) <= bound), t
+    # the drop-in aggregator (one GPU, same draws) gives the same average
+    named = shapes.model_shapes("resnet18")
+    agg = DeviceAggregator(named, device=gpu)
+    assert agg.plan is plan
+    agg.plan.qsgd_decode(q, 8, 16, norms, y_out=agg.acc, accumulate=True)
+    agg.total_samples = int(w)
+    avg = agg.apply()
+    for (name, _), o, n in zip(named, plan.offsets, plan.sizes):
+        assert avg[name].cpu().numpy().reshape(-1).tobytes() == oh[o:o + n].tobytes(), name
+
+
+@pytest.mark.parametrize("dst", [None, 0])
+def test_topk_sparse_aggregate_rccl_world1(nccl1, dst):
+    """topk_sparse_aggregate over RCCL (all-gather, or gather to a root) of one client's
+    selection: zeros, scatter-add in rank order, / client count — the reference's
+    layerwise_decompress (core.py:62-71) restated by the oracle, bit for bit."""
+    from omnifed_amd.ps import GpuOps, topk_sparse_aggregate
+
+    gpu = nccl1
+    sizes = [5000, 1 << 20, 70001, 300_000]
+    plan = codec.Plan.get(sizes, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(21)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g)
+    ratio = 0.01
+    vals, idx, ks = plan.topk_encode(x, ratio)
+    ops = GpuOps(plan)
+    acc = torch.empty(plan.arena_end, device=gpu)
+    out = topk_sparse_aggregate(vals, idx, ratio, acc, ops, client_count=1, dst=dst)
+    torch.cuda.synchronize()
+    vh, ih, oh = vals.cpu(), idx.cpu(), out.cpu()
+    K = 0
+    for o, n, k in zip(plan.offsets, sizes, ks):
+        want = oracle.layerwise_decompress([vh[K:K + k]], [ih[K:K + k]], (n,), 1)
+        assert oh[o:o + n].numpy().tobytes() == want.reshape(-1).numpy().tobytes()
+        K += k
+
+
+def test_weighted_round_timeout_raises_on_every_rank(nccl1):
+    """A forced encoder timeout inside qsgd_weighted_round raises before any payload moves
+    (the flags are agreed with an RCCL all-reduce), and the next round is clean."""
+    from omnifed_amd.ps import GpuOps, qsgd_weighted_round
+
+    gpu = nccl1
+    sizes = [1 << 20, 5000, 3 << 20]
+    plan = codec.Plan.get(sizes, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(5)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g)
+    ops = GpuOps(plan, seed=3)
+    for strategy in ("bracket", "ring"):
+        with _Forced(plan, strategy):
+            with pytest.raises(RuntimeError, match="in-kernel timeout"):
+                qsgd_weighted_round(x, 2.0, 2.0, ops, 4, 0, mode="gather")
+        out = qsgd_weighted_round(x, 2.0, 2.0, ops, 4, 1, mode="reduce")
+        assert bool(torch.isfinite(out).all())
+
+
+# ---------------------------------------------------------------- oracle pins (f2, bracketed L400)
+
+@pytest.mark.parametrize("strategy", ["bracket", "ring"])
+def test_fused_ps_step_against_the_oracle(gpu, strategy):
+    """omf_ps_apply_encode: avg = acc / total (numpy's fp32 division) and, per tensor, the payload
+    equals the oracle's quantisation of that average given the GPU norm and Philox draws, and the
+    norm is within 2e-6 of the fp64 norm (not a comparison with another GPU encoder call)."""
+    sizes = [5, 16384, 70001, 1 << 20, 3000, 2_000_000]
+    plan = codec.Plan(sizes, device=gpu)
+    plan.set_encode_strategy(strategy)
+    g = torch.Generator(device=gpu).manual_seed(19)
+    acc = torch.randn(plan.arena_end, device=gpu, generator=g) * 3.0
+    total, s, seed, off = 7.0, 3, 1234, 2
+    avg, q, norms = plan.ps_apply_encode(acc, total, s, seed=seed, offset=off)
+    assert plan.check()
+    avg_np = acc.cpu().numpy() / np.float32(total)
+    ah, qh, nh = avg.cpu().numpy(), q.cpu().numpy(), norms.cpu().numpy()
+    for t, (o, n) in enumerate(zip(plan.offsets, sizes)):
+        a = avg_np[o:o + n]
+        assert ah[o:o + n].tobytes() == a.tobytes(), t
+        ref = float(np.sqrt(np.sum(a.astype(np.float64) ** 2)))
+        assert abs(float(nh[t]) - ref) <= 2e-6 * ref, t
+        want = _oracle_q(a, s, float(nh[t]), oracle.philox_uniforms(seed, off, t, n))
+        assert qh[o:o + n].tobytes() == want.tobytes(), t
+
+
+def test_llama400m_bracketed_sample_against_the_oracle(gpu):
+    """Llama-400M at s = 3 on the default (bracketed single-read) encoder: a stratified sample of
+    8 whole tensors — embed_tokens, lm_head, the final norm, attention / MLP matrices and RMSNorm
+    vectors of early, middle and late layers — equals the oracle given the GPU norm and draws."""
+    named = shapes.model_shapes("llama400m")
+    sizes = [shapes.numel(s) for _, s in named]
+    plan = codec.Plan.get(sizes, device=gpu)
+    assert plan.strategy == "bracket"
+    g = torch.Generator(device=gpu).manual_seed(31)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    s, seed, off = 3, 99, 6
+    q, norms = plan.qsgd_encode(x, s, seed=seed, offset=off)
+    assert plan.check()
+    names = [n for n, _ in named]
+    want_names = ["model.embed_tokens.weight", "lm_head.weight", "model.norm.weight"]
+    for layer, part in ((0, "self_attn.q_proj.weight"), (7, "mlp.down_proj.weight"),
+                        (10, "input_layernorm.weight"), (15, "self_attn.o_proj.weight"),
+                        (19, "mlp.up_proj.weight")):
+        want_names.append(f"model.layers.{layer}.{part}")
+    sample = [names.index(n) for n in want_names]
+    assert len(set(sample)) == 8
+    nh = norms.cpu().numpy()
+    for t in sample:
+        o, n = plan.offsets[t], sizes[t]
+        xh = x[o:o + n].cpu().numpy()
+        want = _oracle_q(xh, s, float(nh[t]), oracle.philox_uniforms(seed, off, t, n))
+        assert q[o:o + n].cpu().numpy().tobytes() == want.tobytes(), names[t]
