@@ -63,6 +63,8 @@ SIGNATURES = {
     "omf_topk_encode": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_f64, _c_f32, _c_p, _c_p, _c_p, _c_size, _c_p]),
     "omf_topk_decode": (ctypes.c_int, [_c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i32, _c_p]),
     "omf_topk_decode_arena": (ctypes.c_int, [_c_p, _c_f64, _c_p, _c_p, _c_p, _c_i32, _c_p]),
+    "omf_topk_decode_workspace_bytes": (_c_size, [_c_p, _c_f64]),
+    "omf_topk_decode_arena_ws": (ctypes.c_int, [_c_p, _c_f64, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_size, _c_p]),
 }
 
 _lock = threading.Lock()

@@ -106,6 +106,7 @@ class Plan:
         self._h = h
         self._lock = threading.Lock()
         self._topk_ws: Dict[int, torch.Tensor] = {}  # per stream: launches on two streams never share one
+        self._dec_ws: Dict[int, torch.Tensor] = {}   # tiled Top-K decode workspace, per stream
         self._topk_cache: Dict[float, tuple] = {}
         # the library's choice (by arena size, or OMF_ENCODE_STRATEGY)
         self.strategy = STRATEGIES[int(L.omf_plan_encode_strategy(h))]
@@ -428,8 +429,20 @@ class Plan:
             y = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
         _need(y, "y", torch.float32, dev, self.arena_end, 4)
         st = stream if stream is not None else _stream(dev)
-        check(lib().omf_topk_decode_arena(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), int(mode),
-                                          ctypes.c_void_p(st)), "omf_topk_decode_arena")
+        L = lib()
+        if mode == 0 and y.data_ptr() % 16 == 0:  # one streaming write of the arena (tiled decode)
+            need = int(L.omf_topk_decode_workspace_bytes(self._h, float(ratio)))
+            with self._lock:
+                ws = self._dec_ws.get(st)
+                if ws is None or ws.numel() < need:
+                    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+                    self._dec_ws[st] = ws
+                check(L.omf_topk_decode_arena_ws(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), 0,
+                                                 _ptr(ws), ctypes.c_size_t(ws.numel()), ctypes.c_void_p(st)),
+                      "omf_topk_decode_arena_ws")
+            return y
+        check(L.omf_topk_decode_arena(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), int(mode),
+                                      ctypes.c_void_p(st)), "omf_topk_decode_arena")
         return y
 
 

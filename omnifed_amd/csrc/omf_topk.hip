@@ -221,7 +221,7 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
                                                               uint32_t* __restrict__ fcount,
                                                               uint32_t* __restrict__ fhist) {
   constexpr int PER = kSBins / 1024;
-  constexpr int U = 4;  // runs in flight per lane group
+  constexpr int U = 8;  // runs in flight per lane group: a 4096-run tensor is two round trips
   __shared__ uint32_t h[kSBins];
   __shared__ uint32_t s_w[16];
   const int t = blockIdx.x;
@@ -1219,6 +1219,21 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
   }
 }
 
+// The call's verdict (status[0..2]) straight into mapped, coherent host memory — no copy packet
+// in the stream, so the bucket kernels queued behind this one start at once: the data words,
+// then this call's sequence number with release semantics at system scope (the host spins on
+// it).  One wave; vector stores.
+__global__ __launch_bounds__(64) void topk_publish_status(const uint32_t* __restrict__ status, uint32_t* host,
+                                                          uint32_t seq) {
+  if (threadIdx.x == 0) {
+    const uint32_t s0 = status[0], s1 = status[1], s2 = status[2];
+    __hip_atomic_store(&host[0], s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host[1], s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host[2], s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 template <bool GLOBAL>
 __global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict__ tp, float scale,
                                                         float* __restrict__ r, const uint64_t* __restrict__ sorted,
@@ -1313,6 +1328,197 @@ __global__ __launch_bounds__(kThreads) void topk_scatter_arena(const float* __re
   }
 }
 
+// ---------------------------------------------------------------- tiled zero-fill decode (mode 0)
+// y := 0 over the whole arena, then y[begin_t + idx] = v for one client's selection, as ONE
+// streaming write of the arena: the scattered 4-byte stores of a fill-then-scatter decode reach
+// HBM as partial-line read-modify-writes (3.7x their bytes, profiles/r02), so the values are
+// first bucketed by 64 Ki-element super-tile of the arena (count, scan, place: 12k bytes read
+// twice, 8k written), then one workgroup per super-tile builds each 16 Ki-element sub-tile in
+// LDS (zeros + its values) and streams it out with 16-byte non-temporal stores.
+constexpr int kDecSuperBits = 16;
+constexpr int kDecSubBits = 14;
+constexpr int kDecSubs = 1 << (kDecSuperBits - kDecSubBits);
+constexpr int kDecMaxSuper = 16384;  // LDS bins of the count / place blocks (arenas <= 2^30 elements)
+constexpr int kDecChunk = 4096;      // selected values per count / place block
+constexpr int kDecTileThreads = 512;
+
+// k_t prefix of the plan's tensors at `ratio` (exactly omf_topk_k), in LDS, by the whole block.
+template <int NT>
+__device__ __forceinline__ void dec_koff(const int64_t* __restrict__ sizes, int nt, double ratio, int64_t* koff,
+                                         int64_t* s_part) {
+  constexpr int PER = kArenaMaxTensors / NT;
+  int64_t kv[PER], loc = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int t = threadIdx.x * PER + j;
+    int64_t k = 0;
+    if (t < nt) {
+      k = (int64_t)((double)sizes[t] * ratio);
+      if (k < 1) k = 1;
+    }
+    kv[j] = k;
+    loc += k;
+  }
+  s_part[threadIdx.x] = loc;
+  __syncthreads();
+  for (int o = 1; o < NT; o <<= 1) {
+    const int64_t add = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0;
+    __syncthreads();
+    s_part[threadIdx.x] += add;
+    __syncthreads();
+  }
+  int64_t run = s_part[threadIdx.x] - loc;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int t = threadIdx.x * PER + j;
+    if (t <= nt) koff[t] = run;
+    run += kv[j];
+  }
+  if (threadIdx.x == NT - 1) koff[nt] = s_part[NT - 1];
+  __syncthreads();
+}
+
+__device__ __forceinline__ int dec_tensor_of(const int64_t* koff, int nt, int64_t j) {
+  int lo = 0, hi = nt - 1;  // koff[t] <= j < koff[t + 1]
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (koff[mid] <= j) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Count (PLACE = false) or place (PLACE = true) the selection's values by super-tile.  One block
+// per kDecChunk consecutive values (one or a few tensors, so a narrow super-tile range): LDS
+// counts over the block's range, one global atomic per touched super-tile; placing takes the
+// block's slots from the scanned cursors and writes (position in the super-tile << 32 | value).
+template <bool PLACE>
+__global__ __launch_bounds__(kThreads) void topk_dec_bucket(const float* __restrict__ values,
+                                                            const int64_t* __restrict__ indices,
+                                                            const int64_t* __restrict__ sizes,
+                                                            const int64_t* __restrict__ begins, int nt, double ratio,
+                                                            int64_t ktot, uint32_t* __restrict__ cnt,
+                                                            uint32_t* __restrict__ cur, uint64_t* __restrict__ pairs) {
+  __shared__ int64_t koff[kArenaMaxTensors + 1];
+  __shared__ int64_t s_part[kThreads];
+  extern __shared__ uint32_t h[];  // min(nsuper, kDecMaxSuper) bins (dynamic)
+  dec_koff<kThreads>(sizes, nt, ratio, koff, s_part);
+  const int64_t j0 = (int64_t)blockIdx.x * kDecChunk, j1 = min(j0 + kDecChunk, ktot);
+  const int tf = dec_tensor_of(koff, nt, j0), tl = dec_tensor_of(koff, nt, j1 - 1);
+  const uint32_t s_lo = (uint32_t)(begins[tf] >> kDecSuperBits);
+  const uint32_t nbin = (uint32_t)((begins[tl] + sizes[tl] - 1) >> kDecSuperBits) - s_lo + 1;  // <= kDecMaxSuper
+  for (uint32_t b = threadIdx.x; b < nbin; b += kThreads) h[b] = 0;
+  __syncthreads();
+  constexpr int U = kDecChunk / kThreads;
+  int64_t pos[U];
+  float val[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // every load issued before any is used
+    const int64_t j = j0 + threadIdx.x + (int64_t)u * kThreads;
+    const int64_t jc = j < j1 ? j : j1 - 1;
+    pos[u] = indices[jc];
+    val[u] = PLACE ? values[jc] : 0.0f;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t j = j0 + threadIdx.x + (int64_t)u * kThreads;
+    if (j >= j1) { pos[u] = -1; continue; }
+    const int t = dec_tensor_of(koff, nt, j);
+    const int64_t i = pos[u];
+    pos[u] = (i < 0 || i >= sizes[t]) ? -1 : begins[t] + i;  // padding (-1) / out of range: skipped
+    if (!PLACE && pos[u] >= 0) atomicAdd(&h[(uint32_t)(pos[u] >> kDecSuperBits) - s_lo], 1u);
+  }
+  if (!PLACE) {
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < nbin; b += kThreads)
+      if (h[b]) atomicAdd(&cnt[s_lo + b], h[b]);
+    return;
+  }
+  uint32_t rank[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    rank[u] = pos[u] >= 0 ? atomicAdd(&h[(uint32_t)(pos[u] >> kDecSuperBits) - s_lo], 1u) : 0u;
+  __syncthreads();
+  for (uint32_t b = threadIdx.x; b < nbin; b += kThreads)
+    if (h[b]) h[b] = atomicAdd(&cur[s_lo + b], h[b]);  // this block's first slot of the super-tile
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (pos[u] < 0) continue;
+    const uint32_t s = (uint32_t)(pos[u] >> kDecSuperBits);
+    const uint32_t in = (uint32_t)(pos[u] & ((1 << kDecSuperBits) - 1));
+    pairs[h[s - s_lo] + rank[u]] = ((uint64_t)in << 32) | (uint64_t)__float_as_uint(val[u]);
+  }
+}
+
+// Exclusive scan of the super-tile counts (one block): start[s] (nsuper + 1 entries) and the
+// placing cursors; the counts are zeroed for the next call.
+__global__ __launch_bounds__(1024) void topk_dec_scan(uint32_t* __restrict__ cnt, int32_t nsuper,
+                                                      uint32_t* __restrict__ start, uint32_t* __restrict__ cur) {
+  __shared__ uint32_t s_w[16];
+  uint32_t carry = 0;
+  for (int32_t s0 = 0; s0 < nsuper; s0 += 4096) {
+    uint32_t c[4], loc = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int32_t s = s0 + 4 * (int32_t)threadIdx.x + q;
+      c[q] = s < nsuper ? cnt[s] : 0u;
+      loc += c[q];
+    }
+    uint32_t tot;
+    const uint32_t inc = block_scan_incl<1024>(loc, s_w, tot);
+    uint32_t run = carry + inc - loc;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int32_t s = s0 + 4 * (int32_t)threadIdx.x + q;
+      if (s < nsuper) {
+        start[s] = run;
+        cur[s] = run;
+        cnt[s] = 0u;
+      }
+      run += c[q];
+    }
+    carry += tot;
+  }
+  if (threadIdx.x == 0) start[nsuper] = carry;
+}
+
+// One workgroup per super-tile: each 16 Ki-element sub-tile is zeroed in LDS, gets its values
+// (the super-tile's list is re-read per sub-tile from L2), and is streamed out (non-temporal
+// float4; the arena's partial last super-tile element by element).
+__global__ __launch_bounds__(kDecTileThreads) void topk_dec_tiles(const uint64_t* __restrict__ pairs,
+                                                                  const uint32_t* __restrict__ start,
+                                                                  float* __restrict__ y, int64_t arena_end) {
+  __shared__ float4 tile[(1 << kDecSubBits) / 4];
+  float* tf = reinterpret_cast<float*>(tile);
+  const uint32_t s = blockIdx.x;
+  const uint32_t p0 = start[s], p1 = start[s + 1];
+  constexpr int Q = (1 << kDecSubBits) / 4 / kDecTileThreads;  // float4 per thread per sub-tile
+  for (int sub = 0; sub < kDecSubs; ++sub) {
+    const int64_t base = ((int64_t)s << kDecSuperBits) + ((int64_t)sub << kDecSubBits);
+    if (base >= arena_end) break;  // block-uniform
+#pragma unroll
+    for (int q = 0; q < Q; ++q) tile[threadIdx.x + q * kDecTileThreads] = make_float4(0.f, 0.f, 0.f, 0.f);
+    __syncthreads();
+    for (uint32_t p = p0 + threadIdx.x; p < p1; p += kDecTileThreads) {
+      const uint64_t pr = pairs[p];
+      const uint32_t in = (uint32_t)(pr >> 32);
+      if ((int)(in >> kDecSubBits) == sub) tf[in & ((1u << kDecSubBits) - 1)] = __uint_as_float((uint32_t)pr);
+    }
+    __syncthreads();
+    if (base + (1 << kDecSubBits) <= arena_end) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int e = 4 * (threadIdx.x + q * kDecTileThreads);
+        store_nt(y + base + e, tile[threadIdx.x + q * kDecTileThreads]);
+      }
+    } else {
+      for (int64_t e = threadIdx.x; base + e < arena_end; e += kDecTileThreads) y[base + e] = tf[e];
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- host side
@@ -1332,25 +1538,29 @@ namespace {
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // OMF_TOPK_FALLBACK=1: always take the device-wide radix-sort path (tests of that path).
-// Per host thread and device: a pinned 16-byte status buffer and an event (never freed: a
-// few bytes per thread that calls the encoder).
+// Per host thread and device: a 16-byte status buffer in mapped, coherent host memory that
+// topk_publish_status writes (never freed: a few bytes per thread that calls the encoder).
 struct HostSync {
-  uint32_t* pinned = nullptr;
-  hipEvent_t ev = nullptr;
+  uint32_t* pinned = nullptr;  // host view
+  uint32_t* dev = nullptr;     // device view of the same bytes
   uint32_t seq = 0;
 };
 
-// Wait for the status copy of call `seq`: spin on the pinned word (the copy lands a few µs
-// after the plan kernel; an event wait costs tens of µs of wake-up, and every µs the host
-// spends here is a µs the next call's launches come later), then the event (which also
-// reports a failed launch).
-int wait_status(HostSync* h, uint32_t seq) {
+// Wait for the verdict of call `seq`: spin on the mapped word (it lands as soon as the plan
+// kernel's successor runs; an event or a copy packet would add tens of µs, and every µs the
+// host spends here is a µs the next call's launches come later).  If it has not come after
+// 200 ms, synchronise the stream (which reports a failed launch or fault) and look again.
+int wait_status(HostSync* h, uint32_t seq, hipStream_t st) {
   const auto t0 = std::chrono::steady_clock::now();
   while (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq) {
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) break;  // let the event decide
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+      OMF_HIP(hipStreamSynchronize(st));
+      if (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq)
+        return fail(OMF_EHIP, "omf_topk_encode: the plan verdict never reached the host");
+      break;
+    }
     __builtin_ia32_pause();
   }
-  OMF_HIP(hipEventSynchronize(h->ev));
   return OMF_OK;
 }
 HostSync* host_sync(int dev) {
@@ -1360,12 +1570,15 @@ HostSync* host_sync(int dev) {
   HostSync& h = hs[dev];
   if (!h.pinned) {
     void* p = nullptr;
-    if (hipHostMalloc(&p, 16, hipHostMallocDefault) != hipSuccess) return nullptr;
-    if (hipEventCreateWithFlags(&h.ev, hipEventDisableTiming) != hipSuccess) {
+    if (hipHostMalloc(&p, 16, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
       (void)hipHostFree(p);
       return nullptr;
     }
+    std::memset(p, 0, 16);
     h.pinned = static_cast<uint32_t*>(p);
+    h.dev = static_cast<uint32_t*>(d);
   }
   return &h;
 }
@@ -1600,11 +1813,10 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     hipLaunchKernelGGL(topk_plan, sgrid, sblk, 0, st, kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2,
                        flag, status, fse, dbg_bits());
     OMF_HIP(hipGetLastError());
-    // The plan's verdict goes to pinned host memory behind an event; the bucket kernels are
-    // enqueued before the host waits for it (they do nothing when the verdict is a fallback),
-    // so the GPU does not idle while the host reads it.
-    OMF_HIP(hipMemcpyAsync(hsync->pinned, status, 16, hipMemcpyDeviceToHost, st));
-    OMF_HIP(hipEventRecord(hsync->ev, st));
+    // The plan's verdict goes straight to mapped host memory (a one-wave kernel, no copy
+    // packet); the bucket kernels are enqueued before the host waits for it (they do nothing
+    // when the verdict is a fallback), so the GPU does not idle while the host reads it.
+    hipLaunchKernelGGL(topk_publish_status, dim3(1), dim3(64), 0, st, (const uint32_t*)status, hsync->dev, seq);
     const bool forced = force_fallback();
     if (!forced) {
       hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast,
@@ -1613,7 +1825,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
                          d_sizes, rz, values, indices, status, fmap, tlo, fcount, fhist, fse, thi, dbg_bits());
       OMF_HIP(hipGetLastError());
     }
-    if (int rc = wait_status(hsync, seq)) return rc;
+    if (int rc = wait_status(hsync, seq, st)) return rc;
     uint32_t host_status[4];
     std::memcpy(host_status, hsync->pinned, 16);
     if (dbg_bits() & 4) fprintf(stderr, "omf_topk: redo %u overflow %u\n", host_status[1], host_status[2]);
@@ -1672,24 +1884,85 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   return OMF_OK;
 }
 
+// Tiled zero-fill decode workspace: [cnt nsuper][start nsuper + 1][cur nsuper][pairs ktot x 8 B].
+struct DecWs {
+  size_t cnt, start, cur, pairs, total;
+  int32_t nsuper;
+};
+static DecWs dec_ws_layout(const omf_plan* p, int64_t ktot) {
+  DecWs d;
+  d.nsuper = (int32_t)((omf_plan_access::arena_end(p) + (1 << kDecSuperBits) - 1) >> kDecSuperBits);
+  size_t o = 0;
+  d.cnt = o; o = align256(o + 4 * (size_t)d.nsuper);
+  d.start = o; o = align256(o + 4 * ((size_t)d.nsuper + 1));
+  d.cur = o; o = align256(o + 4 * (size_t)d.nsuper);
+  d.pairs = o; o = align256(o + 8 * (size_t)std::max<int64_t>(ktot, 1));
+  d.total = o;
+  return d;
+}
+
+static int64_t decode_ktot(const omf_plan* plan, double ratio) {
+  int64_t ktot = 0;
+  for (int64_t n : omf_plan_access::sizes(plan)) {
+    const int64_t k = omf_topk_k(n, ratio);
+    if (k > n) return -1;
+    ktot += k;
+  }
+  return ktot;
+}
+
+size_t omf_topk_decode_workspace_bytes(const omf_plan* plan, double ratio) {
+  if (!plan || !(ratio == ratio)) return 0;
+  const int64_t ktot = decode_ktot(plan, ratio);
+  return ktot < 0 ? 0 : dec_ws_layout(plan, ktot).total;
+}
+
 int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
                           int32_t mode, void* stream) {
+  return omf_topk_decode_arena_ws(plan, ratio, values, indices, y, mode, nullptr, 0, stream);
+}
+
+int omf_topk_decode_arena_ws(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
+                             int32_t mode, void* ws, size_t ws_bytes, void* stream) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
   if (mode < 0 || mode > 2) return fail(OMF_EINVAL, "omf_topk_decode_arena: mode must be 0, 1 or 2");
   if (!(ratio == ratio)) return fail(OMF_EINVAL, "ratio is NaN");
   if (!values || !indices || !y) return fail(OMF_EINVAL, "omf_topk_decode_arena: NULL buffer");
   const int32_t nt = omf_plan_access::ntensors(plan);
   if (nt > kArenaMaxTensors) return fail(OMF_EINVAL, "omf_topk_decode_arena: too many tensors (decode per tensor)");
-  int64_t ktot = 0;
-  for (int64_t n : omf_plan_access::sizes(plan)) {
-    const int64_t k = omf_topk_k(n, ratio);
-    if (k > n) return fail(OMF_EINVAL, "selected index k out of range (k > numel): compress_ratio too large");
-    ktot += k;
-  }
+  const int64_t ktot = decode_ktot(plan, ratio);
+  if (ktot < 0) return fail(OMF_EINVAL, "selected index k out of range (k > numel): compress_ratio too large");
   DeviceGuard g(omf_plan_access::device(plan));
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   hipStream_t st = (hipStream_t)stream;
-  if (mode == 0) OMF_HIP(hipMemsetAsync(y, 0, 4 * (size_t)omf_plan_access::arena_end(plan), st));
+  const int64_t ae = omf_plan_access::arena_end(plan);
+  if (mode == 0 && ws) {
+    const DecWs d = dec_ws_layout(plan, ktot);
+    if (ws_bytes < d.total) return fail(OMF_EINVAL, "omf_topk_decode_arena: workspace too small");
+    if (((uintptr_t)ws & 255) || ((uintptr_t)y & 15)) return fail(OMF_EINVAL, "omf_topk_decode_arena: misaligned buffer");
+    if (d.nsuper <= kDecMaxSuper) {  // one streaming write of the arena (larger arenas: fill + scatter)
+      uint8_t* w = static_cast<uint8_t*>(ws);
+      uint32_t* cnt = reinterpret_cast<uint32_t*>(w + d.cnt);
+      uint32_t* start = reinterpret_cast<uint32_t*>(w + d.start);
+      uint32_t* cur = reinterpret_cast<uint32_t*>(w + d.cur);
+      uint64_t* pairs = reinterpret_cast<uint64_t*>(w + d.pairs);
+      const int64_t* sizes = omf_plan_access::d_sizes(plan);
+      const int64_t* begins = omf_plan_access::d_begins(plan);
+      OMF_HIP(hipMemsetAsync(cnt, 0, 4 * (size_t)d.nsuper, st));
+      const dim3 gb((unsigned)std::max<int64_t>(1, (ktot + kDecChunk - 1) / kDecChunk));
+      const size_t lds = 4 * (size_t)d.nsuper;
+      hipLaunchKernelGGL(topk_dec_bucket<false>, gb, dim3(kThreads), lds, st, values, indices, sizes, begins, (int)nt,
+                         ratio, ktot, cnt, cur, pairs);
+      hipLaunchKernelGGL(topk_dec_scan, dim3(1), dim3(1024), 0, st, cnt, d.nsuper, start, cur);
+      hipLaunchKernelGGL(topk_dec_bucket<true>, gb, dim3(kThreads), lds, st, values, indices, sizes, begins, (int)nt,
+                         ratio, ktot, cnt, cur, pairs);
+      hipLaunchKernelGGL(topk_dec_tiles, dim3((unsigned)d.nsuper), dim3(kDecTileThreads), 0, st,
+                         (const uint64_t*)pairs, (const uint32_t*)start, y, ae);
+      OMF_HIP(hipGetLastError());
+      return OMF_OK;
+    }
+  }
+  if (mode == 0) OMF_HIP(hipMemsetAsync(y, 0, 4 * (size_t)ae, st));
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ktot + kThreads - 1) / kThreads, 4096));
   hipLaunchKernelGGL(topk_scatter_arena, dim3(gx), dim3(kThreads), 0, st, values, indices,
                      omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (int)nt, ratio, ktot, y,

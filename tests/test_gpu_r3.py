@@ -285,3 +285,64 @@ def test_llama400m_bracketed_sample_against_the_oracle(gpu):
         xh = x[o:o + n].cpu().numpy()
         want = _oracle_q(xh, s, float(nh[t]), oracle.philox_uniforms(seed, off, t, n))
         assert q[o:o + n].cpu().numpy().tobytes() == want.tobytes(), names[t]
+
+
+# ---------------------------------------------------------------- tiled zero-fill Top-K decode
+
+def _scatter_ref(plan, values, indices, ks):
+    """zeros(arena) then y[begin_t + idx] = v per tensor (torch on the GPU), skipping -1 / out of range."""
+    y = torch.zeros(plan.arena_end, device=values.device)
+    K = 0
+    for o, n, k in zip(plan.offsets, plan.sizes, ks):
+        ix, v = indices[K:K + k], values[K:K + k]
+        ok = (ix >= 0) & (ix < n)
+        y[o + ix[ok]] = v[ok]
+        K += k
+    return y
+
+
+def test_topk_tiled_decode_matches_scatter(gpu):
+    """Mode 0 through the tiled decoder (bucket by 64 Ki super-tile, LDS sub-tiles) equals zeros +
+    scatter over the whole arena, padding included: random selections, a tensor whose selection is
+    clustered in one sub-tile, padding indices (-1) and out-of-range indices are skipped, and stale
+    contents of y are overwritten everywhere."""
+    sizes = [5, 70001, 1 << 20, 3000, 200_003, 65536, 131_071]
+    plan = codec.Plan(sizes, device=gpu)
+    ratio = 0.05
+    ks = plan.topk_ks(ratio)
+    g = torch.Generator(device=gpu).manual_seed(12)
+    vals, idx = [], []
+    for t, (n, k) in enumerate(zip(sizes, ks)):
+        if t == 2:  # clustered: every selected index in one 16 Ki sub-tile of a super-tile
+            ix = torch.randperm(16384, device=gpu, generator=g)[:k] + 3 * 16384
+        else:
+            ix = torch.randperm(n, device=gpu, generator=g)[:k]
+        if t == 4:
+            ix[::7] = -1        # padding
+            ix[3::11] = n + 5   # out of range
+        idx.append(ix.to(torch.int64))
+        vals.append(torch.randn(k, device=gpu, generator=g))
+    v, ix = torch.cat(vals), torch.cat(idx)
+    y = torch.full((plan.arena_end,), 7.0, device=gpu)
+    got = plan.topk_decode_arena(v, ix, ratio, y=y, mode=0)
+    torch.cuda.synchronize()
+    want = _scatter_ref(plan, v, ix, ks)
+    assert torch.equal(got, want)
+    # the same workspace again (counts left zeroed by the previous call), another selection
+    v2 = torch.randn_like(v)
+    got2 = plan.topk_decode_arena(v2, ix, ratio, y=y, mode=0)
+    assert torch.equal(got2, _scatter_ref(plan, v2, ix, ks))
+
+
+def test_llama400m_topk_encode_then_tiled_decode(gpu):
+    """Llama-400M, k = 1 %: the encoder's selection decoded by the tiled decoder equals zeros +
+    scatter of the same (values, indices), over the whole arena."""
+    named = shapes.model_shapes("llama400m")
+    sizes = [shapes.numel(s) for _, s in named]
+    plan = codec.Plan.get(sizes, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(23)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    vals, idx, ks = plan.topk_encode(x, 0.01)
+    y = plan.topk_decode_arena(vals, idx, 0.01, mode=0)
+    torch.cuda.synchronize()
+    assert torch.equal(y, _scatter_ref(plan, vals, idx, ks))
