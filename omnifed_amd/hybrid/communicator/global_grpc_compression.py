@@ -9,9 +9,11 @@ work happens, not what is produced:
   the reference's 4·N ``.cpu()`` copy at :105);
 * ``encode_updates_dict`` encodes every QSGD tensor of the dict in ONE kernel
   launch (``omf_qsgd_encode`` over an update arena) and fetches the payload
-  arena with one device-to-host copy;
+  arena through pinned staging in chunks, the host copies into ``bytes`` done by
+  worker threads while earlier messages are built (``omnifed_amd.hostio``);
 * ``decode_updates_dict`` decodes every QSGD layer of a message in ONE launch from
-  one pinned staging buffer (one host-to-device copy of the payloads), and
+  pinned staging (chunked host-to-device copies overlapped with the reading of
+  later messages), and
   ``decode_updates_into`` (client downlink, global_grpc_client.py:98-111) writes the
   decoded tensors straight into the model's device tensors;
 * decoders take an optional ``device=`` (default: the reference's placement —
@@ -35,7 +37,7 @@ from ..compression.qsgd import (
 )
 from ..compression.topk import TOPK_COMPRESSION_NAME, TopKCompression
 from ..compression.core import compute_device
-from ... import codec
+from ... import codec, hostio
 
 GlobalHybridCompressor = Union[TopKCompression, QSGDQuantCompression]
 
@@ -44,26 +46,7 @@ _QSGD_TORCH_DTYPES = {8: torch.int8, 32: torch.int32}
 _QSGD_TYPES = (QSGD_COMPRESSION_NAME, QSGD_PACKED_COMPRESSION_NAME)
 
 
-class _PinnedStaging:
-    """Reusable page-locked host buffers (one per purpose), grown on demand.
-
-    Payload bytes cross PCIe once per message through these: a pageable tensor's
-    ``.cpu()`` / ``.to(dev)`` would stage through a driver bounce buffer instead.
-    Callers copy out of a buffer before it is reused (protobuf ``bytes`` are copies).
-    """
-
-    def __init__(self):
-        self._bufs: Dict[str, torch.Tensor] = {}
-
-    def get(self, key: str, nbytes: int) -> torch.Tensor:
-        b = self._bufs.get(key)
-        if b is None or b.numel() < nbytes:
-            b = torch.empty(max(int(nbytes), 4096), dtype=torch.uint8, pin_memory=True)
-            self._bufs[key] = b
-        return b[:nbytes]
-
-
-_STAGING = _PinnedStaging()
+_STAGING = hostio.STAGING
 
 
 def compression_mode_name(compressor: Optional[GlobalHybridCompressor]) -> str:
@@ -165,22 +148,6 @@ def qsgd_packed_layer_from_payload(name: str, shape, packed: bytes, norm: float,
     layer.width = bits
     layer.level = int(levels)
     return layer
-
-
-def _packed_host(plan, q: torch.Tensor, width: int, levels: int) -> np.ndarray:
-    """Pack a device payload arena and fetch it (one D2H through pinned staging); tensor t's
-    bytes start at ``plan.offsets[t] * b // 8``."""
-    packed = plan.qsgd_pack(q, width, levels)
-    staged = _STAGING.get("encode", packed.numel() * 4).view(torch.int32)
-    staged.copy_(packed, non_blocking=True)
-    torch.cuda.current_stream(q.device).synchronize()
-    return staged.numpy().view(np.uint8)
-
-
-def _packed_slice(host: np.ndarray, offset: int, n: int, levels: int) -> bytes:
-    b = codec.packed_bits(levels)
-    start = offset * b // 8
-    return host[start:start + (n * b + 7) // 8].tobytes()
 
 
 def topk_layer_from_payload(name: str, shape, values: np.ndarray, indices: np.ndarray):
@@ -357,16 +324,39 @@ def decode_layer_tensor(layer, *, base_tensor: Optional[torch.Tensor] = None, de
 
 # ---------------------------------------------------------------- dict helpers (batched)
 
+def wire_size(layers) -> Dict[str, int]:
+    """Wire-size figures of a list of ``LayerState``s, for the caller's metrics (SURVEY.md §5;
+    the reference's docs/HYBRID_QSGD_IMPLEMENTATION_STEPS.md:373 notes QSGD's wire size is not
+    yet in its CSV): ``wire_bytes`` = the serialised size of the layers (what a ModelUpdate /
+    ModelParameters carries for them), ``payload_bytes`` = their values/indices/dense data,
+    ``dense_fp32_bytes`` = 4 bytes per element (the uncompressed update), ``layers``."""
+    wire = payload = dense = 0
+    for L in layers:
+        wire += L.ByteSize()
+        payload += len(L.values_data) + len(L.indices_data) + 4 * len(L.param_update)
+        shape = tuple(L.original_shape) or tuple(L.param_shape)
+        dense += 4 * int(np.prod(shape)) if shape else 0
+    return {"wire_bytes": wire, "payload_bytes": payload, "dense_fp32_bytes": dense, "layers": len(layers)}
+
+
 def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[GlobalHybridCompressor], *,
-                        weight=None) -> list:
+                        weight=None, stats: Optional[Dict[str, int]] = None) -> list:
     """global_grpc_compression.py:207-211; QSGD tensors go through ONE batched launch.
 
-    ``weight``: as encode_layer_state (the client's ``batch_samples``, fused into the encoder)."""
+    ``weight``: as encode_layer_state (the client's ``batch_samples``, fused into the encoder).
+    ``stats`` (optional dict, ours): receives ``wire_size`` of the returned layers."""
+    layers = _encode_updates(updates, compressor, weight)
+    if stats is not None:
+        stats.update(wire_size(layers))
+    return layers
+
+
+def _encode_updates(updates, compressor, weight) -> list:
     if not isinstance(compressor, QSGDQuantCompression):
         return [encode_layer_state(name, tensor, compressor, weight=weight) for name, tensor in updates.items()]
     names = list(updates.keys())
     comp_idx = [i for i, n in enumerate(names) if should_compress_tensor(updates[n])]
-    results = {}
+    layers: List = [None] * len(names)
     if comp_idx:
         if not (0 <= compressor.s <= 30):
             raise ValueError(f"QSGD bit_width={compressor.s} out of range [0, 30]")
@@ -380,74 +370,64 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
         width, _ = choose_qsgd_storage_width(levels)
         for plan, q, norms, members in groups:  # one group per dtype (normally one)
             idx = [comp_idx[m] for m in members]
+            stream = torch.cuda.current_stream(dev)
+            nh = _STAGING.get("encode_norms", 4 * plan.nt).view(torch.float32)
+            nh.copy_(norms, non_blocking=True)  # queued before the payload chunks: it lands first
+            ev = torch.cuda.Event()
+            ev.record(stream)
             if compressor.packed_wire:  # pack on the GPU; (b/8) bytes per element cross PCIe
-                p_host = _packed_host(plan, q, width, levels)
-                host_norms = norms.cpu().tolist()
-                plan.check()  # an in-kernel timeout raises: the payload would be invalid
-                for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, host_norms):
-                    if nv != 0:
-                        results[i] = (_packed_slice(p_host, o, n, levels), nv)
-            else:
-                staged = _STAGING.get("encode", q.numel() * q.element_size()).view(q.dtype)
-                staged.copy_(q, non_blocking=True)  # one D2H of the payload arena (w bytes per element)
-                host_norms = norms.cpu().tolist()  # synchronises the stream: the payload copy has landed
-                plan.check()  # an in-kernel timeout raises: the payload would be invalid
-                q_host = staged.numpy()
-                for i, o, n, nv in zip(idx, plan.offsets, plan.sizes, host_norms):
-                    if nv != 0:
-                        results[i] = (q_host[o:o + n].tobytes(), nv)  # bytes are copies: staging reusable
-    layers = []
+                src = plan.qsgd_pack(q, width, levels)
+                b = codec.packed_bits(levels)
+                spans = [(o * b // 8, (n * b + 7) // 8) for o, n in zip(plan.offsets, plan.sizes)]
+            else:  # the payload arena: w bytes per element
+                src, isz = q, q.element_size()
+                spans = [(o * isz, n * isz) for o, n in zip(plan.offsets, plan.sizes)]
+            ev.synchronize()
+            host_norms = nh.tolist()
+            spans = [(off, ln if nv != 0 else 0) for (off, ln), nv in zip(spans, host_norms)]  # zero norm: dense
+            # chunked D2H; each chunk's bytes filled by worker threads while the previous chunk's
+            # LayerStates are built (protobuf copies the bytes into its message)
+            for k, payload in hostio.device_to_bytes(src, spans, stream=stream):
+                i = idx[k]
+                t = updates[names[i]]
+                if compressor.packed_wire:
+                    layers[i] = qsgd_packed_layer_from_payload(names[i], tuple(t.shape), payload, host_norms[k], levels)
+                else:
+                    layers[i] = qsgd_layer_from_payload(names[i], tuple(t.shape), payload, host_norms[k], width, levels)
+            plan.check()  # an in-kernel timeout raises: the payload would be invalid
     for i, name in enumerate(names):
-        t = updates[name]
-        if i in results:
-            payload, nv = results[i]
-            levels = 2**compressor.s
-            width, _ = choose_qsgd_storage_width(levels)
-            if compressor.packed_wire:
-                layers.append(qsgd_packed_layer_from_payload(name, tuple(t.shape), payload, nv, levels))
-            else:
-                layers.append(qsgd_layer_from_payload(name, tuple(t.shape), payload, nv, width, levels))
-        else:
-            layers.append(_encode_dense_layer(name, _weighted(t, weight)))
+        if layers[i] is None:
+            layers[i] = _encode_dense_layer(name, _weighted(updates[name], weight))
     return layers
 
 
 def _decode_qsgd_batch(layers, dev: torch.device):
     """Decode QSGD layers that share (width, level) in ONE launch.
 
-    The payloads are packed into one pinned buffer in a plan's arena layout, copied to
-    the GPU once, and decoded by one ``omf_qsgd_decode``; returns the decoded fp32 arena
+    The payloads are staged in a plan's arena layout through pinned memory, chunk by chunk
+    (hostio.bytes_to_device: each chunk's host-to-device copy overlaps the reading of the next
+    chunk's payloads), and decoded by one ``omf_qsgd_decode``; returns the decoded fp32 arena
     and the plan (layer i at ``[plan.offsets[i], + plan.sizes[i])``).
     """
     width, level = layers[0].width, layers[0].level
     sizes = [max(int(np.prod(tuple(L.original_shape))), 1) for L in layers]
     plan = codec.Plan.get(sizes, device=dev)
+    norms = np.zeros(plan.nt, dtype=np.float32)
+    for i, L in enumerate(layers):
+        norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
+    nd = torch.from_numpy(norms).to(dev)
     if layers[0].compression_type == QSGD_PACKED_COMPRESSION_NAME:  # tensor t at byte offsets[t] * b / 8
         words = plan.packed_words(level)
-        hostb = _STAGING.get("decode", words * 4).numpy()
-        norms = np.zeros(plan.nt, dtype=np.float32)
-        for i, (L, o) in enumerate(zip(layers, plan.offsets)):
-            start = o * width // 8
-            hostb[start:start + len(L.values_data)] = np.frombuffer(L.values_data, dtype=np.uint8)
-            norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
-        pd = torch.empty(words, dtype=torch.int32, device=dev)
-        pd.copy_(torch.from_numpy(hostb).view(torch.int32), non_blocking=True)
-        nd = torch.from_numpy(norms).to(dev, non_blocking=False)
-        y = plan.qsgd_decode_packed(pd, level, nd)
-        torch.cuda.current_stream(dev).synchronize()
-        return y, plan
-    np_dt = _QSGD_NUMPY_DTYPES[width]
-    itemsize = np.dtype(np_dt).itemsize
-    host = _STAGING.get("decode", plan.arena_end * itemsize).numpy().view(np_dt)
-    norms = np.zeros(plan.nt, dtype=np.float32)
-    for i, (L, o) in enumerate(zip(layers, plan.offsets)):
-        q = np.frombuffer(L.values_data, dtype=np_dt)
-        host[o:o + q.size] = q
-        norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
-    qd = torch.empty(plan.arena_end, dtype=_QSGD_TORCH_DTYPES[width], device=dev)
-    qd.copy_(torch.from_numpy(host), non_blocking=True)  # one H2D of every payload
-    nd = torch.from_numpy(norms).to(dev, non_blocking=False)
-    y = plan.qsgd_decode(qd, width, level, nd)
+        qd = torch.empty(words, dtype=torch.int32, device=dev)
+        items = [(o * width // 8, (lambda L=L: L.values_data)) for L, o in zip(layers, plan.offsets)]
+        hostio.bytes_to_device(items, qd, 4 * words)
+        y = plan.qsgd_decode_packed(qd, level, nd)
+    else:
+        isz = width // 8
+        qd = torch.empty(plan.arena_end, dtype=_QSGD_TORCH_DTYPES[width], device=dev)
+        items = [(o * isz, (lambda L=L: L.values_data)) for L, o in zip(layers, plan.offsets)]
+        hostio.bytes_to_device(items, qd, isz * plan.arena_end)
+        y = plan.qsgd_decode(qd, width, level, nd)
     # the staging buffer is reused by the next call: make sure this copy has been consumed
     torch.cuda.current_stream(dev).synchronize()
     return y, plan
@@ -547,4 +527,5 @@ __all__: List[str] = [
     "qsgd_layer_from_payload",
     "qsgd_packed_layer_from_payload",
     "topk_layer_from_payload",
+    "wire_size",
 ]

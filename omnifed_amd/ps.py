@@ -34,7 +34,7 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-from . import codec
+from . import codec, hostio
 from .shapes import numel
 
 
@@ -133,21 +133,32 @@ class DeviceAggregator:
                 raise ValueError("mixed QSGD width/level within one update")
             if width not in (8, 32) or level <= 0:
                 raise ValueError(f"unsupported QSGD width={width} / level={level}")
-            np_dt = np.int8 if width == 8 else np.int32
-            host = np.zeros(self.plan.arena_end, dtype=np_dt)
+            isz = width // 8
             norms = np.zeros(self.plan.nt, dtype=np.float32)  # absent tensors: norm 0 adds +0
-            for L in qsgd:
+            # one payload per name (a repeated name: the last one, as the reference's decoded dict),
+            # in ascending arena offsets
+            order = sorted({L.layer_name: L for L in qsgd}.values(), key=lambda L: self.index[L.layer_name])
+            items = []
+            for L in order:
                 i = self.index[L.layer_name]
-                o, n = self.plan.offsets[i], self.plan.sizes[i]
-                q = np.frombuffer(L.values_data, dtype=np_dt)
-                if q.size != n:
-                    raise ValueError(f"QSGD layer {L.layer_name!r}: {q.size} values, expected {n}")
-                host[o:o + n] = q
                 norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
-            qd = torch.from_numpy(host).to(self.device)
+                items.append((self.plan.offsets[i] * isz, (lambda L=L: L.values_data)))
+
+            def check(k, payload):
+                n = self.plan.sizes[self.index[order[k].layer_name]]
+                if len(payload) != n * isz:
+                    raise ValueError(f"QSGD layer {order[k].layer_name!r}: {len(payload) // isz} values, expected {n}")
+
+            qd = torch.empty(self.plan.payload_elems(width), dtype=torch.int8 if width == 8 else torch.int32,
+                             device=self.device)
             nd = torch.from_numpy(norms).to(self.device)
-            # Tensors absent from this update keep acc += (0 * q)/L = +0 (q is zero there).
+            # the payloads through pinned staging, chunk by chunk (omnifed_amd.hostio); validated
+            # before anything reaches the accumulator
+            hostio.bytes_to_device(items, qd, isz * self.plan.payload_elems(width), key="ps_decode", check=check)
+            # Tensors absent from this update keep acc += (0 * q)/L = +0 (whatever q holds there:
+            # any int8 / int32 level times a zero norm is a zero).
             self.plan.qsgd_decode(qd, width, level, nd, y_out=self.acc, accumulate=True)
+            torch.cuda.current_stream(self.device).synchronize()  # the staging is reused by the next update
         for L in layers:
             if L.layer_name not in self.index or L.compression_type == "QSGDQuantCompression":
                 continue

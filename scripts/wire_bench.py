@@ -1,9 +1,10 @@
 """Host-inclusive wire path timing: the drop-in's user-visible API on Llama-400M.
 
-encode_updates_dict : device gradients -> one encode launch -> one pinned D2H of the
-                      int8 payload arena -> 183 LayerState messages (bytes copies)
-decode_updates_dict : LayerStates -> pinned staging -> one H2D -> one decode launch
-                      (device="cuda": stays on the GPU; default: CPU tensors, as the reference)
+encode_updates_dict : device gradients -> one encode launch -> chunked pinned D2H of the
+                      int8 payload arena -> bytes filled by worker threads -> 183 LayerState
+                      messages (omnifed_amd.hostio)
+decode_updates_dict : LayerStates -> pinned staging (worker threads) -> chunked H2D -> one
+                      decode launch (device="cuda": stays on the GPU; default: CPU tensors)
 decode_updates_into : client downlink straight into the model's device tensors
 """
 import json
@@ -39,14 +40,23 @@ def tm(fn, reps=3):
     return sorted(ts)[len(ts) // 2]
 
 
-layers = encode_updates_dict(upd, comp)
-res = {"config": cfg, "elements": N, "tensors": len(named),
+stats = {}
+layers = encode_updates_dict(upd, comp, stats=stats)
+from omnifed_amd import hostio  # noqa: E402
+res = {"config": cfg, "elements": N, "tensors": len(named), "wire": stats, "copy_threads": hostio.workers(),
+       "agg_accumulate_layers_ms": None,
        "encode_updates_dict_ms": tm(lambda: encode_updates_dict(upd, comp)) * 1e3,
        "decode_updates_dict_gpu_ms": tm(lambda: decode_updates_dict(layers, device=dev)) * 1e3,
        "decode_updates_into_ms": tm(lambda: decode_updates_into(layers, targets)) * 1e3,
        "decode_updates_dict_cpu_ms": tm(lambda: decode_updates_dict(layers)) * 1e3}
-# fused PS step (omf_ps_apply_encode) vs divide + encode, device-resident
+# the PS uplink: one client's LayerStates decode-accumulated into the aggregator arena
 from omnifed_amd import codec  # noqa: E402
+from omnifed_amd.ps import DeviceAggregator  # noqa: E402
+
+agg = DeviceAggregator(named, device=dev)
+res["agg_accumulate_layers_ms"] = round(tm(lambda: agg.accumulate_layers(layers, number_samples=1)) * 1e3, 2)
+del agg
+# fused PS step (omf_ps_apply_encode) vs divide + encode, device-resident
 
 plan = codec.Plan.get([t.numel() for t in upd.values()], device=dev)
 acc = torch.randn(plan.arena_end, device=dev, generator=g)

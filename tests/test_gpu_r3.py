@@ -308,8 +308,9 @@ def test_topk_tiled_decode_matches_scatter(gpu):
     contents of y are overwritten everywhere."""
     sizes = [5, 70001, 1 << 20, 3000, 200_003, 65536, 131_071]
     plan = codec.Plan(sizes, device=gpu)
-    ratio = 0.05
+    ratio = 0.01
     ks = plan.topk_ks(ratio)
+    assert ks[2] <= 16384
     g = torch.Generator(device=gpu).manual_seed(12)
     vals, idx = [], []
     for t, (n, k) in enumerate(zip(sizes, ks)):
