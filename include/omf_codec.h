@@ -280,11 +280,13 @@ int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, con
                           int32_t mode, void* stream);
 /* omf_topk_decode_arena with a caller workspace of omf_topk_decode_workspace_bytes(plan, ratio)
  * bytes (256-byte aligned): mode 0 then writes the arena in ONE streaming pass — the values are
- * bucketed by 64 Ki-element super-tile and each 16 Ki-element sub-tile is built in LDS (zeros +
- * its values) and stored whole — instead of a fill followed by scattered 4-byte stores (which
- * reach HBM as partial-line read-modify-writes).  Same bytes as omf_topk_decode_arena (indices
- * unique per tensor; the reference's zeros().scatter_ leaves a duplicate's last value, which
- * neither decoder promises).  Modes 1/2 and arenas over 2^30 elements ignore the workspace. */
+ * placed into per-super-tile buckets (64 Ki arena elements; capacity twice the expected count +
+ * 256, an overflow list past it) and each 8 Ki-element sub-tile is built in LDS (zeros + its
+ * values) and stored whole — instead of a fill followed by scattered 4-byte stores (which reach
+ * HBM as partial-line read-modify-writes).  Same bytes as omf_topk_decode_arena (indices unique
+ * per tensor; the reference's zeros().scatter_ leaves a duplicate's last value, which neither
+ * decoder promises).  The first call of a plan at a ratio uploads the plan's bucket tables
+ * (synchronous, once).  Modes 1/2 and arenas over 2^30 elements ignore the workspace. */
 size_t omf_topk_decode_workspace_bytes(const omf_plan* plan, double ratio);
 int omf_topk_decode_arena_ws(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
                              int32_t mode, void* ws, size_t ws_bytes, void* stream);

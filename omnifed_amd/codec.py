@@ -107,6 +107,7 @@ class Plan:
         self._lock = threading.Lock()
         self._topk_ws: Dict[int, torch.Tensor] = {}  # per stream: launches on two streams never share one
         self._dec_ws: Dict[int, torch.Tensor] = {}   # tiled Top-K decode workspace, per stream
+        self._dec_need: Dict[float, int] = {}
         self._topk_cache: Dict[float, tuple] = {}
         # the library's choice (by arena size, or OMF_ENCODE_STRATEGY)
         self.strategy = STRATEGIES[int(L.omf_plan_encode_strategy(h))]
@@ -431,7 +432,10 @@ class Plan:
         st = stream if stream is not None else _stream(dev)
         L = lib()
         if mode == 0 and y.data_ptr() % 16 == 0:  # one streaming write of the arena (tiled decode)
-            need = int(L.omf_topk_decode_workspace_bytes(self._h, float(ratio)))
+            key = float(ratio)
+            need = self._dec_need.get(key)
+            if need is None:
+                need = self._dec_need[key] = int(L.omf_topk_decode_workspace_bytes(self._h, key))
             with self._lock:
                 ws = self._dec_ws.get(st)
                 if ws is None or ws.numel() < need:

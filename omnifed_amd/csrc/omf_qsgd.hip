@@ -1138,6 +1138,14 @@ struct omf_plan {
   uint32_t* d_dec_binfo = nullptr;
   uint32_t* d_spec_flags = nullptr;
   uint32_t* d_spec_status = nullptr;
+  // Top-K tiled decode: per-ratio constant tables (omf_topk.hip), allocated on first use, with
+  // one host word each (the table's size facts)
+  struct TopkTable {
+    uint64_t key;
+    void* dev;
+    uint64_t host;
+  };
+  std::vector<TopkTable> topk_tables;
   // Launches that use the sync block / granules are ordered across streams: a launch on a
   // stream other than the previous one first waits for the previous launch's event.
   hipEvent_t last_ev = nullptr;
@@ -1170,6 +1178,24 @@ int64_t arena_end(const omf_plan* p) { return p->arena_end; }
 const int64_t* d_sizes(const omf_plan* p) { return p->d_sizes; }
 const int64_t* d_begins(const omf_plan* p) { return p->d_begins; }
 const std::vector<int64_t>& sizes(const omf_plan* p) { return p->sizes; }
+// A plan-owned device buffer of `bytes` for `key` (allocated, and *fresh set, on first use;
+// not on the hot path after that), with a host word the caller keeps beside it.  nullptr if
+// the allocation fails.
+void* topk_table(omf_plan* p, uint64_t key, size_t bytes, bool* fresh, uint64_t** host) {
+  *fresh = false;
+  for (auto& e : p->topk_tables)
+    if (e.key == key) {
+      *host = &e.host;
+      return e.dev;
+    }
+  void* d = nullptr;
+  if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+  p->topk_tables.push_back({key, d, 0});
+  *host = &p->topk_tables.back().host;
+  *fresh = true;
+  return d;
+}
+const std::vector<int64_t>& offsets(const omf_plan* p) { return p->offsets; }
 }  // namespace omf_plan_access
 
 static size_t round16(size_t b) { return (b + 15) & ~(size_t)15; }
@@ -1581,6 +1607,7 @@ int omf_plan_destroy(omf_plan* plan) {
   DeviceGuard g(plan->device);
   if (plan->last_ev) (void)hipEventDestroy(plan->last_ev);
   if (plan->d_block) (void)hipFree(plan->d_block);
+  for (auto& e : plan->topk_tables) (void)hipFree(e.dev);
   delete plan;
   return OMF_OK;
 }

@@ -1331,56 +1331,22 @@ __global__ __launch_bounds__(kThreads) void topk_scatter_arena(const float* __re
 // ---------------------------------------------------------------- tiled zero-fill decode (mode 0)
 // y := 0 over the whole arena, then y[begin_t + idx] = v for one client's selection, as ONE
 // streaming write of the arena: the scattered 4-byte stores of a fill-then-scatter decode reach
-// HBM as partial-line read-modify-writes (3.7x their bytes, profiles/r02), so the values are
-// first bucketed by 64 Ki-element super-tile of the arena (count, scan, place: 12k bytes read
-// twice, 8k written), then one workgroup per super-tile builds each 16 Ki-element sub-tile in
-// LDS (zeros + its values) and streams it out with 16-byte non-temporal stores.
+// HBM as partial-line read-modify-writes (3.7x their bytes, profiles/r02).  So the values are
+// first placed into per-super-tile buckets (64 Ki arena elements each; a bucket's capacity is
+// twice the selection's expected count there + 256, fixed per (plan, ratio); what does not fit
+// goes to an overflow list), then one workgroup per super-tile stages its bucket in LDS, builds
+// each 8 Ki-element sub-tile in LDS (zeros + its values) and streams it out with 16-byte
+// non-temporal stores; a last kernel applies the (normally empty) overflow list.
 constexpr int kDecSuperBits = 16;
-constexpr int kDecSubBits = 14;
+constexpr int kDecSubBits = 13;
 constexpr int kDecSubs = 1 << (kDecSuperBits - kDecSubBits);
-constexpr int kDecMaxSuper = 16384;  // LDS bins of the count / place blocks (arenas <= 2^30 elements)
-constexpr int kDecChunk = 4096;      // selected values per count / place block
+constexpr int kDecMaxSuper = 16384;  // LDS bins of a place block (arenas <= 2^30 elements)
+constexpr int kDecChunk = 4096;      // selected values per place block
 constexpr int kDecTileThreads = 512;
+constexpr int kDecStage = 2048;      // bucket entries a tile workgroup stages in LDS (more: read from L2)
 
-// k_t prefix of the plan's tensors at `ratio` (exactly omf_topk_k), in LDS, by the whole block.
-template <int NT>
-__device__ __forceinline__ void dec_koff(const int64_t* __restrict__ sizes, int nt, double ratio, int64_t* koff,
-                                         int64_t* s_part) {
-  constexpr int PER = kArenaMaxTensors / NT;
-  int64_t kv[PER], loc = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int t = threadIdx.x * PER + j;
-    int64_t k = 0;
-    if (t < nt) {
-      k = (int64_t)((double)sizes[t] * ratio);
-      if (k < 1) k = 1;
-    }
-    kv[j] = k;
-    loc += k;
-  }
-  s_part[threadIdx.x] = loc;
-  __syncthreads();
-  for (int o = 1; o < NT; o <<= 1) {
-    const int64_t add = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0;
-    __syncthreads();
-    s_part[threadIdx.x] += add;
-    __syncthreads();
-  }
-  int64_t run = s_part[threadIdx.x] - loc;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) {
-    const int t = threadIdx.x * PER + j;
-    if (t <= nt) koff[t] = run;
-    run += kv[j];
-  }
-  if (threadIdx.x == NT - 1) koff[nt] = s_part[NT - 1];
-  __syncthreads();
-}
-
-__device__ __forceinline__ int dec_tensor_of(const int64_t* koff, int nt, int64_t j) {
-  int lo = 0, hi = nt - 1;  // koff[t] <= j < koff[t + 1]
-  while (lo < hi) {
+__device__ __forceinline__ int dec_tensor_of(const int64_t* __restrict__ koff, int lo, int hi, int64_t j) {
+  while (lo < hi) {  // koff[t] <= j < koff[t + 1]
     const int mid = (lo + hi + 1) >> 1;
     if (koff[mid] <= j) lo = mid;
     else hi = mid - 1;
@@ -1388,134 +1354,117 @@ __device__ __forceinline__ int dec_tensor_of(const int64_t* koff, int nt, int64_
   return lo;
 }
 
-// Count (PLACE = false) or place (PLACE = true) the selection's values by super-tile.  One block
-// per kDecChunk consecutive values (one or a few tensors, so a narrow super-tile range): LDS
-// counts over the block's range, one global atomic per touched super-tile; placing takes the
-// block's slots from the scanned cursors and writes (position in the super-tile << 32 | value).
-template <bool PLACE>
-__global__ __launch_bounds__(kThreads) void topk_dec_bucket(const float* __restrict__ values,
-                                                            const int64_t* __restrict__ indices,
-                                                            const int64_t* __restrict__ sizes,
-                                                            const int64_t* __restrict__ begins, int nt, double ratio,
-                                                            int64_t ktot, uint32_t* __restrict__ cnt,
-                                                            uint32_t* __restrict__ cur, uint64_t* __restrict__ pairs) {
-  __shared__ int64_t koff[kArenaMaxTensors + 1];
-  __shared__ int64_t s_part[kThreads];
-  extern __shared__ uint32_t h[];  // min(nsuper, kDecMaxSuper) bins (dynamic)
-  dec_koff<kThreads>(sizes, nt, ratio, koff, s_part);
+// Place one block of kDecChunk consecutive selected values into their super-tiles' buckets:
+// LDS counts over the block's super-tile range, one global reservation per touched super-tile,
+// then (position in the super-tile << 32 | value bits) at its slot, or into the overflow list
+// (arena position << 32 | value bits) past the bucket's capacity.
+__global__ __launch_bounds__(kThreads) void topk_dec_place(const float* __restrict__ values,
+                                                           const int64_t* __restrict__ indices,
+                                                           const int64_t* __restrict__ sizes,
+                                                           const int64_t* __restrict__ begins,
+                                                           const int64_t* __restrict__ koff, int nt, int64_t ktot,
+                                                           const uint32_t* __restrict__ cap_base,
+                                                           uint32_t* __restrict__ fill, uint64_t* __restrict__ pairs,
+                                                           uint32_t* __restrict__ ovf_cnt, uint64_t* __restrict__ ovf) {
+  extern __shared__ uint32_t h[];  // the block's super-tile range (dynamic, <= kDecMaxSuper)
+  __shared__ int s_t[2];
   const int64_t j0 = (int64_t)blockIdx.x * kDecChunk, j1 = min(j0 + kDecChunk, ktot);
-  const int tf = dec_tensor_of(koff, nt, j0), tl = dec_tensor_of(koff, nt, j1 - 1);
-  const uint32_t s_lo = (uint32_t)(begins[tf] >> kDecSuperBits);
-  const uint32_t nbin = (uint32_t)((begins[tl] + sizes[tl] - 1) >> kDecSuperBits) - s_lo + 1;  // <= kDecMaxSuper
-  for (uint32_t b = threadIdx.x; b < nbin; b += kThreads) h[b] = 0;
+  if (threadIdx.x == 0) {
+    s_t[0] = dec_tensor_of(koff, 0, nt - 1, j0);
+    s_t[1] = dec_tensor_of(koff, s_t[0], nt - 1, j1 - 1);
+  }
   __syncthreads();
+  const int tf = s_t[0], tl = s_t[1];
+  const uint32_t s_lo = (uint32_t)(begins[tf] >> kDecSuperBits);
+  const uint32_t nbin = (uint32_t)((begins[tl] + sizes[tl] - 1) >> kDecSuperBits) - s_lo + 1;
+  for (uint32_t b = threadIdx.x; b < nbin; b += kThreads) h[b] = 0;
   constexpr int U = kDecChunk / kThreads;
   int64_t pos[U];
   float val[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {  // every load issued before any is used
-    const int64_t j = j0 + threadIdx.x + (int64_t)u * kThreads;
-    const int64_t jc = j < j1 ? j : j1 - 1;
-    pos[u] = indices[jc];
-    val[u] = PLACE ? values[jc] : 0.0f;
+    const int64_t j = min(j0 + threadIdx.x + (int64_t)u * kThreads, j1 - 1);
+    pos[u] = indices[j];
+    val[u] = values[j];
   }
+  __syncthreads();  // h zeroed
+  uint32_t rank[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t j = j0 + threadIdx.x + (int64_t)u * kThreads;
-    if (j >= j1) { pos[u] = -1; continue; }
-    const int t = dec_tensor_of(koff, nt, j);
+    const int t = tf == tl ? tf : dec_tensor_of(koff, tf, tl, j);
     const int64_t i = pos[u];
-    pos[u] = (i < 0 || i >= sizes[t]) ? -1 : begins[t] + i;  // padding (-1) / out of range: skipped
-    if (!PLACE && pos[u] >= 0) atomicAdd(&h[(uint32_t)(pos[u] >> kDecSuperBits) - s_lo], 1u);
-  }
-  if (!PLACE) {
-    __syncthreads();
-    for (uint32_t b = threadIdx.x; b < nbin; b += kThreads)
-      if (h[b]) atomicAdd(&cnt[s_lo + b], h[b]);
-    return;
-  }
-  uint32_t rank[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u)
+    pos[u] = (j >= j1 || i < 0 || i >= sizes[t]) ? -1 : begins[t] + i;  // padding / out of range: skipped
     rank[u] = pos[u] >= 0 ? atomicAdd(&h[(uint32_t)(pos[u] >> kDecSuperBits) - s_lo], 1u) : 0u;
+  }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbin; b += kThreads)
-    if (h[b]) h[b] = atomicAdd(&cur[s_lo + b], h[b]);  // this block's first slot of the super-tile
+    if (h[b]) h[b] = atomicAdd(&fill[s_lo + b], h[b]);  // this block's first slot in the bucket
   __syncthreads();
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (pos[u] < 0) continue;
     const uint32_t s = (uint32_t)(pos[u] >> kDecSuperBits);
-    const uint32_t in = (uint32_t)(pos[u] & ((1 << kDecSuperBits) - 1));
-    pairs[h[s - s_lo] + rank[u]] = ((uint64_t)in << 32) | (uint64_t)__float_as_uint(val[u]);
+    const uint32_t slot = h[s - s_lo] + rank[u], base = cap_base[s], cap = cap_base[s + 1] - base;
+    const uint64_t vb = (uint64_t)__float_as_uint(val[u]);
+    if (slot < cap) {
+      pairs[(uint64_t)base + slot] = ((uint64_t)(pos[u] & ((1 << kDecSuperBits) - 1)) << 32) | vb;
+    } else {  // bucket full (a selection far denser here than expected): the overflow list
+      ovf[atomicAdd(ovf_cnt, 1u)] = ((uint64_t)pos[u] << 32) | vb;
+    }
   }
 }
 
-// Exclusive scan of the super-tile counts (one block): start[s] (nsuper + 1 entries) and the
-// placing cursors; the counts are zeroed for the next call.
-__global__ __launch_bounds__(1024) void topk_dec_scan(uint32_t* __restrict__ cnt, int32_t nsuper,
-                                                      uint32_t* __restrict__ start, uint32_t* __restrict__ cur) {
-  __shared__ uint32_t s_w[16];
-  uint32_t carry = 0;
-  for (int32_t s0 = 0; s0 < nsuper; s0 += 4096) {
-    uint32_t c[4], loc = 0;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int32_t s = s0 + 4 * (int32_t)threadIdx.x + q;
-      c[q] = s < nsuper ? cnt[s] : 0u;
-      loc += c[q];
-    }
-    uint32_t tot;
-    const uint32_t inc = block_scan_incl<1024>(loc, s_w, tot);
-    uint32_t run = carry + inc - loc;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int32_t s = s0 + 4 * (int32_t)threadIdx.x + q;
-      if (s < nsuper) {
-        start[s] = run;
-        cur[s] = run;
-        cnt[s] = 0u;
-      }
-      run += c[q];
-    }
-    carry += tot;
-  }
-  if (threadIdx.x == 0) start[nsuper] = carry;
-}
-
-// One workgroup per super-tile: each 16 Ki-element sub-tile is zeroed in LDS, gets its values
-// (the super-tile's list is re-read per sub-tile from L2), and is streamed out (non-temporal
-// float4; the arena's partial last super-tile element by element).
+// One workgroup per super-tile: its bucket staged in LDS (up to kDecStage entries; a larger
+// one is read from L2 per sub-tile), then per 8 Ki-element sub-tile: zeros in LDS, its values,
+// 16-byte non-temporal stores (the arena's partial last sub-tile element by element).
 __global__ __launch_bounds__(kDecTileThreads) void topk_dec_tiles(const uint64_t* __restrict__ pairs,
-                                                                  const uint32_t* __restrict__ start,
+                                                                  const uint32_t* __restrict__ cap_base,
+                                                                  const uint32_t* __restrict__ fill,
                                                                   float* __restrict__ y, int64_t arena_end) {
   __shared__ float4 tile[(1 << kDecSubBits) / 4];
+  __shared__ uint64_t stage[kDecStage];
   float* tf = reinterpret_cast<float*>(tile);
   const uint32_t s = blockIdx.x;
-  const uint32_t p0 = start[s], p1 = start[s + 1];
+  const uint32_t base = cap_base[s];
+  const uint32_t cnt = min(fill[s], cap_base[s + 1] - base);
+  const bool staged = cnt <= (uint32_t)kDecStage;
+  const uint64_t* src = staged ? stage : pairs + base;
+  if (staged)
+    for (uint32_t p = threadIdx.x; p < cnt; p += kDecTileThreads) stage[p] = pairs[base + p];
   constexpr int Q = (1 << kDecSubBits) / 4 / kDecTileThreads;  // float4 per thread per sub-tile
   for (int sub = 0; sub < kDecSubs; ++sub) {
-    const int64_t base = ((int64_t)s << kDecSuperBits) + ((int64_t)sub << kDecSubBits);
-    if (base >= arena_end) break;  // block-uniform
+    const int64_t b0 = ((int64_t)s << kDecSuperBits) + ((int64_t)sub << kDecSubBits);
+    if (b0 >= arena_end) break;  // block-uniform
 #pragma unroll
     for (int q = 0; q < Q; ++q) tile[threadIdx.x + q * kDecTileThreads] = make_float4(0.f, 0.f, 0.f, 0.f);
-    __syncthreads();
-    for (uint32_t p = p0 + threadIdx.x; p < p1; p += kDecTileThreads) {
-      const uint64_t pr = pairs[p];
+    __syncthreads();  // (also: the staged bucket is complete)
+    for (uint32_t p = threadIdx.x; p < cnt; p += kDecTileThreads) {
+      const uint64_t pr = src[p];
       const uint32_t in = (uint32_t)(pr >> 32);
       if ((int)(in >> kDecSubBits) == sub) tf[in & ((1u << kDecSubBits) - 1)] = __uint_as_float((uint32_t)pr);
     }
     __syncthreads();
-    if (base + (1 << kDecSubBits) <= arena_end) {
+    if (b0 + (1 << kDecSubBits) <= arena_end) {
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
         const int e = 4 * (threadIdx.x + q * kDecTileThreads);
-        store_nt(y + base + e, tile[threadIdx.x + q * kDecTileThreads]);
+        store_nt(y + b0 + e, tile[threadIdx.x + q * kDecTileThreads]);
       }
     } else {
-      for (int64_t e = threadIdx.x; base + e < arena_end; e += kDecTileThreads) y[base + e] = tf[e];
+      for (int64_t e = threadIdx.x; b0 + e < arena_end; e += kDecTileThreads) y[b0 + e] = tf[e];
     }
     __syncthreads();
+  }
+}
+
+// The overflow list after the tiles (normally empty: one wave of each block reads the count).
+__global__ __launch_bounds__(kThreads) void topk_dec_overflow(const uint32_t* __restrict__ ovf_cnt,
+                                                              const uint64_t* __restrict__ ovf, float* __restrict__ y) {
+  const uint32_t n = *ovf_cnt;
+  for (uint32_t j = blockIdx.x * kThreads + threadIdx.x; j < n; j += gridDim.x * kThreads) {
+    const uint64_t pr = ovf[j];
+    y[pr >> 32] = __uint_as_float((uint32_t)pr);
   }
 }
 
@@ -1531,6 +1480,8 @@ int64_t arena_end(const omf_plan* p);
 const int64_t* d_sizes(const omf_plan* p);
 const int64_t* d_begins(const omf_plan* p);
 const std::vector<int64_t>& sizes(const omf_plan* p);
+const std::vector<int64_t>& offsets(const omf_plan* p);
+void* topk_table(omf_plan* p, uint64_t key, size_t bytes, bool* fresh, uint64_t** host);
 }  // namespace omf_plan_access
 
 namespace {
@@ -1884,22 +1835,16 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   return OMF_OK;
 }
 
-// Tiled zero-fill decode workspace: [cnt nsuper][start nsuper + 1][cur nsuper][pairs ktot x 8 B].
-struct DecWs {
-  size_t cnt, start, cur, pairs, total;
-  int32_t nsuper;
+// Tiled zero-fill decode.  Plan-owned constant tables per ratio (omf_plan_access::topk_table):
+// koff[nt + 1] (int64: each tensor's first selected value) and cap_base[nsuper + 1] (uint32:
+// the buckets' prefix of capacities).  Caller workspace: fill[nsuper] + the overflow count
+// (zeroed by the call), the buckets (cap_base[nsuper] entries) and the overflow list (ktot).
+struct DecTables {
+  int64_t* koff = nullptr;
+  uint32_t* cap_base = nullptr;
+  int32_t nsuper = 0;
+  uint64_t cap_total = 0;
 };
-static DecWs dec_ws_layout(const omf_plan* p, int64_t ktot) {
-  DecWs d;
-  d.nsuper = (int32_t)((omf_plan_access::arena_end(p) + (1 << kDecSuperBits) - 1) >> kDecSuperBits);
-  size_t o = 0;
-  d.cnt = o; o = align256(o + 4 * (size_t)d.nsuper);
-  d.start = o; o = align256(o + 4 * ((size_t)d.nsuper + 1));
-  d.cur = o; o = align256(o + 4 * (size_t)d.nsuper);
-  d.pairs = o; o = align256(o + 8 * (size_t)std::max<int64_t>(ktot, 1));
-  d.total = o;
-  return d;
-}
 
 static int64_t decode_ktot(const omf_plan* plan, double ratio) {
   int64_t ktot = 0;
@@ -1911,10 +1856,89 @@ static int64_t decode_ktot(const omf_plan* plan, double ratio) {
   return ktot;
 }
 
+// Host computation of the tables (also sizes the workspace): bucket capacity = 2 x the
+// expected count of the super-tile (each tensor's k spread over its elements) + 256.
+static void dec_tables_host(const omf_plan* p, double ratio, std::vector<int64_t>& koff, std::vector<uint32_t>& cap_base,
+                            int32_t& nsuper) {
+  const std::vector<int64_t>& sizes = omf_plan_access::sizes(p);
+  const int32_t nt = (int32_t)sizes.size();
+  const int64_t ae = omf_plan_access::arena_end(p);
+  nsuper = (int32_t)((ae + (1 << kDecSuperBits) - 1) >> kDecSuperBits);
+  koff.assign((size_t)nt + 1, 0);
+  std::vector<double> expect((size_t)nsuper, 0.0);
+  const std::vector<int64_t>& begins = omf_plan_access::offsets(p);
+  for (int32_t t = 0; t < nt; ++t) {
+    const int64_t n = sizes[t], k = omf_topk_k(n, ratio);
+    koff[(size_t)t + 1] = koff[(size_t)t] + k;
+    const int64_t begin = begins[t];
+    const double dens = (double)k / (double)n;
+    for (int64_t s0 = begin >> kDecSuperBits; s0 <= (begin + n - 1) >> kDecSuperBits; ++s0) {
+      const int64_t lo = std::max(begin, s0 << kDecSuperBits), hi = std::min(begin + n, (s0 + 1) << kDecSuperBits);
+      expect[(size_t)s0] += dens * (double)(hi - lo);
+    }
+  }
+  cap_base.assign((size_t)nsuper + 1, 0);
+  for (int32_t q = 0; q < nsuper; ++q) {
+    const uint64_t cap = std::min<uint64_t>((uint64_t)std::ceil(2.0 * expect[(size_t)q]) + 256, (uint64_t)1 << kDecSuperBits);
+    cap_base[(size_t)q + 1] = cap_base[(size_t)q] + (uint32_t)cap;
+  }
+}
+
+struct DecWs {
+  size_t fill, pairs, ovf, total;
+};
+static DecWs dec_ws_layout(int32_t nsuper, uint64_t cap_total, int64_t ktot) {
+  DecWs d;
+  size_t o = 0;
+  d.fill = o; o = align256(o + 4 * ((size_t)nsuper + 1));  // + the overflow count
+  d.pairs = o; o = align256(o + 8 * (size_t)std::max<uint64_t>(cap_total, 1));
+  d.ovf = o; o = align256(o + 8 * (size_t)std::max<int64_t>(ktot, 1));
+  d.total = o;
+  return d;
+}
+
+static uint64_t ratio_key(double ratio) {
+  uint64_t k;
+  std::memcpy(&k, &ratio, 8);
+  return k;
+}
+
+// The plan's tables for `ratio` (computed and uploaded on first use; the bucket total is
+// kept in the table's host word).
+static int dec_tables(omf_plan* p, double ratio, DecTables* out) {
+  const int32_t nt = omf_plan_access::ntensors(p);
+  const int64_t ae = omf_plan_access::arena_end(p);
+  const int32_t nsuper = (int32_t)((ae + (1 << kDecSuperBits) - 1) >> kDecSuperBits);
+  const size_t bytes = align256(8 * ((size_t)nt + 1)) + 4 * ((size_t)nsuper + 1);
+  bool fresh = false;
+  uint64_t* host = nullptr;
+  void* d = omf_plan_access::topk_table(p, ratio_key(ratio), bytes, &fresh, &host);
+  if (!d) return fail(OMF_ENOMEM, "omf_topk_decode_arena: table allocation failed");
+  out->koff = static_cast<int64_t*>(d);
+  out->cap_base = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d) + align256(8 * ((size_t)nt + 1)));
+  out->nsuper = nsuper;
+  if (fresh) {
+    std::vector<int64_t> koff;
+    std::vector<uint32_t> cap_base;
+    int32_t ns = 0;
+    dec_tables_host(p, ratio, koff, cap_base, ns);
+    OMF_HIP(hipMemcpy(out->koff, koff.data(), 8 * koff.size(), hipMemcpyHostToDevice));
+    OMF_HIP(hipMemcpy(out->cap_base, cap_base.data(), 4 * cap_base.size(), hipMemcpyHostToDevice));
+    *host = cap_base.back();
+  }
+  out->cap_total = *host;
+  return OMF_OK;
+}
+
 size_t omf_topk_decode_workspace_bytes(const omf_plan* plan, double ratio) {
   if (!plan || !(ratio == ratio)) return 0;
   const int64_t ktot = decode_ktot(plan, ratio);
-  return ktot < 0 ? 0 : dec_ws_layout(plan, ktot).total;
+  if (ktot < 0) return 0;
+  std::vector<int64_t> koff;
+  std::vector<uint32_t> cap_base;
+  int32_t nsuper = 0;
+  dec_tables_host(plan, ratio, koff, cap_base, nsuper);
+  return dec_ws_layout(nsuper, cap_base.back(), ktot).total;
 }
 
 int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
@@ -1936,31 +1960,29 @@ int omf_topk_decode_arena_ws(omf_plan* plan, double ratio, const float* values, 
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   hipStream_t st = (hipStream_t)stream;
   const int64_t ae = omf_plan_access::arena_end(plan);
-  if (mode == 0 && ws) {
-    const DecWs d = dec_ws_layout(plan, ktot);
+  if (mode == 0 && ws && ((ae + (1 << kDecSuperBits) - 1) >> kDecSuperBits) <= kDecMaxSuper) {
+    // one streaming write of the arena (larger arenas: fill + scatter below)
+    DecTables tb;
+    if (int r = dec_tables(plan, ratio, &tb)) return r;
+    const DecWs d = dec_ws_layout(tb.nsuper, tb.cap_total, ktot);
     if (ws_bytes < d.total) return fail(OMF_EINVAL, "omf_topk_decode_arena: workspace too small");
     if (((uintptr_t)ws & 255) || ((uintptr_t)y & 15)) return fail(OMF_EINVAL, "omf_topk_decode_arena: misaligned buffer");
-    if (d.nsuper <= kDecMaxSuper) {  // one streaming write of the arena (larger arenas: fill + scatter)
-      uint8_t* w = static_cast<uint8_t*>(ws);
-      uint32_t* cnt = reinterpret_cast<uint32_t*>(w + d.cnt);
-      uint32_t* start = reinterpret_cast<uint32_t*>(w + d.start);
-      uint32_t* cur = reinterpret_cast<uint32_t*>(w + d.cur);
-      uint64_t* pairs = reinterpret_cast<uint64_t*>(w + d.pairs);
-      const int64_t* sizes = omf_plan_access::d_sizes(plan);
-      const int64_t* begins = omf_plan_access::d_begins(plan);
-      OMF_HIP(hipMemsetAsync(cnt, 0, 4 * (size_t)d.nsuper, st));
-      const dim3 gb((unsigned)std::max<int64_t>(1, (ktot + kDecChunk - 1) / kDecChunk));
-      const size_t lds = 4 * (size_t)d.nsuper;
-      hipLaunchKernelGGL(topk_dec_bucket<false>, gb, dim3(kThreads), lds, st, values, indices, sizes, begins, (int)nt,
-                         ratio, ktot, cnt, cur, pairs);
-      hipLaunchKernelGGL(topk_dec_scan, dim3(1), dim3(1024), 0, st, cnt, d.nsuper, start, cur);
-      hipLaunchKernelGGL(topk_dec_bucket<true>, gb, dim3(kThreads), lds, st, values, indices, sizes, begins, (int)nt,
-                         ratio, ktot, cnt, cur, pairs);
-      hipLaunchKernelGGL(topk_dec_tiles, dim3((unsigned)d.nsuper), dim3(kDecTileThreads), 0, st,
-                         (const uint64_t*)pairs, (const uint32_t*)start, y, ae);
-      OMF_HIP(hipGetLastError());
-      return OMF_OK;
-    }
+    uint8_t* w = static_cast<uint8_t*>(ws);
+    uint32_t* fill = reinterpret_cast<uint32_t*>(w + d.fill);
+    uint32_t* ovf_cnt = fill + tb.nsuper;
+    uint64_t* pairs = reinterpret_cast<uint64_t*>(w + d.pairs);
+    uint64_t* ovf = reinterpret_cast<uint64_t*>(w + d.ovf);
+    OMF_HIP(hipMemsetAsync(fill, 0, 4 * ((size_t)tb.nsuper + 1), st));
+    const dim3 gb((unsigned)std::max<int64_t>(1, (ktot + kDecChunk - 1) / kDecChunk));
+    hipLaunchKernelGGL(topk_dec_place, gb, dim3(kThreads), 4 * (size_t)tb.nsuper, st, values, indices,
+                       omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (const int64_t*)tb.koff,
+                       (int)nt, ktot, (const uint32_t*)tb.cap_base, fill, pairs, ovf_cnt, ovf);
+    hipLaunchKernelGGL(topk_dec_tiles, dim3((unsigned)tb.nsuper), dim3(kDecTileThreads), 0, st, (const uint64_t*)pairs,
+                       (const uint32_t*)tb.cap_base, (const uint32_t*)fill, y, ae);
+    hipLaunchKernelGGL(topk_dec_overflow, dim3(64), dim3(kThreads), 0, st, (const uint32_t*)ovf_cnt,
+                       (const uint64_t*)ovf, y);
+    OMF_HIP(hipGetLastError());
+    return OMF_OK;
   }
   if (mode == 0) OMF_HIP(hipMemsetAsync(y, 0, 4 * (size_t)ae, st));
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ktot + kThreads - 1) / kThreads, 4096));

@@ -39,12 +39,33 @@ _bytes_addr = ctypes.pythonapi.PyBytes_AsString
 _bytes_addr.restype = ctypes.c_void_p
 _bytes_addr.argtypes = [ctypes.py_object]
 
-_pool: Optional[ThreadPoolExecutor] = None
+_pool = None
 _pool_lock = threading.Lock()
+_workers: Optional[int] = None
+
+
+class _Inline:
+    """Executor of ``workers() == 0``: every copy runs at once on the calling thread."""
+
+    class _Done:
+        def __init__(self, value):
+            self._value = value
+
+        def result(self):
+            return self._value
+
+    def submit(self, fn, *args):
+        return self._Done(fn(*args))
 
 
 def workers() -> int:
-    """Copy threads: half the CPUs this process may run on, 2..8."""
+    """Copy threads: ``OMF_WIRE_THREADS`` (0 = copy on the calling thread), else half the CPUs
+    this process may run on, 2..8."""
+    if _workers is not None:
+        return _workers
+    env = os.environ.get("OMF_WIRE_THREADS")
+    if env is not None and env.strip().isdigit():
+        return int(env)
     try:
         n = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover - non-Linux
@@ -52,12 +73,23 @@ def workers() -> int:
     return max(2, min(8, n // 2))
 
 
-def pool() -> ThreadPoolExecutor:
+def set_workers(n: Optional[int]) -> None:
+    """Override the copy-thread count (None: back to ``workers()``'s default); tuning hook."""
+    global _workers, _pool
+    with _pool_lock:
+        _workers = None if n is None else max(0, int(n))
+        old, _pool = _pool, None
+    if isinstance(old, ThreadPoolExecutor):
+        old.shutdown(wait=True)
+
+
+def pool():
     global _pool
     if _pool is None:
         with _pool_lock:
             if _pool is None:
-                _pool = ThreadPoolExecutor(max_workers=workers(), thread_name_prefix="omf-wire")
+                n = workers()
+                _pool = ThreadPoolExecutor(max_workers=n, thread_name_prefix="omf-wire") if n > 0 else _Inline()
     return _pool
 
 
@@ -100,31 +132,17 @@ def _groups(spans: Sequence[Tuple[int, int]], limit: int) -> List[Tuple[int, int
     return out
 
 
-def device_to_bytes(src: torch.Tensor, spans: Sequence[Tuple[int, int]], stream=None, key: str = "encode",
-                    limit: int = CHUNK_BYTES) -> Iterator[Tuple[int, bytes]]:
-    """Yield ``(i, bytes)`` for every span i = (byte offset, length) of the device buffer ``src``
-    (ascending offsets; length 0 is skipped), in order, each as soon as its bytes are filled.
-    The device-to-host copies are queued on ``stream`` (default: the current stream of ``src``'s
-    device) behind the work already there."""
-    if stream is None:
-        stream = torch.cuda.current_stream(src.device)
-    raw = src.reshape(-1).view(torch.uint8)
-    total = max((off + n for off, n in spans), default=0)
-    staged = STAGING.get(key, total)
-    groups = _groups(spans, limit)
-    events = []
-    with torch.cuda.stream(stream):
-        for a, b, _ in groups:
-            if b > a:
-                staged[a:b].copy_(raw[a:b], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            events.append(ev)
-    base = staged.data_ptr()
+def fill_bytes(base: int, spans: Sequence[Tuple[int, int]], landed: Callable[[int], None],
+               limit: int = CHUNK_BYTES) -> Iterator[Tuple[int, bytes]]:
+    """Yield ``(i, bytes)`` copies of the host spans i = (byte offset from ``base``, length) in
+    order (length 0 skipped).  Chunk g's ``bytes`` objects are allocated once ``landed(g)``
+    returns and filled by the worker threads while the caller consumes chunk g - 1; at most two
+    chunks of ``bytes`` are alive at a time, so their memory is recycled from one chunk to the
+    next instead of being faulted in fresh."""
     ex = pool()
     pending: List[Tuple[int, bytes, object]] = []
-    for (a, b, idx), ev in zip(groups, events):
-        ev.synchronize()
+    for g, (a, b, idx) in enumerate(_groups(spans, limit)):
+        landed(g)
         filled = []
         for i in idx:
             off, n = spans[i]
@@ -132,43 +150,59 @@ def device_to_bytes(src: torch.Tensor, spans: Sequence[Tuple[int, int]], stream=
                 continue
             obj = _new_bytes(None, n)
             filled.append((i, obj, ex.submit(ctypes.memmove, _bytes_addr(obj), base + off, n)))
-        for i, obj, fut in pending:  # the previous chunk, while this one is copied
-            fut.result()
-            yield i, obj
+        for item in pending:  # the previous chunk, while this one is copied
+            item[2].result()
+            yield item[0], item[1]
         pending = filled
-    for i, obj, fut in pending:
-        fut.result()
-        yield i, obj
+    for item in pending:
+        item[2].result()
+        yield item[0], item[1]
 
 
-def bytes_to_device(items: Sequence[Tuple[int, Callable[[], bytes]]], dst: torch.Tensor, total_bytes: int,
-                    stream=None, key: str = "decode", limit: int = CHUNK_BYTES,
-                    check: Optional[Callable[[int, bytes], None]] = None) -> None:
-    """Copy the payloads ``getter()`` of ``items`` = (byte offset in ``dst``, getter) — ascending
-    offsets, all below ``total_bytes`` — into the device buffer ``dst`` through pinned staging:
-    each payload is handed to a worker thread as soon as it is read, and every ~``limit``-byte
-    chunk goes host-to-device (queued on ``stream``) while the next chunk's payloads are read.
-    ``check(i, payload)`` may raise before item i is copied (copies already started are waited
-    for first).  Returns once the last copy is queued; the caller synchronises the stream before
-    the staging is reused (the next call)."""
+def device_to_bytes(src: torch.Tensor, spans: Sequence[Tuple[int, int]], stream=None, key: str = "encode",
+                    limit: int = CHUNK_BYTES) -> Iterator[Tuple[int, bytes]]:
+    """Yield ``(i, bytes)`` for every span i = (byte offset, length) of the device buffer ``src``
+    (ascending offsets; length 0 is skipped), in order, each as soon as its bytes are filled.
+    The device-to-host copies (one per ~``limit`` bytes, each followed by an event) are queued on
+    ``stream`` (default: the current stream of ``src``'s device) behind the work already there."""
     if stream is None:
-        stream = torch.cuda.current_stream(dst.device)
-    raw = dst.reshape(-1).view(torch.uint8)
-    staged = STAGING.get(key, max(int(total_bytes), 1))
-    base = staged.data_ptr()
-    ex = pool()
-    keep: List[bytes] = []  # alive until their copies are done
-    every: List[object] = []
+        stream = torch.cuda.current_stream(src.device)
+    raw = src.reshape(-1).view(torch.uint8)
+    total = max((off + n for off, n in spans), default=0)
+    staged = STAGING.get(key, max(total, 1))
+    events = []
+    with torch.cuda.stream(stream):
+        for a, b, _ in _groups(spans, limit):
+            if b > a:
+                staged[a:b].copy_(raw[a:b], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            events.append(ev)
+    yield from fill_bytes(staged.data_ptr(), spans, lambda g: events[g].synchronize(), limit)
 
-    def flush(a: int, b: int, futs: List[object]) -> None:
-        for f in futs:
+
+def stage_payloads(items: Sequence[Tuple[int, Callable[[], bytes]]], base: int, total_bytes: int,
+                   flush: Callable[[int, int], None], limit: int = CHUNK_BYTES,
+                   check: Optional[Callable[[int, bytes], None]] = None) -> None:
+    """Copy the payloads ``getter()`` of ``items`` = (byte offset from ``base``, getter) —
+    ascending offsets, all below ``total_bytes`` — into host memory at ``base``: each payload is
+    handed to a worker thread as soon as it is read (protobuf's get-copy, on this thread), and
+    once a ~``limit``-byte chunk [a, b) is complete ``flush(a, b)`` runs (the caller queues its
+    host-to-device copy) while the next chunk is read.  At most two chunks of payloads are alive
+    at a time (their memory is recycled).  ``check(i, payload)`` may raise before item i is
+    copied; copies already started are waited for first."""
+    ex = pool()
+    started: List[object] = []
+    prev = None  # (a, b, futures, payloads) of the chunk being copied
+    ga, gb, futs, held = -1, 0, [], []
+
+    def close(chunk) -> None:
+        a, b, fs, _ = chunk
+        for f in fs:
             f.result()
         if b > a:
-            with torch.cuda.stream(stream):
-                raw[a:b].copy_(staged[a:b], non_blocking=True)
+            flush(a, b)
 
-    prev = None
-    ga, gb, futs = -1, 0, []
     try:
         for i, (off, get) in enumerate(items):
             p = get()
@@ -179,20 +213,39 @@ def bytes_to_device(items: Sequence[Tuple[int, Callable[[], bytes]]], dst: torch
                 raise ValueError("payload past the end of the staging arena")
             if ga < 0:
                 ga = off
-            if futs and off + n - ga > limit:  # close the chunk: copy the previous one to the GPU
+            if futs and off + n - ga > limit:  # this chunk is complete: the previous one goes out
                 if prev is not None:
-                    flush(*prev)
-                prev, ga, futs = (ga, gb, futs), off, []
+                    close(prev)
+                prev, ga, gb, futs, held = (ga, gb, futs, held), off, off, [], []
             if n:
                 f = ex.submit(ctypes.memmove, base + off, _bytes_addr(p), n)
                 futs.append(f)
-                every.append(f)
-                keep.append(p)
+                started.append(f)
+                held.append(p)
             gb = max(gb, off + n)
         if prev is not None:
-            flush(*prev)
+            close(prev)
+            prev = None
         if ga >= 0:
-            flush(ga, gb, futs)
+            close((ga, gb, futs, held))
     finally:
-        for f in every:
+        for f in started:
             f.result()
+
+
+def bytes_to_device(items: Sequence[Tuple[int, Callable[[], bytes]]], dst: torch.Tensor, total_bytes: int,
+                    stream=None, key: str = "decode", limit: int = CHUNK_BYTES,
+                    check: Optional[Callable[[int, bytes], None]] = None) -> None:
+    """``stage_payloads`` into pinned staging, each chunk's host-to-device copy into the device
+    buffer ``dst`` queued on ``stream`` as soon as the chunk is complete.  Returns once the last
+    copy is queued; the caller synchronises the stream before the staging is reused."""
+    if stream is None:
+        stream = torch.cuda.current_stream(dst.device)
+    raw = dst.reshape(-1).view(torch.uint8)
+    staged = STAGING.get(key, max(int(total_bytes), 1))
+
+    def flush(a: int, b: int) -> None:
+        with torch.cuda.stream(stream):
+            raw[a:b].copy_(staged[a:b], non_blocking=True)
+
+    stage_payloads(items, staged.data_ptr(), total_bytes, flush, limit, check)

@@ -44,11 +44,18 @@ stats = {}
 layers = encode_updates_dict(upd, comp, stats=stats)
 from omnifed_amd import hostio  # noqa: E402
 res = {"config": cfg, "elements": N, "tensors": len(named), "wire": stats, "copy_threads": hostio.workers(),
-       "agg_accumulate_layers_ms": None,
+       "agg_accumulate_layers_ms": None, "by_copy_threads": {},
        "encode_updates_dict_ms": tm(lambda: encode_updates_dict(upd, comp)) * 1e3,
        "decode_updates_dict_gpu_ms": tm(lambda: decode_updates_dict(layers, device=dev)) * 1e3,
        "decode_updates_into_ms": tm(lambda: decode_updates_into(layers, targets)) * 1e3,
        "decode_updates_dict_cpu_ms": tm(lambda: decode_updates_dict(layers)) * 1e3}
+# the host copies on the calling thread vs worker threads (hostio.set_workers), same process
+for nthr in (0, 2, 4, 8):
+    hostio.set_workers(nthr)
+    res["by_copy_threads"][str(nthr)] = {
+        "encode_updates_dict_ms": round(tm(lambda: encode_updates_dict(upd, comp)) * 1e3, 2),
+        "decode_updates_dict_gpu_ms": round(tm(lambda: decode_updates_dict(layers, device=dev)) * 1e3, 2)}
+hostio.set_workers(None)
 # the PS uplink: one client's LayerStates decode-accumulated into the aggregator arena
 from omnifed_amd import codec  # noqa: E402
 from omnifed_amd.ps import DeviceAggregator  # noqa: E402
