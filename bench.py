@@ -103,6 +103,14 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def visible_cores() -> int:
+    """CPU cores this process may run on (its affinity mask), which the thread counts are drawn from."""
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        return os.cpu_count() or 1
+
+
 def stratified_sample(named, budget):
     """Every k-th tensor of the arena (a representative mix of shapes) up to ``budget`` elements."""
     sizes = [int(np.prod(s)) for _, s in named]
@@ -155,7 +163,8 @@ def cpu_baseline(torch, named, bits, budget=40_000_000):
     return {
         "value": round(per * tot / times[best] / 1e9, 4),
         "unit": "GB/s",
-        "cores": best,
+        "cores": visible_cores(),
+        "threads": best,
         "kind": "port",
         "cpu": cpu_model(),
         "sample": f"{len(picked)} of {len(sizes)} tensors (every {max(1, int(np.ceil(N / budget)))}th; {tot} of {N} "
@@ -191,7 +200,8 @@ def cpu_baseline_topk(torch, named, ratio, budget=12_000_000):
     torch.set_num_threads(all_threads)
     alg = 16 * tot + 24 * sum(ks)
     best = min(times, key=lambda k: times[k])
-    return {"value": round(alg / times[best] / 1e9, 4), "unit": "GB/s", "cores": best, "kind": "port",
+    return {"value": round(alg / times[best] / 1e9, 4), "unit": "GB/s", "cores": visible_cores(), "threads": best,
+            "kind": "port",
             "cpu": cpu_model(),
             "sample": f"{len(picked)} of {len(sizes)} tensors ({tot} fp32 elements), Top-K k={ratio:g} with error "
                       f"feedback + zero-fill decode, median of 5 after 1 warm-up",
@@ -336,13 +346,18 @@ def main():
         ratio = args.ratio
         ks = plan.topk_ks(ratio)
         K = sum(ks)
+        # a fresh gradient every step, as in training (4 resident arenas in rotation): error
+        # feedback on one repeated gradient makes every never-selected residual grow in lockstep
+        # (r = c x after c steps), a degenerate magnitude distribution no client produces
+        xs = [x] + [torch.randn(plan.arena_end, device=dev, generator=g) * 1e-3 for _ in range(3)]
         res = torch.zeros(plan.arena_end, dtype=torch.float32, device=dev)
         vals = torch.empty(K, dtype=torch.float32, device=dev)
         idx = torch.empty(K, dtype=torch.int64, device=dev)
         yt = torch.empty(plan.arena_end, dtype=torch.float32, device=dev)
 
         def t_enc(i):
-            plan.topk_encode(x, ratio, residual=res, residual_mode=1, values=vals, indices=idx, alpha=weight)
+            plan.topk_encode(xs[i % len(xs)], ratio, residual=res, residual_mode=1, values=vals, indices=idx,
+                             alpha=weight)
 
         def t_step(i):
             t_enc(i)
@@ -366,7 +381,7 @@ def main():
                              "kernel": "omf_topk_encode (all launches of one call, host sync included)",
                              "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(tenc, 4),
                              "decode_ms": round(tdec, 4)}}
-        del res, yt
+        del res, yt, xs
 
     extras = {}
     if not args.no_extras and world == 1 and qsgd is not None and args.config == "llama400m":

@@ -248,52 +248,80 @@ def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, dev
     return y[:numel].reshape(original_shape).to(out_dev)
 
 
-def _check_qsgd_layer(layer):
-    """global_grpc_compression.py:164-171."""
+# protobuf (upb) copies a bytes field on every read, so the payload checks take the payload the
+# caller already holds (``payload``); the batched decoders check the fields first and each
+# payload's size as they stage it, before anything is decoded.
+
+def _payload_nbytes(layer) -> int:
+    n = int(np.prod(tuple(layer.original_shape)))
+    if layer.compression_type == QSGD_PACKED_COMPRESSION_NAME:
+        return (n * layer.width + 7) // 8
+    return n * (layer.width // 8)
+
+
+def _check_qsgd_payload(layer, payload: bytes) -> None:
+    """The size check of global_grpc_compression.py:173 (np.frombuffer(...).reshape(shape)
+    raises ValueError on a mismatch) and the empty-payload check of :164-165."""
+    if not payload:
+        raise ValueError(f"QSGD layer {layer.layer_name!r} missing values_data")
+    if len(payload) != _payload_nbytes(layer):
+        kind = "packed QSGD" if layer.compression_type == QSGD_PACKED_COMPRESSION_NAME else "QSGD"
+        raise ValueError(f"cannot reshape {kind} payload of {len(payload)} bytes into {tuple(layer.original_shape)}")
+
+
+def _field_error(layer, msg: str):
+    """Raise the reference's first error (global_grpc_compression.py:164-171 checks values_data
+    before the other fields; reading it is a copy, so only on this error path)."""
     if not layer.values_data:
         raise ValueError(f"QSGD layer {layer.layer_name!r} missing values_data")
+    raise ValueError(msg)
+
+
+def _check_qsgd_fields(layer):
+    """global_grpc_compression.py:164-171 without the payload's size (see _check_qsgd_payload)."""
     if not layer.meta_tensor:
-        raise ValueError(f"QSGD layer {layer.layer_name!r} missing meta_tensor (norm)")
+        _field_error(layer, f"QSGD layer {layer.layer_name!r} missing meta_tensor (norm)")
     if layer.width not in _QSGD_NUMPY_DTYPES:
-        raise ValueError(f"QSGD layer {layer.layer_name!r} has unsupported width={layer.width}")
+        _field_error(layer, f"QSGD layer {layer.layer_name!r} has unsupported width={layer.width}")
     if layer.level <= 0:
-        raise ValueError(f"QSGD layer {layer.layer_name!r} has invalid level={layer.level}")
-    n = int(np.prod(tuple(layer.original_shape)))
-    if len(layer.values_data) != n * (layer.width // 8):
-        # np.frombuffer(...).reshape(shape) raises ValueError on a size mismatch (:173)
-        raise ValueError(f"cannot reshape QSGD payload of {len(layer.values_data)} bytes into {tuple(layer.original_shape)}")
+        _field_error(layer, f"QSGD layer {layer.layer_name!r} has invalid level={layer.level}")
 
 
-def _check_packed_layer(layer):
-    """The packed layer's fields, checked like _check_qsgd_layer checks the reference's."""
-    if not layer.values_data:
-        raise ValueError(f"QSGD layer {layer.layer_name!r} missing values_data")
+def _check_packed_fields(layer):
+    """The packed layer's fields, checked like _check_qsgd_fields checks the reference's."""
     if not layer.meta_tensor:
-        raise ValueError(f"QSGD layer {layer.layer_name!r} missing meta_tensor (norm)")
+        _field_error(layer, f"QSGD layer {layer.layer_name!r} missing meta_tensor (norm)")
     if layer.level <= 0:
-        raise ValueError(f"QSGD layer {layer.layer_name!r} has invalid level={layer.level}")
+        _field_error(layer, f"QSGD layer {layer.layer_name!r} has invalid level={layer.level}")
     if layer.width != codec.packed_bits(layer.level):
-        raise ValueError(f"QSGD layer {layer.layer_name!r} has unsupported width={layer.width}")
-    n = int(np.prod(tuple(layer.original_shape)))
-    if len(layer.values_data) != (n * layer.width + 7) // 8:
-        raise ValueError(f"cannot reshape packed QSGD payload of {len(layer.values_data)} bytes into "
-                         f"{tuple(layer.original_shape)}")
+        _field_error(layer, f"QSGD layer {layer.layer_name!r} has unsupported width={layer.width}")
+
+
+def _check_qsgd_layer(layer, payload: bytes):
+    _check_qsgd_fields(layer)
+    _check_qsgd_payload(layer, payload)
+
+
+def _check_packed_layer(layer, payload: bytes):
+    _check_packed_fields(layer)
+    _check_qsgd_payload(layer, payload)
 
 
 def _decode_qsgd_layer(layer, *, device=None) -> torch.Tensor:
     """global_grpc_compression.py:163-182, decoded on the GPU."""
     if layer.compression_type == QSGD_PACKED_COMPRESSION_NAME:
-        _check_packed_layer(layer)
+        _check_packed_layer(layer, layer.values_data)
         shape = tuple(layer.original_shape)
         out_dev = _out_device(None, device)
         if int(np.prod(shape)) == 0:
             return torch.zeros(shape, dtype=torch.float32, device=out_dev)
         y, plan = _decode_qsgd_batch([layer], _gpu_for(out_dev))
         return y[:plan.sizes[0]].reshape(shape).to(out_dev)
-    _check_qsgd_layer(layer)
+    payload = layer.values_data  # one copy out of the message
+    _check_qsgd_layer(layer, payload)
     shape = tuple(layer.original_shape)
     n = int(np.prod(shape))
-    q = np.frombuffer(layer.values_data, dtype=_QSGD_NUMPY_DTYPES[layer.width])
+    q = np.frombuffer(payload, dtype=_QSGD_NUMPY_DTYPES[layer.width])
     norm = float(np.frombuffer(layer.meta_tensor, dtype=np.float32).reshape(-1)[0])
     out_dev = _out_device(None, device)
     dev = _gpu_for(out_dev)
@@ -333,7 +361,10 @@ def wire_size(layers) -> Dict[str, int]:
     wire = payload = dense = 0
     for L in layers:
         wire += L.ByteSize()
-        payload += len(L.values_data) + len(L.indices_data) + 4 * len(L.param_update)
+        if L.compression_type in _QSGD_TYPES:  # from the metadata: reading values_data copies it
+            payload += _payload_nbytes(L)
+        else:
+            payload += len(L.values_data) + len(L.indices_data) + 4 * len(L.param_update)
         shape = tuple(L.original_shape) or tuple(L.param_shape)
         dense += 4 * int(np.prod(shape)) if shape else 0
     return {"wire_bytes": wire, "payload_bytes": payload, "dense_fp32_bytes": dense, "layers": len(layers)}
@@ -420,13 +451,13 @@ def _decode_qsgd_batch(layers, dev: torch.device):
         words = plan.packed_words(level)
         qd = torch.empty(words, dtype=torch.int32, device=dev)
         items = [(o * width // 8, (lambda L=L: L.values_data)) for L, o in zip(layers, plan.offsets)]
-        hostio.bytes_to_device(items, qd, 4 * words)
+        hostio.bytes_to_device(items, qd, 4 * words, check=lambda i, p: _check_qsgd_payload(layers[i], p))
         y = plan.qsgd_decode_packed(qd, level, nd)
     else:
         isz = width // 8
         qd = torch.empty(plan.arena_end, dtype=_QSGD_TORCH_DTYPES[width], device=dev)
         items = [(o * isz, (lambda L=L: L.values_data)) for L, o in zip(layers, plan.offsets)]
-        hostio.bytes_to_device(items, qd, isz * plan.arena_end)
+        hostio.bytes_to_device(items, qd, isz * plan.arena_end, check=lambda i, p: _check_qsgd_payload(layers[i], p))
         y = plan.qsgd_decode(qd, width, level, nd)
     # the staging buffer is reused by the next call: make sure this copy has been consumed
     torch.cuda.current_stream(dev).synchronize()
@@ -444,9 +475,9 @@ def _validate_layer(layer):
         if not layer.values_data or not layer.indices_data:
             raise ValueError(f"Compressed layer {layer.layer_name!r} missing values/indices")
     elif ct == QSGD_COMPRESSION_NAME:
-        _check_qsgd_layer(layer)
+        _check_qsgd_fields(layer)  # the payload's size: checked as it is staged (_decode_qsgd_batch)
     elif ct == QSGD_PACKED_COMPRESSION_NAME:
-        _check_packed_layer(layer)
+        _check_packed_fields(layer)
     else:
         raise ValueError(f"Unsupported compression_type={ct!r}")
 
