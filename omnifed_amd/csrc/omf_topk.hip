@@ -206,13 +206,68 @@ __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict
 __device__ __forceinline__ int64_t sample_stride(int64_t n) {
   return max((int64_t)kSStride, (n + kSMaxRuns - 1) / kSMaxRuns);
 }
+// Sampling is split over the tensor's runs: kSRunsPerBlock runs per block (a 4096-run tensor
+// is 8 blocks on 8 CUs instead of one CU doing all its loads and its 64 Ki contended LDS
+// histogram atomics), each block adding its LDS histogram's non-empty bins into the tensor's
+// global histogram gh (zero between calls: topk_sample_threshold clears it after reading).
+// smap: per block, (tensor, first run).  Block 0 also clears this call's status words.
+constexpr int kSRunsPerBlock = 512;
 template <int MODE>
-__global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __restrict__ x, const float* __restrict__ r,
-                                                              float alpha, const int64_t* __restrict__ tbegin,
-                                                              const int64_t* __restrict__ tsize,
+__global__ __launch_bounds__(1024) void topk_sample_runs(const float* __restrict__ x, const float* __restrict__ r,
+                                                         float alpha, const int64_t* __restrict__ tbegin,
+                                                         const int64_t* __restrict__ tsize,
+                                                         const uint32_t* __restrict__ smap, uint32_t* __restrict__ gh,
+                                                         uint32_t* __restrict__ status) {
+  constexpr int U = kSRunsPerBlock / 256;  // runs per lane group, all loads in flight at once
+  __shared__ uint32_t h[kSBins];
+  const int t = (int)smap[2 * blockIdx.x];
+  const int64_t r0 = smap[2 * blockIdx.x + 1];
+  if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = 0u;
+  for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
+  const int64_t base = tbegin[t], n = tsize[t];
+  const int64_t stride = sample_stride(n), nr = (n + stride - 1) / stride;
+  const int64_t r1 = min(r0 + (int64_t)kSRunsPerBlock, nr);
+  const uint32_t salt = (uint32_t)t * 0x9E3779B9u;
+  const int q = threadIdx.x & 3;  // float4 of the run
+  float4 xv[U], rv[U];
+  int64_t rel[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // every load issued unconditionally (no branch around a load:
+    // hipcc would wait for each one in turn); past-the-end runs clamped
+    const int64_t j = min(r0 + (threadIdx.x >> 2) + (int64_t)u * 256, r1 - 1);
+    const int64_t lo = j * stride;
+    const int64_t span = min(stride, n - lo);
+    const int64_t runs = max((int64_t)1, span / kSRun);
+    rel[u] = lo + kSRun * (int64_t)(hash32((uint32_t)lo ^ salt) % (uint32_t)runs) + 4 * q;
+    const int64_t e = base + min(rel[u], (n - 1) & ~(int64_t)3);  // 16-byte aligned, inside the arena
+    xv[u] = *reinterpret_cast<const float4*>(x + e);
+    rv[u] = MODE == 1 ? *reinterpret_cast<const float4*>(r + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();  // h cleared
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (r0 + (threadIdx.x >> 2) + (int64_t)u * 256 >= r1) continue;
+    const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+    const float rs[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (rel[u] + c < n) atomicAdd(&h[mag_key(tprime<MODE>(xs[c], rs[c], alpha)) >> kSShift], 1u);
+  }
+  __syncthreads();
+  uint32_t* g = gh + (size_t)t * kSBins;
+  for (int b = threadIdx.x; b < kSBins; b += 1024)
+    if (h[b]) atomicAdd(&g[b], h[b]);
+}
+
+// One 1024-thread block per tensor, after topk_sample_runs: the tensor's sample histogram (read
+// from gh, then cleared for the next call), the threshold bin — the bin whose suffix holds
+// k*S/n + 6 sqrt(k*S/n) + 32 of the S samples (0 = every element, for tensors too small to
+// sample) — the "sure" bin, and the fine-bin map.
+__global__ __launch_bounds__(1024) void topk_sample_threshold(const int64_t* __restrict__ tsize,
                                                               const int64_t* __restrict__ kk,
                                                               const uint32_t* __restrict__ tfirst,
                                                               const uint32_t* __restrict__ tlast,
+                                                              uint32_t* __restrict__ gh,
                                                               uint32_t* __restrict__ tbin,
                                                               uint32_t* __restrict__ hist,
                                                               uint32_t* __restrict__ item_cnt,
@@ -221,43 +276,23 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const float* __res
                                                               uint32_t* __restrict__ fcount,
                                                               uint32_t* __restrict__ fhist) {
   constexpr int PER = kSBins / 1024;
-  constexpr int U = 8;  // runs in flight per lane group: a 4096-run tensor is two round trips
   __shared__ uint32_t h[kSBins];
   __shared__ uint32_t s_w[16];
   const int t = blockIdx.x;
-  for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
-  for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;  // this call's redo histogram
-  for (uint32_t i = tfirst[t] + threadIdx.x; i <= tlast[t]; i += 1024) item_cnt[i] = 0;  // the fused pass adds to them
-  __syncthreads();
-  const int64_t base = tbegin[t], n = tsize[t];
-  const int64_t stride = sample_stride(n), nr = (n + stride - 1) / stride;
-  const uint32_t salt = (uint32_t)t * 0x9E3779B9u;
-  const int q = threadIdx.x & 3;  // float4 of the run
-  for (int64_t j0 = threadIdx.x >> 2; j0 < nr; j0 += (int64_t)U * 256) {
-    float4 xv[U], rv[U];
-    int64_t rel[U];
+  const int64_t n = tsize[t];
+  uint32_t* g = gh + (size_t)t * kSBins;
+  {
+    uint4 v[PER / 4];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {  // every load of the batch issued unconditionally (no branch
-      // around a load: hipcc would wait for each one in turn); past-the-end runs clamped
-      const int64_t j = min(j0 + (int64_t)u * 256, nr - 1);
-      const int64_t lo = j * stride;
-      const int64_t span = min(stride, n - lo);
-      const int64_t runs = max((int64_t)1, span / kSRun);
-      rel[u] = lo + kSRun * (int64_t)(hash32((uint32_t)lo ^ salt) % (uint32_t)runs) + 4 * q;
-      const int64_t e = base + min(rel[u], (n - 1) & ~(int64_t)3);  // 16-byte aligned, inside the arena
-      xv[u] = *reinterpret_cast<const float4*>(x + e);
-      rv[u] = MODE == 1 ? *reinterpret_cast<const float4*>(r + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
+    for (int j = 0; j < PER / 4; ++j) v[j] = reinterpret_cast<const uint4*>(g + PER * threadIdx.x)[j];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (j0 + (int64_t)u * 256 >= nr) continue;
-      const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
-      const float rs[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-        if (rel[u] + c < n) atomicAdd(&h[mag_key(tprime<MODE>(xs[c], rs[c], alpha)) >> kSShift], 1u);
+    for (int j = 0; j < PER / 4; ++j) {
+      reinterpret_cast<uint4*>(g + PER * threadIdx.x)[j] = make_uint4(0u, 0u, 0u, 0u);  // clear for the next call
+      reinterpret_cast<uint4*>(h + PER * threadIdx.x)[j] = v[j];
     }
   }
+  for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;  // this call's redo histogram
+  for (uint32_t i = tfirst[t] + threadIdx.x; i <= tlast[t]; i += 1024) item_cnt[i] = 0;  // the fused pass adds to them
   __syncthreads();
   uint32_t c[PER], loc = 0;
 #pragma unroll
@@ -916,13 +951,46 @@ __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restric
 // (se_i = keys in higher bins), a bucket starts at its smallest se.  Flags the tensor for
 // the exact redo when it has fewer than k candidates, and the call for the fallback sort
 // when a kept fine bin holds more than kBucketHalf keys.  status[1] |= redo, [2] |= overflow.
+__device__ void topk_plan_tensor(const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
+                                 const uint32_t* __restrict__ fhist, const uint32_t* __restrict__ bbase,
+                                 int32_t* __restrict__ fbucket, uint32_t* __restrict__ bstart,
+                                 BucketRec* __restrict__ brec, uint32_t* __restrict__ bfill,
+                                 const int64_t* __restrict__ kb2, uint32_t* __restrict__ flag,
+                                 uint32_t* __restrict__ status, uint32_t* __restrict__ fse, int dbg);
 __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
                                                   const uint32_t* __restrict__ fhist,
                                                   const uint32_t* __restrict__ bbase, int32_t* __restrict__ fbucket,
                                                   uint32_t* __restrict__ bstart, BucketRec* __restrict__ brec,
                                                   uint32_t* __restrict__ bfill, const int64_t* __restrict__ kb2,
                                                   uint32_t* __restrict__ flag, uint32_t* __restrict__ status,
-                                                  uint32_t* __restrict__ fse, int dbg) {
+                                                  uint32_t* __restrict__ fse, int dbg, uint32_t* __restrict__ done,
+                                                  uint32_t* host, uint32_t seq) {
+  topk_plan_tensor(kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2, flag, status, fse, dbg);
+  // The last block to finish publishes the call's verdict straight into mapped, coherent host
+  // memory (no copy packet in the stream, so the bucket kernels behind this one start at once):
+  // the data words, then the sequence number with release semantics at system scope; the host
+  // spins on it.  Each block's status atomics come before its arrival (fence); the last one
+  // reads status with atomic RMWs (performed where the other blocks' atomics were).
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    if (atomicAdd(done, 1u) == gridDim.x - 1) {
+      atomicExch(done, 0u);
+      const uint32_t s0 = atomicOr(&status[0], 0u), s1 = atomicOr(&status[1], 0u), s2 = atomicOr(&status[2], 0u);
+      __hip_atomic_store(&host[0], s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&host[1], s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&host[2], s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
+__device__ void topk_plan_tensor(const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
+                                 const uint32_t* __restrict__ fhist, const uint32_t* __restrict__ bbase,
+                                 int32_t* __restrict__ fbucket, uint32_t* __restrict__ bstart,
+                                 BucketRec* __restrict__ brec, uint32_t* __restrict__ bfill,
+                                 const int64_t* __restrict__ kb2, uint32_t* __restrict__ flag,
+                                 uint32_t* __restrict__ status, uint32_t* __restrict__ fse, int dbg) {
   constexpr int PER = kFineMax / 1024;
   __shared__ uint32_t s_bs[kPlanMaxBuckets];
   __shared__ uint32_t part[1024];
@@ -1219,21 +1287,6 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
   }
 }
 
-// The call's verdict (status[0..2]) straight into mapped, coherent host memory — no copy packet
-// in the stream, so the bucket kernels queued behind this one start at once: the data words,
-// then this call's sequence number with release semantics at system scope (the host spins on
-// it).  One wave; vector stores.
-__global__ __launch_bounds__(64) void topk_publish_status(const uint32_t* __restrict__ status, uint32_t* host,
-                                                          uint32_t seq) {
-  if (threadIdx.x == 0) {
-    const uint32_t s0 = status[0], s1 = status[1], s2 = status[2];
-    __hip_atomic_store(&host[0], s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&host[1], s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&host[2], s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
 template <bool GLOBAL>
 __global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict__ tp, float scale,
                                                         float* __restrict__ r, const uint64_t* __restrict__ sorted,
@@ -1490,7 +1543,7 @@ size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // OMF_TOPK_FALLBACK=1: always take the device-wide radix-sort path (tests of that path).
 // Per host thread and device: a 16-byte status buffer in mapped, coherent host memory that
-// topk_publish_status writes (never freed: a few bytes per thread that calls the encoder).
+// topk_plan's last block writes (never freed: a few bytes per thread that calls the encoder).
 struct HostSync {
   uint32_t* pinned = nullptr;  // host view
   uint32_t* dev = nullptr;     // device view of the same bytes
@@ -1648,6 +1701,70 @@ WsLayout layout_uncached(const omf_plan* p) {
   return L;
 }
 
+// Per (plan, ratio) constant tables of the encoder, plan-owned (omf_plan_access::topk_table),
+// made once: topk_setup's per-tensor k / offsets / item ranges / bucket and super-item bases,
+// the sampling blocks' (tensor, first run) map, the sample histograms gh (zeroed here once,
+// left zeroed by every call) and the plan kernel's arrival counter.
+struct SetupTable {
+  int64_t *kk, *koff, *kb2;
+  uint32_t *tfirst, *tlast, *bbase, *sbase, *smap, *gh, *done;
+  int32_t nsb;
+};
+
+constexpr uint64_t kSetupTag = 0x5E7A9B1C00000000ull;
+
+int setup_table(omf_plan* p, double ratio, hipStream_t st, uint32_t* status, SetupTable* out) {
+  const std::vector<int64_t>& sizes = omf_plan_access::sizes(p);
+  const int32_t nt = (int32_t)sizes.size();
+  std::vector<uint32_t> smap;
+  for (int32_t t = 0; t < nt; ++t) {  // sampling blocks: as sample_stride on the device
+    const int64_t n = sizes[t];
+    const int64_t stride = std::max<int64_t>(kSStride, (n + kSMaxRuns - 1) / kSMaxRuns);
+    const int64_t nr = (n + stride - 1) / stride;
+    for (int64_t r0 = 0; r0 < nr; r0 += kSRunsPerBlock) {
+      smap.push_back((uint32_t)t);
+      smap.push_back((uint32_t)r0);
+    }
+  }
+  size_t o = 0;
+  const size_t o_kk = o; o = align256(o + 8 * (size_t)nt);
+  const size_t o_koff = o; o = align256(o + 8 * ((size_t)nt + 1));
+  const size_t o_kb2 = o; o = align256(o + 8 * (size_t)nt);
+  const size_t o_tf = o; o = align256(o + 4 * (size_t)nt);
+  const size_t o_tl = o; o = align256(o + 4 * (size_t)nt);
+  const size_t o_bb = o; o = align256(o + 4 * ((size_t)nt + 1));
+  const size_t o_sb = o; o = align256(o + 4 * ((size_t)nt + 1));
+  const size_t o_sm = o; o = align256(o + 4 * smap.size());
+  const size_t o_done = o; o = align256(o + 16);
+  const size_t o_gh = o; o = align256(o + 4 * (size_t)nt * kSBins);
+  bool fresh = false;
+  uint64_t* host = nullptr;
+  uint64_t key;
+  std::memcpy(&key, &ratio, 8);
+  uint8_t* d = static_cast<uint8_t*>(omf_plan_access::topk_table(p, key ^ kSetupTag, o, &fresh, &host));
+  if (!d) return fail(OMF_ENOMEM, "omf_topk_encode: table allocation failed");
+  out->kk = reinterpret_cast<int64_t*>(d + o_kk);
+  out->koff = reinterpret_cast<int64_t*>(d + o_koff);
+  out->kb2 = reinterpret_cast<int64_t*>(d + o_kb2);
+  out->tfirst = reinterpret_cast<uint32_t*>(d + o_tf);
+  out->tlast = reinterpret_cast<uint32_t*>(d + o_tl);
+  out->bbase = reinterpret_cast<uint32_t*>(d + o_bb);
+  out->sbase = reinterpret_cast<uint32_t*>(d + o_sb);
+  out->smap = reinterpret_cast<uint32_t*>(d + o_sm);
+  out->done = reinterpret_cast<uint32_t*>(d + o_done);
+  out->gh = reinterpret_cast<uint32_t*>(d + o_gh);
+  out->nsb = (int32_t)(smap.size() / 2);
+  if (fresh) {
+    OMF_HIP(hipMemsetAsync(out->done, 0, o - o_done, st));  // the arrival counter and gh
+    OMF_HIP(hipMemcpyAsync(out->smap, smap.data(), 4 * smap.size(), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(topk_setup, dim3(1), dim3(kThreads), 0, st, omf_plan_access::d_sizes(p), nt, ratio, out->kk,
+                       out->koff, out->tfirst, out->tlast, out->bbase, out->kb2, out->sbase, status, 0u);
+    OMF_HIP(hipGetLastError());
+    OMF_HIP(hipStreamSynchronize(st));  // once per (plan, ratio): the host copy of smap is freed on return
+  }
+  return OMF_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1738,18 +1855,25 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   HostSync* hsync = host_sync(omf_plan_access::device(plan));
   if (!hsync) return fail(OMF_EHIP, "omf_topk_encode: pinned status buffer");
   const uint32_t seq = ++hsync->seq == 0 ? ++hsync->seq : hsync->seq;
-  hipLaunchKernelGGL(topk_setup, dim3(1), blk, 0, st, d_sizes, nt, ratio, kk, koff, tfirst, tlast, bbase, kb2, sbase, status,
-                     seq);
+  // the per-(plan, ratio) constant tables: made by topk_setup on the first call at this ratio
+  SetupTable tb;
+  if (int r = setup_table(plan, ratio, st, status, &tb)) return r;
+  kk = tb.kk; koff = tb.koff; tfirst = tb.tfirst; tlast = tb.tlast; bbase = tb.bbase; kb2 = tb.kb2; sbase = tb.sbase;
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
     const dim3 sgrid((unsigned)nt), sblk(1024), fgrid((unsigned)(n_items * kSubsPerItem));
+    const dim3 rgrid((unsigned)tb.nsb);
+    if (residual_mode == 1)
+      hipLaunchKernelGGL((topk_sample_runs<1>), rgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes,
+                         (const uint32_t*)tb.smap, tb.gh, status);
+    else
+      hipLaunchKernelGGL((topk_sample_runs<0>), rgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes,
+                         (const uint32_t*)tb.smap, tb.gh, status);
+    hipLaunchKernelGGL(topk_sample_threshold, sgrid, sblk, 0, st, d_sizes, kk, tfirst, tlast, tb.gh, tbin, hist, item_cnt,
+                       thi, fmap, tlo, fcount, fhist);
     if (residual_mode == 1) {
-      hipLaunchKernelGGL((topk_sample_threshold<1>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
-                         tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
       hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt, item_cnt, cand);
     } else {
-      hipLaunchKernelGGL((topk_sample_threshold<0>), sgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes, kk,
-                         tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
       if (residual_mode == 2)
         hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi,
                            sub_cnt, item_cnt, cand);
@@ -1761,13 +1885,12 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     const dim3 supgrid((unsigned)nsup), supblk(1024);
     hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast, fmap,
                        tlo, fcount, fhist);
+    // the plan's last block publishes the verdict to mapped host memory; the bucket kernels are
+    // enqueued before the host waits for it (they do nothing when the verdict is a fallback),
+    // so the GPU does not idle while the host reads it
     hipLaunchKernelGGL(topk_plan, sgrid, sblk, 0, st, kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2,
-                       flag, status, fse, dbg_bits());
+                       flag, status, fse, dbg_bits(), tb.done, hsync->dev, seq);
     OMF_HIP(hipGetLastError());
-    // The plan's verdict goes straight to mapped host memory (a one-wave kernel, no copy
-    // packet); the bucket kernels are enqueued before the host waits for it (they do nothing
-    // when the verdict is a fallback), so the GPU does not idle while the host reads it.
-    hipLaunchKernelGGL(topk_publish_status, dim3(1), dim3(64), 0, st, (const uint32_t*)status, hsync->dev, seq);
     const bool forced = force_fallback();
     if (!forced) {
       hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast,
