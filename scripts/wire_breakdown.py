@@ -63,4 +63,10 @@ res["stage_payloads_only_ms"] = tm(lambda: hostio.stage_payloads(items, staged.d
                                                                  lambda a, b: None))
 res["bytes_to_device_ms"] = tm(lambda: hostio.bytes_to_device(items, dst, plan.arena_end, key="probe3"))
 res["decode_updates_dict_gpu_ms"] = tm(lambda: decode_updates_dict(layers, device=dev))
+# the same with the process's freed memory retained (hostio.retain_host_memory, opt-in)
+res["retain_host_memory"] = hostio.retain_host_memory()
+res["retained_layerstate_build_only_ms"] = tm(lambda: [qsgd_layer_from_payload(n, s, p, 1.0, 8, 16)
+                                                       for (n, s), p in zip(named, payloads)])
+res["retained_encode_updates_dict_ms"] = tm(lambda: encode_updates_dict(upd, comp))
+res["retained_decode_updates_dict_gpu_ms"] = tm(lambda: decode_updates_dict(layers, device=dev))
 print(json.dumps(res), flush=True)
