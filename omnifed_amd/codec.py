@@ -69,7 +69,7 @@ def _need(t: torch.Tensor, name: str, dtype, device, numel: int, align: int):
 
 
 # encoder strategies by omf_plan_set_encode_strategy code (include/omf_codec.h)
-STRATEGIES = ("resident", "ordered", "ring", "bracket")
+STRATEGIES = ("resident", "ordered", "ring", "bracket", "grid")
 
 
 class Plan:
@@ -168,8 +168,9 @@ class Plan:
         check(lib().omf_plan_set_resident_capacity(self._h, int(cap), int(wait_us)), "omf_plan_set_resident_capacity")
 
     def set_encode_strategy(self, strategy: str) -> None:
-        """'bracket' (bracketed single-read encoder), 'ring' (single-read ring encoder),
-        'ordered' (two-pass everywhere) or 'resident' (register-resident small tensors + two-pass)."""
+        """'grid' (one-launch encoder of small arenas: registers + one grid-wide barrier), 'bracket'
+        (bracketed single-read encoder), 'ring' (single-read ring encoder), 'ordered' (two-pass
+        everywhere) or 'resident' (register-resident small tensors + two-pass)."""
         code = STRATEGIES.index(strategy)
         check(lib().omf_plan_set_encode_strategy(self._h, code), "omf_plan_set_encode_strategy")
         self.strategy = strategy
@@ -178,7 +179,8 @@ class Plan:
     def encoder_kernel(self) -> str:
         """Name of the kernel one encode launch runs (profiling / roofline bookkeeping)."""
         # the bracketed encoder is three launches (qsgd_spec_bracket, _quant, _finish): "qsgd_spec_all"
-        return {"ring": "qsgd_encode_pc", "bracket": "qsgd_spec_all"}.get(self.strategy, "qsgd_encode_ordered")
+        return {"ring": "qsgd_encode_pc", "bracket": "qsgd_spec_all", "grid": "qsgd_encode_grid"}.get(
+            self.strategy, "qsgd_encode_ordered")
 
     def set_ring(self, cfg: int = -1, big_mode: int = -1, gap: int = -2, hold_max: int = -1) -> None:
         """Tuning / test hook of the ring encoder: see omf_plan_set_ring."""

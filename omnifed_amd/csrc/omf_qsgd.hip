@@ -888,6 +888,195 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
   }
 }
 
+// ---------------------------------------------------------------- grid encoder (strategy 4)
+// Small arenas (ResNet-18: 11 M elements in 2 976 blocks of 4 Ki): ONE launch of one 1024-thread
+// workgroup per CU; each quarter (256 threads) holds kGridNB 4 Ki blocks of x in registers
+// (its four waves publish their fp64 partial sums of squares, the bracketed encoder's layout),
+// every workgroup arrives at one grid-wide counter, and after it every tensor's norm is the same
+// deterministic fold of its partials in every workgroup (no second barrier) and the blocks are
+// quantised from registers: x is read once, with no per-tensor hand-off chain (the ring's) and
+// no sampled bracket (the bracketed encoder's four launches).  The hand-off is cdna_hip_
+// programming.md §6 Guideline 16, table row 1: 8-byte sc1 partial stores, every wave's
+// vmcnt(0), a workgroup barrier, one agent-scope add per workgroup; an sc1 poll of the counter,
+// a workgroup barrier, sc1 loads; one workgroup per CU.  The counter wait is bounded (20 ms
+// and a minimum number of polls); on expiry each workgroup recomputes the partials it needs
+// from x in the producers' exact order (same bits) and sets err bit 2.
+constexpr int kGridNB = 3;  // 4 Ki blocks per quarter-workgroup per launch
+
+struct GridArgs {
+  EncArgs e;                    // x, q, norm_out, alpha, fmt, levels, Philox key / offset, err, wait_ticks
+  uint64_t* partials;           // fp64 bits, 4 per 4 Ki block
+  unsigned long long* bar;      // grid arrival counter (monotonic over launches)
+  unsigned long long target;    // its value once every workgroup of this launch has arrived
+  int64_t nblocks;              // 4 Ki blocks of the plan (4 per flat item)
+  uint32_t dbg;                 // test hook (omf_plan_set_debug spec bit 32): never arrive
+};
+
+typedef uint32_t g32x4_t __attribute__((ext_vector_type(4)));
+// Range-checked buffer load of the float4 at byte offset voff of [base, base + bytes): dwords
+// past the range read 0, so a tensor's partial last block needs no branch around its loads.
+__device__ __forceinline__ float4 grid_ld4(const float* base, int64_t bytes, int voff) {
+  const __amdgpu_buffer_rsrc_t r =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), (short)0, (int)max(bytes, (int64_t)0), 0x00020000);
+  const g32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0);
+  return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+
+// Rows k = 0..3 of 4 Ki block [b, end) at quarter-thread lt: x * alpha (value format applied).
+__device__ __forceinline__ void grid_load_block(const EncArgs& e, int64_t b, int64_t end, int lt, float4 (&v)[4]) {
+  const float* base = e.x + b;
+  const int64_t bytes = 4 * (end - b);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = grid_ld4(base, bytes, 16 * (k * kThreads + lt));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (e.alpha != 1.0f) {
+      v[k] = make_float4(__fmul_rn(v[k].x, e.alpha), __fmul_rn(v[k].y, e.alpha), __fmul_rn(v[k].z, e.alpha),
+                         __fmul_rn(v[k].w, e.alpha));
+      if (e.fmt) v[k] = round_fmt4(v[k], e.fmt);
+    }
+  }
+}
+
+// The block's wave partial of quarter-thread lt's wave: the fp32 fma chain over its 16 values,
+// then the fp64 wave butterfly (identical in the producer and in the recovery).
+__device__ __forceinline__ double grid_partial(const float4 (&v)[4]) {
+  float acc = 0.0f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc = sq4(v[k], acc);
+  return wave_sum_f64((double)acc);
+}
+
+// Tensor t's norm by ONE wave: lane l sums partials l, l + 64, ... in order (fp64), then the
+// butterfly — the same bits in every workgroup.  recover: the partials are recomputed from x.
+__device__ float grid_fold(const GridArgs& a, const Item* __restrict__ items, uint32_t p0, uint32_t pn, bool recover) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  if (!recover) {
+    constexpr int U = 8;
+    for (uint32_t j0 = 0; j0 < pn; j0 += 64 * U) {
+      double d[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const uint32_t j = j0 + 64 * u + lane;
+        d[u] = j < pn ? __longlong_as_double((long long)ld_agent(&a.partials[p0 + j])) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (j0 + 64 * u + lane < pn) s += d[u];
+    }
+  } else {  // each partial as its wave made it: quarter wave wq of block p / 4
+    for (uint32_t j = 0; j < pn; ++j) {
+      const int64_t vb = (int64_t)(p0 + j) >> 2;
+      const int wq = (int)((p0 + j) & 3);
+      const Item it = items[vb >> 2];
+      const int64_t b = it.begin + (vb & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
+      float4 v[4];
+      grid_load_block(a.e, b, end, 64 * wq + lane, v);
+      const double p = grid_partial(v);
+      if ((j & 63) == (uint32_t)lane) s += p;
+    }
+  }
+  return finish_norm(wave_sum_f64(s), a.e.fmt);
+}
+
+template <int WIDTH>
+__global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item* __restrict__ items,
+                                                         const int64_t* __restrict__ begins,
+                                                         const uint32_t* __restrict__ pbeg,
+                                                         const uint32_t* __restrict__ pcnt) {
+  __shared__ float s_norm[kGridNB];
+  __shared__ uint32_t s_ok;
+  const EncArgs& e = a.e;
+  const int lt = threadIdx.x & 255, qv = threadIdx.x >> 8, lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6, wq = wave & 3;
+  const int64_t W = gridDim.x;
+  float4 v[kGridNB][4];
+  int64_t bb[kGridNB], be[kGridNB];
+  int32_t tt[kGridNB];
+  // phase 1: the blocks' x into registers, their wave partials published
+#pragma unroll
+  for (int i = 0; i < kGridNB; ++i) {
+    const int64_t item = (int64_t)i * W + blockIdx.x;
+    const bool live = 4 * item < a.nblocks;
+    const Item it = items[live ? item : 0];
+    bb[i] = it.begin + qv * kSpecBlk;
+    be[i] = live ? min(bb[i] + kSpecBlk, it.end) : bb[i];  // empty range: loads read 0
+    tt[i] = live ? it.tensor : -1;
+    grid_load_block(e, bb[i], be[i], lt, v[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < kGridNB; ++i) {
+    const double p = grid_partial(v[i]);
+    const int64_t vb = 4 * ((int64_t)i * W + blockIdx.x) + qv;
+    if (tt[i] >= 0 && lane == 0) st_agent(&a.partials[4 * vb + wq], (uint64_t)__double_as_longlong(p));
+  }
+  drain_vmem();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (!(a.dbg & 32u)) __hip_atomic_fetch_add(a.bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // bounded wait: wall clock AND a minimum number of polls (a queue context switch advances
+    // the clock while the wave is saved)
+    uint32_t ok = 1;
+    if (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.target) {
+      const uint64_t t0 = wall_clock64(), min_polls = e.wait_ticks >> 10;
+      uint64_t polls = 0;
+      for (int k = 0;; k = min(k + 1, 4)) {
+        if (k < 2) __builtin_amdgcn_s_sleep(2);
+        else __builtin_amdgcn_s_sleep(16);
+        if (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= a.target) break;
+        if (++polls > min_polls && wall_clock64() - t0 > e.wait_ticks) {
+          ok = 0;
+          __hip_atomic_fetch_or(e.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+      }
+    }
+    s_ok = ok;
+  }
+  __syncthreads();
+  // phase 2: wave i folds the norm of iteration i's tensor (the quarters of one item share it)
+  if (wave < kGridNB && tt[wave] >= 0) {
+    const int32_t t = tt[wave];
+    const uint32_t p0 = pbeg[t];
+    const float norm = grid_fold(a, items, p0, pcnt[t], s_ok == 0u);
+    if (lane == 0) {
+      s_norm[wave] = norm;
+      if (4 * 4 * ((int64_t)wave * W + blockIdx.x) == (int64_t)p0) e.norm_out[t] = norm;  // the tensor's first item
+    }
+  }
+  __syncthreads();
+  // phase 3: levels from registers
+#pragma unroll
+  for (int i = 0; i < kGridNB; ++i) {
+    if (tt[i] < 0 || bb[i] >= be[i]) continue;
+    const float norm = s_norm[i];
+    const Divisor dv(norm, e.fmt);
+    float4 uu[4];
+    {
+      const uint64_t G = (uint64_t)((bb[i] - begins[tt[i]]) >> 12) * (uint64_t)kThreads + (uint64_t)lt;
+      uint32_t w[12];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const uint64_t ctr = 3 * G + c;
+        const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)tt[i], e.offset),
+                                      e.seed_lo, e.seed_hi);
+        w[4 * c] = r.x; w[4 * c + 1] = r.y; w[4 * c + 2] = r.z; w[4 * c + 3] = r.w;
+      }
+#pragma unroll
+      for (int sl = 0; sl < 4; ++sl) uu[sl] = u24x4(w[3 * sl], w[3 * sl + 1], w[3 * sl + 2]);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int64_t el = bb[i] + 4 * ((int64_t)k * kThreads + lt);
+      if (el >= be[i]) continue;
+      int32_t qq[4];
+      qsgd_quad<false>(v[i][k], uu[k], dv, e.levels, !(norm != 0.0f), qq);
+      store_quad<WIDTH>(e, el, be[i], qq);
+    }
+  }
+}
+
 // Decode one sub-chunk [b, end): y = fl32(fl32(norm * q) / L) (optionally acc += y).
 template <int WIDTH, bool ACC, bool POW2, bool FULL, int V = kV>
 __device__ __forceinline__ void decode_sub(const DecArgs& a, int64_t b, int64_t end, float norm) {
@@ -1138,6 +1327,12 @@ struct omf_plan {
   uint32_t* d_dec_binfo = nullptr;
   uint32_t* d_spec_flags = nullptr;
   uint32_t* d_spec_status = nullptr;
+  // grid encoder (strategy 4): one workgroup per CU, kGridNB 4 Ki blocks per quarter
+  int32_t grid_wgs = 0;             // workgroups of a launch (CUs; 0 = unavailable)
+  uint32_t* d_grid_pbeg = nullptr;  // per tensor: first wave partial (16 per flat item)
+  uint32_t* d_grid_pcnt = nullptr;  // per tensor: wave partials
+  unsigned long long* d_grid_bar = nullptr;  // arrival counter (zeroed at upload)
+  uint64_t grid_launches = 0;
   // Top-K tiled decode: per-ratio constant tables (omf_topk.hip), allocated on first use, with
   // one host word each (the table's size facts)
   struct TopkTable {
@@ -1388,6 +1583,7 @@ static int upload_plan(omf_plan* p) {
   // per flat item).
   std::vector<SpecBrItem> br_items;
   std::vector<SpecFoldItem> fold_items;
+  std::vector<uint32_t> gpbeg((size_t)p->nt), gpcnt((size_t)p->nt);
   int32_t seg_base = 0;
   for (int32_t t = 0; t < p->nt; ++t) {
     const int64_t n = p->sizes[t], b = p->offsets[t];
@@ -1397,6 +1593,8 @@ static int upload_plan(omf_plan* p) {
       flat.push_back(Item{cb, std::min(b + n, cb + kSub), t, kQuant, (int32_t)c, 0});
     }
     const int64_t p_end = (int64_t)kWaves * 4 * (int64_t)flat.size();
+    gpbeg[(size_t)t] = (uint32_t)p_begin;
+    gpcnt[(size_t)t] = (uint32_t)(p_end - p_begin);
     const int64_t R = std::max<int64_t>(1, std::min<int64_t>(kSpecRuns, n / (2 * kSpecRun)));
     br_items.push_back(SpecBrItem{b, n, n / R, (int32_t)R, (int32_t)(n % R), t});
     const int32_t nsegs = (int32_t)((p_end - p_begin + kSpecSeg - 1) / kSpecSeg);
@@ -1457,6 +1655,9 @@ static int upload_plan(omf_plan* p) {
   const size_t o_sp_recs = o; o = round16(o + 32 * (size_t)kWaves * kSpecPerWave * (size_t)p->n_spec_blocks);
   const size_t o_sp_flags = o; o = round16(o + 4 * (size_t)p->nt);
   const size_t o_sp_status = o; o = round16(o + 4 * (size_t)p->nt);
+  const size_t o_g_pbeg = o; o = round16(o + 4 * (size_t)p->nt);
+  const size_t o_g_pcnt = o; o = round16(o + 4 * (size_t)p->nt);
+  const size_t o_g_bar = o; o = round16(o + 16);
   DeviceGuard g(p->device);
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   if (p->d_block) {
@@ -1493,6 +1694,13 @@ static int upload_plan(omf_plan* p) {
   p->d_spec_recs = reinterpret_cast<float4*>(base + o_sp_recs);
   p->d_spec_flags = reinterpret_cast<uint32_t*>(base + o_sp_flags);
   p->d_spec_status = reinterpret_cast<uint32_t*>(base + o_sp_status);
+  p->d_grid_pbeg = reinterpret_cast<uint32_t*>(base + o_g_pbeg);
+  p->d_grid_pcnt = reinterpret_cast<uint32_t*>(base + o_g_pcnt);
+  p->d_grid_bar = reinterpret_cast<unsigned long long*>(base + o_g_bar);
+  OMF_HIP(hipMemcpy(p->d_grid_pbeg, gpbeg.data(), 4 * gpbeg.size(), hipMemcpyHostToDevice));
+  OMF_HIP(hipMemcpy(p->d_grid_pcnt, gpcnt.data(), 4 * gpcnt.size(), hipMemcpyHostToDevice));
+  OMF_HIP(hipMemset(p->d_grid_bar, 0, 16));
+  p->grid_launches = 0;
   OMF_HIP(hipMemcpy(p->d_spec_br_items, br_items.data(), sizeof(SpecBrItem) * br_items.size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_spec_fold_items, fold_items.data(), sizeof(SpecFoldItem) * fold_items.size(),
                     hipMemcpyHostToDevice));
@@ -1586,7 +1794,13 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     // (Llama-400M 0.386 ms against the two-pass 0.59 and the ring 0.63; Llama-150M 0.25 against
     // 0.35), the ring below (ResNet-18: 0.032 ms against 0.08 for the bracket's four launches).
     p->strategy = p->arena_end >= ((int64_t)1 << 25) ? 3 : 2;
-    if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 3));
+    if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 4));
+    {  // grid encoder: one 1024-thread workgroup per CU must fit
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)qsgd_encode_grid<1>, 1024, 0) == hipSuccess &&
+          nb >= 1)
+        p->grid_wgs = prop.multiProcessorCount;
+    }
     p->ring_grid = omf::ring::grid_size(p->ring_cfg, device);
     if (p->ring_grid <= 0) {
       delete p;
@@ -1615,6 +1829,7 @@ int omf_plan_destroy(omf_plan* plan) {
 int64_t omf_plan_encode_items(const omf_plan* plan) {
   if (!plan) return -1;
   if (plan->strategy == 3) return plan->n_spec_blocks;
+  if (plan->strategy == 4) return plan->grid_wgs;
   return plan->strategy == 2 ? plan->n_ring : plan->n_enc[plan->strategy];
 }
 
@@ -1622,8 +1837,9 @@ int32_t omf_plan_encode_strategy(const omf_plan* plan) { return plan ? plan->str
 
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
-  if (strategy < 0 || strategy > 3)
-    return fail(OMF_EINVAL, "strategy must be 0 (resident), 1 (two-pass), 2 (single-read ring) or 3 (bracketed single-read)");
+  if (strategy < 0 || strategy > 4)
+    return fail(OMF_EINVAL, "strategy must be 0 (resident), 1 (two-pass), 2 (single-read ring), 3 (bracketed "
+                            "single-read) or 4 (grid)");
   plan->strategy = strategy;
   return OMF_OK;
 }
@@ -1680,7 +1896,7 @@ int omf_plan_set_resident_capacity(omf_plan* plan, int64_t cap, int64_t wait_us)
 int omf_plan_set_debug(omf_plan* plan, uint32_t ring_dbg, uint32_t spec_dbg, int64_t lds_wait_us) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
   if (lds_wait_us < 0) return fail(OMF_EINVAL, "lds_wait_us must be >= 0");
-  if ((ring_dbg & ~15u) || (spec_dbg & ~31u)) return fail(OMF_EINVAL, "omf_plan_set_debug: unknown switch bits");
+  if ((ring_dbg & ~15u) || (spec_dbg & ~63u)) return fail(OMF_EINVAL, "omf_plan_set_debug: unknown switch bits");
   plan->ring_dbg = ring_dbg;
   plan->spec_skip = spec_dbg;
   plan->lds_wait_ticks = lds_wait_us > 0 ? (uint64_t)lds_wait_us * 100ull : kWaitTicks;
@@ -1795,6 +2011,30 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }
+  // Grid encoder (strategy 4): on-device draws, any value format and width, arenas of at most
+  // grid_wgs x 4 x kGridNB blocks of 4 Ki (larger ones, caller uniforms and the fused PS step
+  // take the ring).  One launch.
+  if (p->strategy == 4 && !norm_only && !u && divisor == 0.0f && p->grid_wgs > 0 &&
+      p->n_spec_blocks <= (int64_t)p->grid_wgs * 4 * kGridNB) {
+    GridArgs ga;
+    a.items = p->d_flat;
+    ga.e = a;
+    ga.partials = p->d_spec_part;
+    ga.bar = p->d_grid_bar;
+    ++p->grid_launches;
+    ga.target = (unsigned long long)p->grid_launches * (unsigned long long)p->grid_wgs;
+    ga.nblocks = p->n_spec_blocks;
+    ga.dbg = p->spec_skip;
+    const dim3 gg((unsigned)p->grid_wgs), gblk(1024);
+    if (width == 1)
+      hipLaunchKernelGGL(qsgd_encode_grid<1>, gg, gblk, 0, st, ga, (const Item*)p->d_flat, (const int64_t*)p->d_begins,
+                         (const uint32_t*)p->d_grid_pbeg, (const uint32_t*)p->d_grid_pcnt);
+    else
+      hipLaunchKernelGGL(qsgd_encode_grid<4>, gg, gblk, 0, st, ga, (const Item*)p->d_flat, (const int64_t*)p->d_begins,
+                         (const uint32_t*)p->d_grid_pbeg, (const uint32_t*)p->d_grid_pcnt);
+    OMF_HIP(hipGetLastError());
+    return OMF_OK;
+  }
   // Bracketed single-read encoder: fp32 values with on-device draws (other formats and
   // caller uniforms take the two-pass encoder).  Four launches, no host interaction.
   if (p->strategy == 3 && !norm_only && !u && fmt == 0 && s >= kSpecMinBits && s <= kSpecMaxBits) {
@@ -1853,7 +2093,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     return OMF_OK;
   }
   // The ring also serves the fused PS step (divide + encode in one launch) under any strategy.
-  if ((p->strategy == 2 || divisor != 0.0f) && !norm_only) {
+  if ((p->strategy == 2 || p->strategy == 4 || divisor != 0.0f) && !norm_only) {
     omf::ring::Args r;
     r.x = x; r.u = u; r.q = q; r.norm_out = norm_out;
     r.items = p->d_ring; r.tinfo = p->d_ring_t; r.gran = p->d_ring_gran;

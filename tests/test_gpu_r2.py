@@ -82,7 +82,7 @@ def test_ring_debug_timing_modes_complete(gpu, dbg):
             assert torch.equal(nd, n_ref) if hold == 0 else torch.allclose(nd, n_ref, rtol=2e-6, atol=0)
 
 
-@pytest.mark.parametrize("strategy", ["ordered", "ring", "bracket"])
+@pytest.mark.parametrize("strategy", ["ordered", "ring", "bracket", "grid"])
 def test_encodes_on_two_streams_are_ordered(gpu, strategy):
     """One plan, launches alternating between two streams with no host synchronisation: each
     result equals the sequential one (the plan orders a launch after the previous stream's)."""
@@ -125,7 +125,7 @@ def test_int8_payload_stays_inside_its_buffer(gpu):
     with pytest.raises(ValueError):
         plan.qsgd_encode(x, 4, q_out=buf[:plan.arena_end], seed=3)
     prev = plan.strategy
-    for strategy in ("ring", "ordered"):
+    for strategy in ("ring", "ordered", "grid"):
         plan.set_encode_strategy(strategy)
         buf.fill_(0x5A)
         q, norms = plan.qsgd_encode(x, 4, q_out=buf[:plan.payload_elems(8)], seed=3)

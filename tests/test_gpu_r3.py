@@ -347,3 +347,69 @@ def test_llama400m_topk_encode_then_tiled_decode(gpu):
     y = plan.topk_decode_arena(vals, idx, 0.01, mode=0)
     torch.cuda.synchronize()
     assert torch.equal(y, _scatter_ref(plan, vals, idx, ks))
+
+
+# ---------------------------------------------------------------- grid encoder (strategy 4)
+
+def _oracle_check(plan, x, q, norms, s, seed, off, alpha=1.0, tensors=None):
+    xh, qh, nh = x.cpu().numpy(), q.cpu().numpy(), norms.cpu().numpy()
+    for t in (range(plan.nt) if tensors is None else tensors):
+        o, n = plan.offsets[t], plan.sizes[t]
+        xs = (xh[o:o + n] * np.float32(alpha)).astype(np.float32) if alpha != 1.0 else xh[o:o + n]
+        ref = float(np.sqrt(np.sum(xs.astype(np.float64) ** 2)))
+        assert abs(float(nh[t]) - ref) <= 2e-6 * ref, t
+        want = _oracle_q(xs, s, float(nh[t]), oracle.philox_uniforms(seed, off, t, n))
+        assert qh[o:o + n].tobytes() == want.tobytes(), t
+
+
+@pytest.mark.parametrize("cfg,s,alpha", [("resnet18", 3, 1.0), ("resnet18", 4, 7.0), ("resnet18", 8, 1.0),
+                                         ("mixed", 4, 3.0)])
+def test_grid_encoder_against_the_oracle(gpu, cfg, s, alpha):
+    """The one-launch grid encoder: every tensor's norm within 2e-6 of fp64 and its payload the
+    oracle's given that norm and the Philox draws (int8 and int32 payloads, weighting fused);
+    its norms equal the bracketed / ring encoders' up to their own fold order."""
+    if cfg == "mixed":
+        sizes = [1, 5, 63, 64, 4097, 16384, 16385, 70001, 1 << 20, 3, 250_000]
+    else:
+        sizes = [shapes.numel(sh) for _, sh in shapes.model_shapes(cfg)]
+    plan = codec.Plan(sizes, device=gpu)
+    plan.set_encode_strategy("grid")
+    assert plan.encoder_kernel == "qsgd_encode_grid"
+    g = torch.Generator(device=gpu).manual_seed(41)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    x[plan.offsets[-1]:plan.offsets[-1] + 7] = 0.0
+    seed, off = 12345, 9
+    q, norms = plan.qsgd_encode(x, s, alpha=alpha, seed=seed, offset=off)
+    assert plan.check() is True  # no recomputation: the grid was co-resident
+    _oracle_check(plan, x, q, norms, s, seed, off, alpha)
+    # decode round trip stays the decoder's
+    L = 2**s
+    y = plan.qsgd_decode(q, 8 if L <= 127 else 32, L, norms)
+    assert bool(torch.isfinite(y[:plan.arena_end]).all())
+
+
+def test_grid_encoder_barrier_timeout_recovers_exactly(gpu):
+    """Test hook: no workgroup arrives at the grid barrier, every wait expires, and each
+    workgroup recomputes the partials it needs from x in the producers' order — the same
+    norms and payload bit for bit, reported as a recomputation (check() returns False)."""
+    sizes = [shapes.numel(sh) for _, sh in shapes.model_shapes("resnet18")][:20]
+    plan = codec.Plan(sizes, device=gpu)
+    plan.set_encode_strategy("grid")
+    g = torch.Generator(device=gpu).manual_seed(42)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g)
+    q0, n0 = plan.qsgd_encode(x, 4, seed=3, offset=1)
+    assert plan.check() is True
+    q0, n0 = q0.clone(), n0.clone()
+    plan.set_debug(spec=32)
+    plan.set_resident_capacity(0, wait_us=100)
+    try:
+        q1, n1 = plan.qsgd_encode(x, 4, seed=3, offset=1)
+        assert plan.check() is False
+    finally:
+        plan.set_debug()
+        plan.set_resident_capacity(0, wait_us=0)
+    assert torch.equal(n0, n1)
+    for o, n in zip(plan.offsets, plan.sizes):
+        assert torch.equal(q0[o:o + n], q1[o:o + n])
+    q2, n2 = plan.qsgd_encode(x, 4, seed=3, offset=1)  # the counter still lines up afterwards
+    assert plan.check() is True and torch.equal(n2, n0)
