@@ -373,11 +373,12 @@ def main():
         tdec = event_ms(torch, st, lambda i: plan.topk_decode_arena(vals, idx, ratio, y=yt, mode=0), reps)
         enc_alg = 12 * N + 12 * K  # read x, read+write the residual, write values+indices
         ach = enc_alg / (tenc * 1e-3) / 1e9
+        t_traffic, t_tsrc = pmc_traffic("topk_encode_all", args.config, s)  # every launch of one encode call
         topk = {"metric": METRIC_TOPK, "value": round(world * alg_t * steps_t / dtt / 1e9, 2), "unit": "GB/s",
                 "ms_per_step": round(dtt / steps_t * 1e3, 4), "steps": steps_t, "ratio": ratio, "k_total": K,
                 "algorithmic_bytes_per_step_per_client": alg_t,
                 "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": t_traffic, "traffic_source": t_tsrc,
                              "kernel": "omf_topk_encode (all launches of one call, host sync included)",
                              "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(tenc, 4),
                              "decode_ms": round(tdec, 4)}}

@@ -26,12 +26,17 @@ def load(d, counter):
     return per
 
 
+TOPK_ENCODE = ("topk_sample_runs", "topk_sample_threshold", "topk_fused", "topk_fine_hist", "topk_plan",
+               "topk_bucket_scatter", "topk_bucket_sort")
+TOPK_DECODE = ("topk_dec_place", "topk_dec_tiles", "topk_dec_overflow")
+
+
 def short(name):
-    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_decode_flat", "qsgd_decode_arena",
-              "qsgd_quant_sub",
+    for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_encode_grid", "qsgd_decode_flat",
+              "qsgd_decode_arena", "qsgd_quant_sub",
               "qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_finish",
-              "topk_fused", "topk_prep_hist", "topk_collect", "topk_gather", "topk_scatter_arena"):
-        if k in name:
+              "topk_prep_hist", "topk_collect", "topk_gather", "topk_scatter_arena") + TOPK_ENCODE + TOPK_DECODE:
+        if k + "(" in name or k + "<" in name:
             return k
     return None
 
@@ -53,6 +58,11 @@ def main():
     if all(k in res for k in spec):  # the bracketed encoder: one launch of each per encode
         res["qsgd_spec_all"] = {kk: sum(res[k][kk] for k in spec) for kk in ("fetch_bytes_corrected", "write_bytes")}
         res["qsgd_spec_all"]["launches"] = res["qsgd_spec_quant"]["launches"]
+    # Top-K: every launch of one encode call (resp. one tiled decode call), summed
+    for agg, parts in (("topk_encode_all", TOPK_ENCODE), ("topk_decode_all", TOPK_DECODE)):
+        if all(k in res for k in parts):
+            res[agg] = {kk: sum(res[k][kk] for k in parts) for kk in ("fetch_bytes_corrected", "write_bytes")}
+            res[agg]["launches"] = res[parts[-1]]["launches"]
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from omnifed_amd.build import source_digest
     import datetime
