@@ -11,8 +11,13 @@
  *
  * Conventions
  *  - Every pointer argument is DEVICE memory owned by the caller unless noted.
- *    The library allocates only in omf_plan_create (its own workspace); the
- *    hot-path calls never allocate, copy host memory or synchronise.
+ *    The library allocates only in omf_plan_create (its own workspace) and, once per
+ *    (plan, Top-K ratio), a small constant table on the first Top-K call at that ratio
+ *    (synchronous, not on the hot path after that).  The hot-path calls never allocate or
+ *    copy host memory, and never synchronise — except omf_topk_encode, which waits once
+ *    per call for its plan kernel's verdict (a 16-byte word the GPU writes into mapped host
+ *    memory; the launches that follow it are already queued), and omf_plan_check /
+ *    omf_plan_spec_stats, which exist to synchronise.
  *  - `stream` is a hipStream_t (NULL = the legacy default stream).  Calls are
  *    asynchronous on that stream; results are ready when the stream is.
  *  - Return value: 0 (OMF_OK) or a negative OMF_E* code; the message for the
@@ -247,8 +252,10 @@ int omf_qsgd_decode_packed(omf_plan* plan, const uint32_t* packed, int32_t level
  * Order within a tensor: descending |t'|, ties by ascending index (torch.topk's
  * order for k*64 <= n on the reference CPU path; ties there are unspecified).
  * ws: caller workspace of omf_topk_workspace_bytes(plan, ratio) bytes.
- * Synchronises `stream` once (the candidate count sizes the device-wide sort), twice
- * when a sampled threshold has to be redone exactly for some tensor.
+ * Waits once for the plan kernel's verdict (mapped host memory, no stream synchronisation;
+ * the bucket kernels are queued before the wait); on the rare fallback verdict (a sampled
+ * threshold too high, or an over-full fine bin) it synchronises `stream` once or twice to size
+ * the device-wide sort.
  */
 int64_t omf_topk_k(int64_t numel, double ratio);
 size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio);
