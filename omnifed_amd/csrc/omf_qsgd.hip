@@ -1014,6 +1014,8 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
   drain_vmem();
   __syncthreads();
   if (threadIdx.x == 0) {
+    // (test hook dbg & 32: arrive only after the wait, so that every wait expires and the counter
+    // still advances by the grid size per launch)
     if (!(a.dbg & 32u)) __hip_atomic_fetch_add(a.bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // bounded wait: wall clock AND a minimum number of polls (a queue context switch advances
     // the clock while the wave is saved)
@@ -1032,6 +1034,7 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
         }
       }
     }
+    if (a.dbg & 32u) __hip_atomic_fetch_add(a.bar, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_ok = ok;
   }
   __syncthreads();
