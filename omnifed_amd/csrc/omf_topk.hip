@@ -7,9 +7,10 @@
 // alpha = 1 leaves x's bits unchanged.
 //
 // Passes (all tensors of a plan per launch; <= 256 tensors of <= 2^25 elements):
-//   1. topk_sample_threshold, one block per tensor: one aligned 16-element run of t' per
-//                       max(256, n/4096) elements (hashed position; a random 64-byte sector
-//                       costs the same as one element) into an LDS 8192-bin histogram of the top 13 bits of
+//   1. topk_sample_runs (512 runs per block) + topk_sample_threshold (one block per tensor):
+//                       one aligned 16-element run of t' per max(256, n/16384) elements
+//                       (hashed position; a random 64-byte sector costs the same as one
+//                       element) into an 8192-bin histogram of the top 13 bits of
 //                       |t'| (exponent + 5 mantissa bits); the bin whose suffix holds
 //                       k*S/n + 6 sqrt(k*S/n) + 32 of the S samples is the threshold — below
 //                       the k-th magnitude with ~6 sigma of margin (tensors too small to
@@ -54,7 +55,7 @@ constexpr int kSBins = 1 << kSBits;
 constexpr int kSShift = 31 - kSBits;
 constexpr int kSRun = 16;       // a sample is a 64-byte run of 16 consecutive elements,
 constexpr int kSStride = 256;   // one run per >= 256 elements,
-constexpr int kSMaxRuns = 4096; // at most 4096 runs (64 Ki samples) per tensor
+constexpr int kSMaxRuns = 16384; // at most 16384 runs (256 Ki samples) per tensor (split over run blocks)
 constexpr int kV = 16;
 constexpr int64_t kSub = (int64_t)kV * kThreads * 4;
 // Composite candidate key: index << 39 | tensor << 31 | (2^31 - 1 - |t'|bits).  Candidates are
@@ -197,8 +198,7 @@ __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict
   }
 }
 
-// Passes 1+2, one 1024-thread block per tensor: R = ceil(n / stride) runs, stride =
-// max(256, n / 4096); run j covers 16 aligned elements at j*stride + 16 * (hash(.) % (span/16))
+// Passes 1+2: R = ceil(n / stride) runs, stride = max(256, n / 16384); run j covers 16 aligned elements at j*stride + 16 * (hash(.) % (span/16))
 // (a whole 64-byte sector: random sectors, not elements, are what the sample costs), so
 // S <= 16 R samples go into an LDS histogram of the top 13 bits of |t'|; then the bin whose
 // suffix holds k*S/n + 6 sqrt(k*S/n) + 32 samples (0 = every element, for tensors too small
