@@ -68,10 +68,13 @@ def main():
     import datetime
     import subprocess
 
-    try:
-        commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True).stdout.strip()
-    except OSError:
-        commit = ""
+    commit = os.environ.get("OMF_COMMIT", "")  # the GPU box's copy has no .git: pass it in
+    if not commit:
+        try:
+            commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True,
+                                    text=True).stdout.strip()
+        except OSError:
+            commit = ""
     j = {"config": cfg, "bits": bits, "source_sha": source_digest(), "commit": commit or None,
          "date": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%d"), "note": "FETCH_SIZE x2 (gfx950 wide-load correction) + WRITE_SIZE, KiB->B, "
          "average per launch; Infinity-Cache hits are counted as fetches",
