@@ -56,7 +56,8 @@ extern "C" {
 
 typedef struct omf_plan omf_plan;
 
-/* ABI version (major*100 + minor): 104. */
+/* ABI version (major*100 + minor). */
+#define OMF_ABI_VERSION 104
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */

@@ -75,6 +75,9 @@ class CodecError(RuntimeError):
     pass
 
 
+ABI_VERSION = 104  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+
+
 def lib() -> ctypes.CDLL:
     """Load (once) and return the HIP codec library; raise if it is absent."""
     global _lib
@@ -92,6 +95,9 @@ def lib() -> ctypes.CDLL:
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
+            if L.omf_abi_version() != ABI_VERSION:
+                raise CodecError(f"{path} has ABI {L.omf_abi_version()}, this package needs {ABI_VERSION} "
+                                 "(rebuild: `python -m omnifed_amd.build`)")
             _lib = L
     return _lib
 

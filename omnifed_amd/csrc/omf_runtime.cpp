@@ -26,7 +26,7 @@ int hip_fail(hipError_t e, const char* what) {
 
 extern "C" {
 
-int omf_abi_version(void) { return 104; }
+int omf_abi_version(void) { return OMF_ABI_VERSION; }
 
 const char* omf_last_error(void) { return omf::g_last_error.c_str(); }
 

@@ -23,7 +23,9 @@ def test_build_and_load():
     path = build()
     assert os.path.exists(path)
     L = _lib.lib()
-    assert L.omf_abi_version() == 104
+    assert L.omf_abi_version() == _lib.ABI_VERSION
+    # the header's define, the library and the Python binding agree
+    assert re.search(r"#define OMF_ABI_VERSION (\d+)", open(HEADER).read()).group(1) == str(_lib.ABI_VERSION)
     assert L.omf_last_error() == b""
 
 
