@@ -7,26 +7,24 @@
 // alpha = 1 leaves x's bits unchanged.
 //
 // Passes (all tensors of a plan per launch; <= 256 tensors of <= 2^25 elements):
-//   1. topk_sample_runs (512 runs per block) + topk_sample_threshold (one block per tensor):
-//                       one aligned 16-element run of t' per max(256, n/16384) elements
+//   1. topk_sample      one aligned 16-element run of t' per max(256, n/16384) elements
 //                       (hashed position; a random 64-byte sector costs the same as one
-//                       element) into an 8192-bin histogram of the top 13 bits of
-//                       |t'| (exponent + 5 mantissa bits); the bin whose suffix holds
-//                       k*S/n + 6 sqrt(k*S/n) + 32 of the S samples is the threshold — below
-//                       the k-th magnitude with ~6 sigma of margin (tensors too small to
-//                       sample keep every element).
-//   3. topk_fused       ONE streaming pass: read x (+ residual), write t' into the residual,
-//                       and append every |t'| at or above the threshold (~1.1-1.8 k) as a
-//                       64-bit key (index << 39 | tensor << 31 | (2^31-1 - |t'|bits)) into the
-//                       1 Ki-element sub-chunk's own region (one block scan per 1 Ki
-//                       elements, one float4 per thread; no contended atomics).
-//   4. topk_check       candidates per tensor from the item scan; a tensor whose sample put
-//                       the threshold too high (fewer than k) is redone exactly from t': its
-//                       1024-bin histogram, the bin of the k-th magnitude, a re-collection.
-//   5. one device-wide radix sort of the candidates (rocPRIM onesweep): tensor ascending,
-//      magnitude descending, index ascending (= torch's partial-sort order when k*64 <= n).
-//   6. topk_gather      first k keys of every tensor -> values / int64 indices; zero the
-//                       selected residual slots.
+//                       element), 512 runs per block, into an 8192-bin histogram of the top
+//                       13 bits of |t'| (exponent + 5 mantissa bits); the last block of each
+//                       tensor takes the bin whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of
+//                       the S samples as the threshold (below the k-th magnitude with ~6 sigma
+//                       of margin; tensors too small to sample keep every element), a "sure"
+//                       bin (above it with the same margin) and the fine-bin map.
+//   2. topk_fused       ONE streaming pass: read x (+ residual), write the residual, append
+//                       every |t'| at or above the threshold as index << 32 | bits(t') to the
+//                       1 Ki-element sub-chunk's own range (one block scan, no atomics).
+//   3. topk_fine_hist   exact fine-bin histogram of the candidates (LDS per super-item).
+//   4. topk_plan        per tensor: the fine bins above rank k -> buckets of <= 4096 keys with
+//                       known first ranks; the last block publishes the verdict to host memory.
+//   5. topk_bucket_scatter / topk_bucket_sort: keys into buckets, an LDS sort per bucket ->
+//                       values / int64 indices (torch's partial-sort order), residual fix-ups.
+//   6. fallback (a verdict flag, rare): exact redo of flagged tensors, one rocPRIM radix sort
+//                       of (index << 39 | tensor << 31 | 2^31-1 - |t'|bits), a gather.
 // Larger plans take the exact path (histogram of every t', collection, a segmented
 // descending sort of (|t'|bits << 32 | ~index) per tensor).
 // Decode is a scatter (mode 0 zero-fill, 1 overlay, 2 scatter-add).
@@ -55,7 +53,7 @@ constexpr int kSBins = 1 << kSBits;
 constexpr int kSShift = 31 - kSBits;
 constexpr int kSRun = 16;       // a sample is a 64-byte run of 16 consecutive elements,
 constexpr int kSStride = 256;   // one run per >= 256 elements,
-constexpr int kSMaxRuns = 16384; // at most 16384 runs (256 Ki samples) per tensor (split over run blocks)
+constexpr int kSMaxRuns = 16384; // default: at most 16 Ki runs (256 Ki samples) per tensor (OMF_TOPK_SAMPLE_RUNS)
 constexpr int kV = 16;
 constexpr int64_t kSub = (int64_t)kV * kThreads * 4;
 // Composite candidate key: index << 39 | tensor << 31 | (2^31 - 1 - |t'|bits).  Candidates are
@@ -198,102 +196,40 @@ __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict
   }
 }
 
-// Passes 1+2: R = ceil(n / stride) runs, stride = max(256, n / 16384); run j covers 16 aligned elements at j*stride + 16 * (hash(.) % (span/16))
+// Passes 1+2 (one launch, topk_sample): R = ceil(n / stride) runs, stride = max(256,
+// ceil(n / max_runs)); run j covers 16 aligned elements at j*stride + 16 * (hash(.) % (span/16))
 // (a whole 64-byte sector: random sectors, not elements, are what the sample costs), so
-// S <= 16 R samples go into an LDS histogram of the top 13 bits of |t'|; then the bin whose
+// S <= 16 R samples go into a histogram of the top 13 bits of |t'|; then the bin whose
 // suffix holds k*S/n + 6 sqrt(k*S/n) + 32 samples (0 = every element, for tensors too small
 // to sample).  Four lanes read one run (float4 each).
-__device__ __forceinline__ int64_t sample_stride(int64_t n) {
-  return max((int64_t)kSStride, (n + kSMaxRuns - 1) / kSMaxRuns);
+__device__ __forceinline__ int64_t sample_stride(int64_t n, int64_t max_runs) {
+  return max((int64_t)kSStride, (n + max_runs - 1) / max_runs);
 }
-// Sampling is split over the tensor's runs: kSRunsPerBlock runs per block (a 4096-run tensor
-// is 8 blocks on 8 CUs instead of one CU doing all its loads and its 64 Ki contended LDS
-// histogram atomics), each block adding its LDS histogram's non-empty bins into the tensor's
-// global histogram gh (zero between calls: topk_sample_threshold clears it after reading).
-// smap: per block, (tensor, first run).  Block 0 also clears this call's status words.
+// Sampling is split over the tensor's runs: kSRunsPerBlock runs per block (a 16 Ki-run tensor
+// is 32 blocks on 32 CUs instead of one CU doing all its loads and contended LDS histogram
+// atomics), each block adding its LDS histogram's non-empty bins into the tensor's global
+// histogram gh.  The LAST block of a tensor to arrive (a per-tensor counter, reset by that
+// block) reads and clears gh with atomic RMWs — performed where the other blocks' atomics
+// were — and derives the tensor's threshold, "sure" bin and fine-bin map
+// (sample_threshold_tensor), so no second launch and no tail of one-block-per-tensor work
+// after the last sample.  smap: per block, (tensor, first run).  Block 0 also clears this
+// call's status words.
 constexpr int kSRunsPerBlock = 512;
-template <int MODE>
-__global__ __launch_bounds__(1024) void topk_sample_runs(const float* __restrict__ x, const float* __restrict__ r,
-                                                         float alpha, const int64_t* __restrict__ tbegin,
-                                                         const int64_t* __restrict__ tsize,
-                                                         const uint32_t* __restrict__ smap, uint32_t* __restrict__ gh,
-                                                         uint32_t* __restrict__ status) {
-  constexpr int U = kSRunsPerBlock / 256;  // runs per lane group, all loads in flight at once
-  __shared__ uint32_t h[kSBins];
-  const int t = (int)smap[2 * blockIdx.x];
-  const int64_t r0 = smap[2 * blockIdx.x + 1];
-  if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = 0u;
-  for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
-  const int64_t base = tbegin[t], n = tsize[t];
-  const int64_t stride = sample_stride(n), nr = (n + stride - 1) / stride;
-  const int64_t r1 = min(r0 + (int64_t)kSRunsPerBlock, nr);
-  const uint32_t salt = (uint32_t)t * 0x9E3779B9u;
-  const int q = threadIdx.x & 3;  // float4 of the run
-  float4 xv[U], rv[U];
-  int64_t rel[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {  // every load issued unconditionally (no branch around a load:
-    // hipcc would wait for each one in turn); past-the-end runs clamped
-    const int64_t j = min(r0 + (threadIdx.x >> 2) + (int64_t)u * 256, r1 - 1);
-    const int64_t lo = j * stride;
-    const int64_t span = min(stride, n - lo);
-    const int64_t runs = max((int64_t)1, span / kSRun);
-    rel[u] = lo + kSRun * (int64_t)(hash32((uint32_t)lo ^ salt) % (uint32_t)runs) + 4 * q;
-    const int64_t e = base + min(rel[u], (n - 1) & ~(int64_t)3);  // 16-byte aligned, inside the arena
-    xv[u] = *reinterpret_cast<const float4*>(x + e);
-    rv[u] = MODE == 1 ? *reinterpret_cast<const float4*>(r + e) : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-  __syncthreads();  // h cleared
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    if (r0 + (threadIdx.x >> 2) + (int64_t)u * 256 >= r1) continue;
-    const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
-    const float rs[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
-#pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (rel[u] + c < n) atomicAdd(&h[mag_key(tprime<MODE>(xs[c], rs[c], alpha)) >> kSShift], 1u);
-  }
-  __syncthreads();
-  uint32_t* g = gh + (size_t)t * kSBins;
-  for (int b = threadIdx.x; b < kSBins; b += 1024)
-    if (h[b]) atomicAdd(&g[b], h[b]);
-}
 
-// One 1024-thread block per tensor, after topk_sample_runs: the tensor's sample histogram (read
-// from gh, then cleared for the next call), the threshold bin — the bin whose suffix holds
-// k*S/n + 6 sqrt(k*S/n) + 32 of the S samples (0 = every element, for tensors too small to
-// sample) — the "sure" bin, and the fine-bin map.
-__global__ __launch_bounds__(1024) void topk_sample_threshold(const int64_t* __restrict__ tsize,
-                                                              const int64_t* __restrict__ kk,
-                                                              const uint32_t* __restrict__ tfirst,
-                                                              const uint32_t* __restrict__ tlast,
-                                                              uint32_t* __restrict__ gh,
-                                                              uint32_t* __restrict__ tbin,
-                                                              uint32_t* __restrict__ hist,
-                                                              uint32_t* __restrict__ item_cnt,
-                                                              uint32_t* __restrict__ thi,
-                                                              uint32_t* __restrict__ fmap, uint32_t* __restrict__ tlo,
-                                                              uint32_t* __restrict__ fcount,
-                                                              uint32_t* __restrict__ fhist) {
+// The tensor's threshold from its sample histogram h (LDS, kSBins, loaded; 1024 threads):
+// the threshold bin — the bin whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of the S samples
+// (0 = every element, for tensors too small to sample) — the "sure" bin, and the fine-bin map.
+// Also clears the tensor's redo histogram, its items' candidate counts and its fine bins.
+__device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, const int64_t* __restrict__ kk,
+                                        const uint32_t* __restrict__ tfirst, const uint32_t* __restrict__ tlast,
+                                        uint32_t* __restrict__ tbin, uint32_t* __restrict__ hist,
+                                        uint32_t* __restrict__ item_cnt, uint32_t* __restrict__ thi,
+                                        uint32_t* __restrict__ fmap, uint32_t* __restrict__ tlo,
+                                        uint32_t* __restrict__ fcount, uint32_t* __restrict__ fhist) {
   constexpr int PER = kSBins / 1024;
-  __shared__ uint32_t h[kSBins];
   __shared__ uint32_t s_w[16];
-  const int t = blockIdx.x;
-  const int64_t n = tsize[t];
-  uint32_t* g = gh + (size_t)t * kSBins;
-  {
-    uint4 v[PER / 4];
-#pragma unroll
-    for (int j = 0; j < PER / 4; ++j) v[j] = reinterpret_cast<const uint4*>(g + PER * threadIdx.x)[j];
-#pragma unroll
-    for (int j = 0; j < PER / 4; ++j) {
-      reinterpret_cast<uint4*>(g + PER * threadIdx.x)[j] = make_uint4(0u, 0u, 0u, 0u);  // clear for the next call
-      reinterpret_cast<uint4*>(h + PER * threadIdx.x)[j] = v[j];
-    }
-  }
   for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;  // this call's redo histogram
   for (uint32_t i = tfirst[t] + threadIdx.x; i <= tlast[t]; i += 1024) item_cnt[i] = 0;  // the fused pass adds to them
-  __syncthreads();
   uint32_t c[PER], loc = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -381,6 +317,75 @@ __global__ __launch_bounds__(1024) void topk_sample_threshold(const int64_t* __r
     fcount[t] = F;
   }
   for (uint32_t i = threadIdx.x; i < F; i += 1024) fhist[(size_t)t * kFineMax + i] = 0;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x, const float* __restrict__ r,
+                                                    float alpha, const int64_t* __restrict__ tbegin,
+                                                    const int64_t* __restrict__ tsize, const uint32_t* __restrict__ smap,
+                                                    int64_t max_runs, uint32_t* __restrict__ gh,
+                                                    uint32_t* __restrict__ arrive, uint32_t* __restrict__ status,
+                                                    const int64_t* __restrict__ kk, const uint32_t* __restrict__ tfirst,
+                                                    const uint32_t* __restrict__ tlast, uint32_t* __restrict__ tbin,
+                                                    uint32_t* __restrict__ hist, uint32_t* __restrict__ item_cnt,
+                                                    uint32_t* __restrict__ thi, uint32_t* __restrict__ fmap,
+                                                    uint32_t* __restrict__ tlo, uint32_t* __restrict__ fcount,
+                                                    uint32_t* __restrict__ fhist) {
+  constexpr int U = kSRunsPerBlock / 256;  // runs per lane group, all loads in flight at once
+  __shared__ uint32_t h[kSBins];
+  __shared__ uint32_t s_last;
+  const int t = (int)smap[2 * blockIdx.x];
+  const int64_t r0 = smap[2 * blockIdx.x + 1];
+  if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = 0u;
+  for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
+  const int64_t base = tbegin[t], n = tsize[t];
+  const int64_t stride = sample_stride(n, max_runs), nr = (n + stride - 1) / stride;
+  const int64_t r1 = min(r0 + (int64_t)kSRunsPerBlock, nr);
+  const uint32_t salt = (uint32_t)t * 0x9E3779B9u;
+  const int q = threadIdx.x & 3;  // float4 of the run
+  float4 xv[U], rv[U];
+  int64_t rel[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // every load issued unconditionally (no branch around a load:
+    // hipcc would wait for each one in turn); past-the-end runs clamped
+    const int64_t j = min(r0 + (threadIdx.x >> 2) + (int64_t)u * 256, r1 - 1);
+    const int64_t lo = j * stride;
+    const int64_t span = min(stride, n - lo);
+    const int64_t runs = max((int64_t)1, span / kSRun);
+    rel[u] = lo + kSRun * (int64_t)(hash32((uint32_t)lo ^ salt) % (uint32_t)runs) + 4 * q;
+    const int64_t e = base + min(rel[u], (n - 1) & ~(int64_t)3);  // 16-byte aligned, inside the arena
+    xv[u] = *reinterpret_cast<const float4*>(x + e);
+    rv[u] = MODE == 1 ? *reinterpret_cast<const float4*>(r + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();  // h cleared
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (r0 + (threadIdx.x >> 2) + (int64_t)u * 256 >= r1) continue;
+    const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
+    const float rs[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (rel[u] + c < n) atomicAdd(&h[mag_key(tprime<MODE>(xs[c], rs[c], alpha)) >> kSShift], 1u);
+  }
+  __syncthreads();
+  uint32_t* g = gh + (size_t)t * kSBins;
+  for (int b = threadIdx.x; b < kSBins; b += 1024)
+    if (h[b]) atomicAdd(&g[b], h[b]);
+  // arrival: every wave's histogram atomics are complete (fence) before its barrier
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t nblk = (uint32_t)((nr + kSRunsPerBlock - 1) / kSRunsPerBlock);
+    const bool last = atomicAdd(&arrive[t], 1u) == nblk - 1;
+    if (last) atomicExch(&arrive[t], 0u);  // ready for the next call
+    s_last = last ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = atomicExch(&g[b], 0u);  // read + clear for the next call
+  __syncthreads();
+  sample_threshold_tensor(t, n, h, kk, tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
 }
 
 // Fine bin of a candidate magnitude (monotone in mag; below / above the mapped range clamp
@@ -1620,7 +1625,7 @@ size_t sort_tmp_bytes(const omf_plan* p) {
 }
 
 // Workspace: everything up to `zero_end` is cleared once per call on the exact path; the
-// sampled path clears its redo histograms in topk_sample_threshold and writes the rest.
+// sampled path clears its redo histograms in topk_sample and writes the rest.
 struct WsLayout {
   size_t hist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
       sub_cnt, item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes, bbase, kb2, fmap, tlo, fcount, fhist,
@@ -1701,25 +1706,34 @@ WsLayout layout_uncached(const omf_plan* p) {
   return L;
 }
 
-// Per (plan, ratio) constant tables of the encoder, plan-owned (omf_plan_access::topk_table),
-// made once: topk_setup's per-tensor k / offsets / item ranges / bucket and super-item bases,
-// the sampling blocks' (tensor, first run) map, the sample histograms gh (zeroed here once,
-// left zeroed by every call) and the plan kernel's arrival counter.
+// Per (plan, ratio, sample size) constant tables of the encoder, plan-owned
+// (omf_plan_access::topk_table), made once: topk_setup's per-tensor k / offsets / item ranges /
+// bucket and super-item bases, the sampling blocks' (tensor, first run) map, the sample
+// histograms gh (zeroed here once, left zeroed by every call) and the arrival counters of the
+// sample (per tensor) and plan kernels (likewise).
 struct SetupTable {
   int64_t *kk, *koff, *kb2;
-  uint32_t *tfirst, *tlast, *bbase, *sbase, *smap, *gh, *done;
+  uint32_t *tfirst, *tlast, *bbase, *sbase, *smap, *gh, *done, *arrive;
   int32_t nsb;
 };
 
+// Runs sampled per tensor at most (a performance knob only: the selection is exact for any
+// sample; OMF_TOPK_SAMPLE_RUNS overrides it for experiments).
+int64_t sample_max_runs() {
+  const char* e = std::getenv("OMF_TOPK_SAMPLE_RUNS");
+  const long long v = e ? std::atoll(e) : 0;
+  return v >= 64 && v <= (1 << 20) ? (int64_t)v : (int64_t)kSMaxRuns;
+}
+
 constexpr uint64_t kSetupTag = 0x5E7A9B1C00000000ull;
 
-int setup_table(omf_plan* p, double ratio, hipStream_t st, uint32_t* status, SetupTable* out) {
+int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uint32_t* status, SetupTable* out) {
   const std::vector<int64_t>& sizes = omf_plan_access::sizes(p);
   const int32_t nt = (int32_t)sizes.size();
   std::vector<uint32_t> smap;
   for (int32_t t = 0; t < nt; ++t) {  // sampling blocks: as sample_stride on the device
     const int64_t n = sizes[t];
-    const int64_t stride = std::max<int64_t>(kSStride, (n + kSMaxRuns - 1) / kSMaxRuns);
+    const int64_t stride = std::max<int64_t>(kSStride, (n + max_runs - 1) / max_runs);
     const int64_t nr = (n + stride - 1) / stride;
     for (int64_t r0 = 0; r0 < nr; r0 += kSRunsPerBlock) {
       smap.push_back((uint32_t)t);
@@ -1736,12 +1750,14 @@ int setup_table(omf_plan* p, double ratio, hipStream_t st, uint32_t* status, Set
   const size_t o_sb = o; o = align256(o + 4 * ((size_t)nt + 1));
   const size_t o_sm = o; o = align256(o + 4 * smap.size());
   const size_t o_done = o; o = align256(o + 16);
+  const size_t o_arr = o; o = align256(o + 4 * (size_t)nt);
   const size_t o_gh = o; o = align256(o + 4 * (size_t)nt * kSBins);
   bool fresh = false;
   uint64_t* host = nullptr;
   uint64_t key;
   std::memcpy(&key, &ratio, 8);
-  uint8_t* d = static_cast<uint8_t*>(omf_plan_access::topk_table(p, key ^ kSetupTag, o, &fresh, &host));
+  key ^= kSetupTag ^ ((uint64_t)max_runs * 0x9E3779B97F4A7C15ull);
+  uint8_t* d = static_cast<uint8_t*>(omf_plan_access::topk_table(p, key, o, &fresh, &host));
   if (!d) return fail(OMF_ENOMEM, "omf_topk_encode: table allocation failed");
   out->kk = reinterpret_cast<int64_t*>(d + o_kk);
   out->koff = reinterpret_cast<int64_t*>(d + o_koff);
@@ -1752,10 +1768,11 @@ int setup_table(omf_plan* p, double ratio, hipStream_t st, uint32_t* status, Set
   out->sbase = reinterpret_cast<uint32_t*>(d + o_sb);
   out->smap = reinterpret_cast<uint32_t*>(d + o_sm);
   out->done = reinterpret_cast<uint32_t*>(d + o_done);
+  out->arrive = reinterpret_cast<uint32_t*>(d + o_arr);
   out->gh = reinterpret_cast<uint32_t*>(d + o_gh);
   out->nsb = (int32_t)(smap.size() / 2);
   if (fresh) {
-    OMF_HIP(hipMemsetAsync(out->done, 0, o - o_done, st));  // the arrival counter and gh
+    OMF_HIP(hipMemsetAsync(out->done, 0, o - o_done, st));  // the arrival counters and gh
     OMF_HIP(hipMemcpyAsync(out->smap, smap.data(), 4 * smap.size(), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(topk_setup, dim3(1), dim3(kThreads), 0, st, omf_plan_access::d_sizes(p), nt, ratio, out->kk,
                        out->koff, out->tfirst, out->tlast, out->bbase, out->kb2, out->sbase, status, 0u);
@@ -1857,20 +1874,21 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   const uint32_t seq = ++hsync->seq == 0 ? ++hsync->seq : hsync->seq;
   // the per-(plan, ratio) constant tables: made by topk_setup on the first call at this ratio
   SetupTable tb;
-  if (int r = setup_table(plan, ratio, st, status, &tb)) return r;
+  const int64_t max_runs = sample_max_runs();
+  if (int r = setup_table(plan, ratio, max_runs, st, status, &tb)) return r;
   kk = tb.kk; koff = tb.koff; tfirst = tb.tfirst; tlast = tb.tlast; bbase = tb.bbase; kb2 = tb.kb2; sbase = tb.sbase;
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
     const dim3 sgrid((unsigned)nt), sblk(1024), fgrid((unsigned)(n_items * kSubsPerItem));
     const dim3 rgrid((unsigned)tb.nsb);
     if (residual_mode == 1)
-      hipLaunchKernelGGL((topk_sample_runs<1>), rgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes,
-                         (const uint32_t*)tb.smap, tb.gh, status);
+      hipLaunchKernelGGL((topk_sample<1>), rgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes,
+                         (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin, hist,
+                         item_cnt, thi, fmap, tlo, fcount, fhist);
     else
-      hipLaunchKernelGGL((topk_sample_runs<0>), rgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes,
-                         (const uint32_t*)tb.smap, tb.gh, status);
-    hipLaunchKernelGGL(topk_sample_threshold, sgrid, sblk, 0, st, d_sizes, kk, tfirst, tlast, tb.gh, tbin, hist, item_cnt,
-                       thi, fmap, tlo, fcount, fhist);
+      hipLaunchKernelGGL((topk_sample<0>), rgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes,
+                         (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin, hist,
+                         item_cnt, thi, fmap, tlo, fcount, fhist);
     if (residual_mode == 1) {
       hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt, item_cnt, cand);
     } else {

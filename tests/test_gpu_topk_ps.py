@@ -118,10 +118,10 @@ def _fmix32(h):
     return h ^ (h >> np.uint64(16))
 
 
-def _sample_positions(n, t):
-    """The elements omf_topk.hip's topk_sample_threshold reads for tensor t: one aligned run
-    of 16 per max(256, n/4096) elements, at a hashed position."""
-    stride = max(256, -(-n // 4096))
+def _sample_positions(n, t, max_runs):
+    """The elements omf_topk.hip's topk_sample reads for tensor t: one aligned run of 16 per
+    max(256, ceil(n / max_runs)) elements, at a hashed position."""
+    stride = max(256, -(-n // max_runs))
     lo = np.arange(0, n, stride, dtype=np.uint64)
     key = lo ^ np.uint64((t * 0x9E3779B9) & 0xFFFFFFFF)
     span = np.minimum(np.uint64(stride), np.uint64(n) - lo)
@@ -161,13 +161,15 @@ def test_topk_sampled_threshold_error_feedback(gpu, alpha):
             K += k
 
 
-def test_topk_sampled_threshold_redo(gpu):
+def test_topk_sampled_threshold_redo(gpu, monkeypatch):
     """A tensor whose sampled elements are exactly its largest: the sample puts the threshold
     above the k-th magnitude, the pass finds fewer than k candidates, and the tensor is redone
     exactly — the k largest, ties by ascending index."""
-    n = 1 << 23  # 4096 runs of 16 = 64 Ki samples < k = 83886
+    runs = 16384
+    monkeypatch.setenv("OMF_TOPK_SAMPLE_RUNS", str(runs))  # the sample size the positions assume
+    n = 1 << 25  # 16 Ki runs of 16 = 256 Ki samples < k = 335544
     x = np.ones(n, np.float32)
-    sp = _sample_positions(n, 1)
+    sp = _sample_positions(n, 1, runs)
     x[sp] = 10.0
     sizes = [40000, n]
     plan = codec.Plan(sizes, device=gpu)
