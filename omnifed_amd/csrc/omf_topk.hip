@@ -371,18 +371,20 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   uint32_t* g = gh + (size_t)t * kSBins;
   for (int b = threadIdx.x; b < kSBins; b += 1024)
     if (h[b]) atomicAdd(&g[b], h[b]);
-  // arrival: every wave's histogram atomics are complete (fence) before its barrier
-  __threadfence();
+  // Arrival (cdna_hip_programming.md §6 Guideline 16, row 1): every wave waits for its
+  // histogram atomics (vmcnt(0); agent-scope RMWs are performed past the XCD's L2), a workgroup
+  // barrier, then one agent-scope add.  No __threadfence: on gfx950 an agent-scope release
+  // writes back the whole L2, and one per wave of ~3 000 blocks cost over a millisecond.
+  drain_vmem();
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint32_t nblk = (uint32_t)((nr + kSRunsPerBlock - 1) / kSRunsPerBlock);
-    const bool last = atomicAdd(&arrive[t], 1u) == nblk - 1;
-    if (last) atomicExch(&arrive[t], 0u);  // ready for the next call
+    const bool last = add_agent(&arrive[t], 1u) == nblk - 1;
+    if (last) __hip_atomic_store(&arrive[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
     s_last = last ? 1u : 0u;
   }
   __syncthreads();
   if (!s_last) return;
-  __threadfence();
   for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = atomicExch(&g[b], 0u);  // read + clear for the next call
   __syncthreads();
   sample_threshold_tensor(t, n, h, kk, tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
@@ -974,13 +976,14 @@ __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk
   // The last block to finish publishes the call's verdict straight into mapped, coherent host
   // memory (no copy packet in the stream, so the bucket kernels behind this one start at once):
   // the data words, then the sequence number with release semantics at system scope; the host
-  // spins on it.  Each block's status atomics come before its arrival (fence); the last one
+  // spins on it.  Each block's status atomics (thread 0's) complete before its arrival
+  // (vmcnt(0), not a fence: an agent-scope release writes back the whole L2); the last one
   // reads status with atomic RMWs (performed where the other blocks' atomics were).
   __syncthreads();
   if (threadIdx.x == 0) {
-    __threadfence();
-    if (atomicAdd(done, 1u) == gridDim.x - 1) {
-      atomicExch(done, 0u);
+    drain_vmem();
+    if (add_agent(done, 1u) == gridDim.x - 1) {
+      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t s0 = atomicOr(&status[0], 0u), s1 = atomicOr(&status[1], 0u), s2 = atomicOr(&status[2], 0u);
       __hip_atomic_store(&host[0], s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&host[1], s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

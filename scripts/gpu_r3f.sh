@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-3: Top-K sampling without fences — tests, sweep, kernel trace; ResNet-18 host issue cost + trace.
+set -o pipefail
+cd "$(dirname "$0")/.." && export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_topk_ps.py tests/test_gpu_r3.py -x -q --timeout 200 \
+    --timeout-method thread -k "topk or Topk or TopK" > gpurun_out/r3f_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/exp/tk_runs_sweep.py 2048 4096 8192 16384 > gpurun_out/r3f_sweep.json 2> gpurun_out/r3f_sweep.err || exit 2
+rm -rf gpurun_out/r3f_topk_prof gpurun_out/r3f_r18_prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r3f_topk_prof -o run -- \
+    python3 bench.py --codec topk --no-cpu-baseline --no-extras --steps 10 > gpurun_out/r3f_topk_prof.log 2>&1 || exit 3
+timeout -k 10 200 python -u scripts/exp/r18_host.py > gpurun_out/r3f_r18_host.json 2> gpurun_out/r3f_r18_host.err || exit 4
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r3f_r18_prof -o run -- \
+    python3 scripts/exp/r18_strategies.py > gpurun_out/r3f_r18_prof.log 2>&1 || exit 5
