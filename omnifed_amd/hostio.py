@@ -94,13 +94,14 @@ def pool():
 
 
 def retain_host_memory(mmap_threshold: int = 32 << 20, trim_threshold: int = 1 << 30) -> bool:
-    """Opt-in, process-wide (glibc ``mallopt``): serve allocations below ``mmap_threshold`` from
+    """Process-wide (glibc ``mallopt``): serve allocations below ``mmap_threshold`` from
     the heap and keep up to ``trim_threshold`` of freed heap memory instead of returning it to
     the OS.  The wire path's host cost is dominated by page faults: every round, protobuf
     allocates ~w·N bytes of fresh message memory for the payloads (the previous round's was
     unmapped when its messages were freed), and each first touch of a 4 KiB page faults.  With
     the memory retained, a round reuses the previous round's pages.  Returns False where glibc
-    is not available.  Not called by the library itself: a deployment opts in."""
+    is not available.  The wire path calls it once (global_grpc_compression._host_memory_policy)
+    unless OMF_RETAIN_HOST_MEMORY=0."""
     try:
         libc = ctypes.CDLL("libc.so.6")
     except OSError:

@@ -1,8 +1,11 @@
 """Where the host-inclusive wire path's time goes (Llama-400M, s = 4, int8 payload): each stage of
 encode_updates_dict / decode_updates_dict timed alone, median of 5 (experiment harness)."""
 import json
+import os
 import sys
 import time
+
+os.environ["OMF_RETAIN_HOST_MEMORY"] = "0"  # glibc defaults first; retained explicitly at the end
 
 import numpy as np
 import torch

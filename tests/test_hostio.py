@@ -53,3 +53,23 @@ def test_fill_bytes_and_stage_payloads_roundtrip(threads):
             hostio.stage_payloads(items, dst.ctypes.data, total, lambda a, b: None, limit=4 << 20, check=check)
     finally:
         hostio.set_workers(None)
+
+
+def test_wire_host_memory_policy_once_and_opt_out(monkeypatch):
+    """The wire path sets the host-memory policy once per process; OMF_RETAIN_HOST_MEMORY=0
+    leaves glibc's defaults alone (hostio.retain_host_memory is never called)."""
+    from omnifed_amd.hybrid.communicator import global_grpc_compression as ggc
+
+    calls = []
+    monkeypatch.setattr(hostio, "retain_host_memory", lambda: calls.append(1) or True)
+    monkeypatch.setattr(ggc, "_HOST_POLICY", None)
+    monkeypatch.setenv("OMF_RETAIN_HOST_MEMORY", "0")
+    assert ggc._host_memory_policy() is False and calls == []
+    monkeypatch.setattr(ggc, "_HOST_POLICY", None)
+    monkeypatch.delenv("OMF_RETAIN_HOST_MEMORY")
+    assert ggc._host_memory_policy() is True and ggc._host_memory_policy() is True
+    assert calls == [1]
+
+
+def test_retain_host_memory_sets_mallopt():
+    assert hostio.retain_host_memory() in (True, False)  # False only without glibc
