@@ -891,9 +891,10 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
 // ---------------------------------------------------------------- grid encoder (strategy 4)
 // Small arenas (ResNet-18: 11 M elements in 2 976 blocks of 4 Ki): ONE launch of one 1024-thread
 // workgroup per CU; each quarter (256 threads) holds kGridNB 4 Ki blocks of x in registers
-// (its four waves publish their fp64 partial sums of squares, the bracketed encoder's layout),
-// every workgroup arrives at one grid-wide counter, and after it every tensor's norm is the same
-// deterministic fold of its partials in every workgroup (no second barrier) and the blocks are
+// (the 16 wave partials of an item — 4 blocks x 4 waves — are summed in a fixed order in LDS and
+// published as ONE fp64 item partial), every workgroup arrives at one grid-wide counter, and
+// after it every tensor's norm is the same deterministic fold of its item partials in every
+// workgroup (no second barrier; one round of loads per wave for tensors of <= 512 items) and the blocks are
 // quantised from registers: x is read once, with no per-tensor hand-off chain (the ring's) and
 // no sampled bracket (the bracketed encoder's four launches).  The hand-off is cdna_hip_
 // programming.md §6 Guideline 16, table row 1: 8-byte sc1 partial stores, every wave's
@@ -905,7 +906,7 @@ constexpr int kGridNB = 3;  // 4 Ki blocks per quarter-workgroup per launch
 
 struct GridArgs {
   EncArgs e;                    // x, q, norm_out, alpha, fmt, levels, Philox key / offset, err, wait_ticks
-  uint64_t* partials;           // fp64 bits, 4 per 4 Ki block
+  uint64_t* partials;           // fp64 bits, one per flat item (16 Ki elements)
   unsigned long long* bar;      // grid arrival counter (monotonic over launches)
   unsigned long long target;    // its value once every workgroup of this launch has arrived
   int64_t nblocks;              // 4 Ki blocks of the plan (4 per flat item)
@@ -947,8 +948,11 @@ __device__ __forceinline__ double grid_partial(const float4 (&v)[4]) {
   return wave_sum_f64((double)acc);
 }
 
-// Tensor t's norm by ONE wave: lane l sums partials l, l + 64, ... in order (fp64), then the
-// butterfly — the same bits in every workgroup.  recover: the partials are recomputed from x.
+// Item partial: its 16 wave partials (block q = 0..3 of the item, wave w = 0..3 of the block's
+// quarter-workgroup) summed in fp64 in the order q-major, w-minor (producer and recovery alike).
+// Tensor t's norm by ONE wave: lane l sums item partials l, l + 64, ... in order (fp64), then
+// the butterfly — the same bits in every workgroup.  recover: the item partials are recomputed
+// from x.
 __device__ float grid_fold(const GridArgs& a, const Item* __restrict__ items, uint32_t p0, uint32_t pn, bool recover) {
   const int lane = threadIdx.x & 63;
   double s = 0.0;
@@ -965,16 +969,19 @@ __device__ float grid_fold(const GridArgs& a, const Item* __restrict__ items, ui
       for (int u = 0; u < U; ++u)
         if (j0 + 64 * u + lane < pn) s += d[u];
     }
-  } else {  // each partial as its wave made it: quarter wave wq of block p / 4
+  } else {  // each item partial as its workgroup made it
     for (uint32_t j = 0; j < pn; ++j) {
-      const int64_t vb = (int64_t)(p0 + j) >> 2;
-      const int wq = (int)((p0 + j) & 3);
-      const Item it = items[vb >> 2];
-      const int64_t b = it.begin + (vb & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
-      float4 v[4];
-      grid_load_block(a.e, b, end, 64 * wq + lane, v);
-      const double p = grid_partial(v);
-      if ((j & 63) == (uint32_t)lane) s += p;
+      const Item it = items[p0 + j];
+      double ip = 0.0;
+      for (int q = 0; q < 4; ++q) {
+        const int64_t b = it.begin + (int64_t)q * kSpecBlk, end = min(b + kSpecBlk, it.end);
+        for (int wq = 0; wq < 4; ++wq) {
+          float4 v[4];
+          grid_load_block(a.e, b, end, 64 * wq + lane, v);
+          ip += grid_partial(v);
+        }
+      }
+      if ((j & 63) == (uint32_t)lane) s += ip;
     }
   }
   return finish_norm(wave_sum_f64(s), a.e.fmt);
@@ -986,6 +993,7 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
                                                          const uint32_t* __restrict__ pbeg,
                                                          const uint32_t* __restrict__ pcnt) {
   __shared__ float s_norm[kGridNB];
+  __shared__ double s_part[kGridNB][16];
   __shared__ uint32_t s_ok;
   const EncArgs& e = a.e;
   const int lt = threadIdx.x & 255, qv = threadIdx.x >> 8, lane = threadIdx.x & 63;
@@ -1008,9 +1016,17 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
 #pragma unroll
   for (int i = 0; i < kGridNB; ++i) {
     const double p = grid_partial(v[i]);
-    const int64_t vb = 4 * ((int64_t)i * W + blockIdx.x) + qv;
-    if (tt[i] >= 0 && lane == 0) st_agent(&a.partials[4 * vb + wq], (uint64_t)__double_as_longlong(p));
+    if (lane == 0) s_part[i][4 * qv + wq] = p;
   }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kGridNB; ++i)  // thread i: item i's partial, in a fixed order
+    if ((int)threadIdx.x == i && tt[i] >= 0) {
+      double ip = 0.0;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ip += s_part[i][j];
+      st_agent(&a.partials[(int64_t)i * W + blockIdx.x], (uint64_t)__double_as_longlong(ip));
+    }
   drain_vmem();
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -1045,7 +1061,7 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
     const float norm = grid_fold(a, items, p0, pcnt[t], s_ok == 0u);
     if (lane == 0) {
       s_norm[wave] = norm;
-      if (4 * 4 * ((int64_t)wave * W + blockIdx.x) == (int64_t)p0) e.norm_out[t] = norm;  // the tensor's first item
+      if ((int64_t)wave * W + blockIdx.x == (int64_t)p0) e.norm_out[t] = norm;  // the tensor's first item
     }
   }
   __syncthreads();
@@ -1332,8 +1348,8 @@ struct omf_plan {
   uint32_t* d_spec_status = nullptr;
   // grid encoder (strategy 4): one workgroup per CU, kGridNB 4 Ki blocks per quarter
   int32_t grid_wgs = 0;             // workgroups of a launch (CUs; 0 = unavailable)
-  uint32_t* d_grid_pbeg = nullptr;  // per tensor: first wave partial (16 per flat item)
-  uint32_t* d_grid_pcnt = nullptr;  // per tensor: wave partials
+  uint32_t* d_grid_pbeg = nullptr;  // per tensor: first flat item (one partial per item)
+  uint32_t* d_grid_pcnt = nullptr;  // per tensor: flat items
   unsigned long long* d_grid_bar = nullptr;  // arrival counter (zeroed at upload)
   uint64_t grid_launches = 0;
   // Top-K tiled decode: per-ratio constant tables (omf_topk.hip), allocated on first use, with
@@ -1596,8 +1612,8 @@ static int upload_plan(omf_plan* p) {
       flat.push_back(Item{cb, std::min(b + n, cb + kSub), t, kQuant, (int32_t)c, 0});
     }
     const int64_t p_end = (int64_t)kWaves * 4 * (int64_t)flat.size();
-    gpbeg[(size_t)t] = (uint32_t)p_begin;
-    gpcnt[(size_t)t] = (uint32_t)(p_end - p_begin);
+    gpbeg[(size_t)t] = (uint32_t)(p_begin / (kWaves * 4));  // the grid encoder: one partial per item
+    gpcnt[(size_t)t] = (uint32_t)((p_end - p_begin) / (kWaves * 4));
     const int64_t R = std::max<int64_t>(1, std::min<int64_t>(kSpecRuns, n / (2 * kSpecRun)));
     br_items.push_back(SpecBrItem{b, n, n / R, (int32_t)R, (int32_t)(n % R), t});
     const int32_t nsegs = (int32_t)((p_end - p_begin + kSpecSeg - 1) / kSpecSeg);
