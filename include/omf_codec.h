@@ -94,7 +94,9 @@ int omf_plan_check(omf_plan* plan, void* stream);
  * encode writes.  ring_dbg (ring encoder): 1 no norm wait (norm := 1), 2 no quantisation,
  * 4 phase cycle counters, 8 slots never marked loaded (every hand-off wait of the poller
  * expires: OMF_ETIMEOUT).  spec_dbg (bracketed encoder): 1 no bracket launch, 2 no finish
- * launch, 4 no fix stores, 8 no fix, 16 no fold (every fix wait expires: OMF_ETIMEOUT).
+ * launch, 4 no fix stores, 8 no fix, 16 no fold (every fix wait expires: OMF_ETIMEOUT);
+ * grid encoder: 32 arrive after the wait (every wait expires, exact recovery), 64 no barrier
+ * wait, 128 no norm fold (norm := 1), 256 no quantisation (phase timings).
  * lds_wait_us > 0 replaces the ring's 20 ms hand-off bound (0 restores it); the norm-wait
  * bound is omf_plan_set_resident_capacity's wait_us. */
 int omf_plan_set_debug(omf_plan* plan, uint32_t ring_dbg, uint32_t spec_dbg, int64_t lds_wait_us);

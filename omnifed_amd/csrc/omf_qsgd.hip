@@ -910,7 +910,8 @@ struct GridArgs {
   unsigned long long* bar;      // grid arrival counter (monotonic over launches)
   unsigned long long target;    // its value once every workgroup of this launch has arrived
   int64_t nblocks;              // 4 Ki blocks of the plan (4 per flat item)
-  uint32_t dbg;                 // test hook (omf_plan_set_debug spec bit 32): never arrive
+  uint32_t dbg;                 // test hooks (omf_plan_set_debug spec bits): 32 arrive late, 64 no wait,
+                                // 128 no fold, 256 no quantisation
 };
 
 typedef uint32_t g32x4_t __attribute__((ext_vector_type(4)));
@@ -1036,7 +1037,7 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
     // bounded wait: wall clock AND a minimum number of polls (a queue context switch advances
     // the clock while the wave is saved)
     uint32_t ok = 1;
-    if (__hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.target) {
+    if (!(a.dbg & 64u) && __hip_atomic_load(a.bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < a.target) {
       const uint64_t t0 = wall_clock64(), min_polls = e.wait_ticks >> 10;
       uint64_t polls = 0;
       for (int k = 0;; k = min(k + 1, 4)) {
@@ -1058,7 +1059,7 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
   if (wave < kGridNB && tt[wave] >= 0) {
     const int32_t t = tt[wave];
     const uint32_t p0 = pbeg[t];
-    const float norm = grid_fold(a, items, p0, pcnt[t], s_ok == 0u);
+    const float norm = (a.dbg & 128u) ? 1.0f : grid_fold(a, items, p0, pcnt[t], s_ok == 0u);
     if (lane == 0) {
       s_norm[wave] = norm;
       if ((int64_t)wave * W + blockIdx.x == (int64_t)p0) e.norm_out[t] = norm;  // the tensor's first item
@@ -1066,6 +1067,7 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
   }
   __syncthreads();
   // phase 3: levels from registers
+  if (a.dbg & 256u) return;
 #pragma unroll
   for (int i = 0; i < kGridNB; ++i) {
     if (tt[i] < 0 || bb[i] >= be[i]) continue;
@@ -1915,7 +1917,7 @@ int omf_plan_set_resident_capacity(omf_plan* plan, int64_t cap, int64_t wait_us)
 int omf_plan_set_debug(omf_plan* plan, uint32_t ring_dbg, uint32_t spec_dbg, int64_t lds_wait_us) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
   if (lds_wait_us < 0) return fail(OMF_EINVAL, "lds_wait_us must be >= 0");
-  if ((ring_dbg & ~15u) || (spec_dbg & ~63u)) return fail(OMF_EINVAL, "omf_plan_set_debug: unknown switch bits");
+  if ((ring_dbg & ~15u) || (spec_dbg & ~511u)) return fail(OMF_EINVAL, "omf_plan_set_debug: unknown switch bits");
   plan->ring_dbg = ring_dbg;
   plan->spec_skip = spec_dbg;
   plan->lds_wait_ticks = lds_wait_us > 0 ? (uint64_t)lds_wait_us * 100ull : kWaitTicks;
