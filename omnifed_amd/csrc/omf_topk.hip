@@ -133,7 +133,7 @@ __device__ __forceinline__ float tprime(float x, float r, float alpha) {
 // sub-chunks in tensor order: omf_qsgd.hip upload_plan), its bucket-table range (bbase) and
 // bucket-buffer region (kb2, k + kBucketHalf keys).  One block; nt may exceed it.  Clears the
 // call's status words.
-__device__ __forceinline__ uint32_t bucket_slots(int64_t k) { return (uint32_t)((k + kBucketHalf) / kBucketHalf + 1); }
+__host__ __device__ __forceinline__ uint32_t bucket_slots(int64_t k) { return (uint32_t)((k + kBucketHalf) / kBucketHalf + 1); }
 
 __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict__ tsize, int32_t nt, double ratio,
                                                        int64_t* __restrict__ kk, int64_t* __restrict__ koff,
@@ -330,13 +330,14 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ item_cnt,
                                                     uint32_t* __restrict__ thi, uint32_t* __restrict__ fmap,
                                                     uint32_t* __restrict__ tlo, uint32_t* __restrict__ fcount,
-                                                    uint32_t* __restrict__ fhist) {
+                                                    uint32_t* __restrict__ fhist, uint32_t blk0) {
   constexpr int U = kSRunsPerBlock / 256;  // runs per lane group, all loads in flight at once
   __shared__ uint32_t h[kSBins];
   __shared__ uint32_t s_last;
-  const int t = (int)smap[2 * blockIdx.x];
-  const int64_t r0 = smap[2 * blockIdx.x + 1];
-  if (blockIdx.x == 0 && threadIdx.x < 4) status[threadIdx.x] = 0u;
+  const uint32_t bid = blk0 + blockIdx.x;  // launches cover ranges of tensors (pipeline groups)
+  const int t = (int)smap[2 * bid];
+  const int64_t r0 = smap[2 * bid + 1];
+  if (bid == 0 && threadIdx.x < 4) status[threadIdx.x] = 0u;
   for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
   const int64_t base = tbegin[t], n = tsize[t];
   const int64_t stride = sample_stride(n, max_runs), nr = (n + stride - 1) / stride;
@@ -500,12 +501,13 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
                                                        const uint32_t* __restrict__ tbin,
                                                        const uint32_t* __restrict__ thi,
                                                        uint32_t* __restrict__ sub_cnt, uint32_t* __restrict__ item_cnt,
-                                                       uint64_t* __restrict__ cand) {
+                                                       uint64_t* __restrict__ cand, uint32_t sub0) {
   __shared__ uint32_t s_w[kWaves];
-  const Item it = items[blockIdx.x / kSubsPerItem];
-  const int64_t b = it.begin + (int64_t)(blockIdx.x % kSubsPerItem) * kSubPer;
+  const uint32_t bid = sub0 + blockIdx.x;
+  const Item it = items[bid / kSubsPerItem];
+  const int64_t b = it.begin + (int64_t)(bid % kSubsPerItem) * kSubPer;
   if (b >= it.end) {  // past a tensor's last sub-chunk
-    if (threadIdx.x == 0) sub_cnt[blockIdx.x] = 0;
+    if (threadIdx.x == 0) sub_cnt[bid] = 0;
     return;
   }
   const uint32_t thr = tbin[it.tensor], hi = thi[it.tensor];
@@ -571,8 +573,8 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
       if ((selm >> c) & 1u) dst[pos++] = ((uint64_t)(idx0 + c) << 32) | (uint64_t)__float_as_uint(vv[c]);
   }
   if (threadIdx.x == 0) {
-    sub_cnt[blockIdx.x] = total;
-    if (total) atomicAdd(&item_cnt[blockIdx.x / kSubsPerItem], total);
+    sub_cnt[bid] = total;
+    if (total) atomicAdd(&item_cnt[bid / kSubsPerItem], total);
   }
 }
 
@@ -862,19 +864,19 @@ struct SupView {
   __device__ __forceinline__ void init(const uint32_t* __restrict__ sbase, int32_t nt,
                                        const uint32_t* __restrict__ tfirst, const uint32_t* __restrict__ tlast,
                                        const Item* __restrict__ items, const uint32_t* __restrict__ sub_cnt,
-                                       uint32_t* s_part, int* s_t) {
-    if (threadIdx.x == 0) {  // the tensor: sbase[t] <= blockIdx.x < sbase[t + 1]
+                                       uint32_t* s_part, int* s_t, uint32_t sup) {
+    if (threadIdx.x == 0) {  // the tensor: sbase[t] <= sup < sbase[t + 1]
       int lo = 0, hi = nt - 1;
       while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
-        if (sbase[mid] <= blockIdx.x) lo = mid;
+        if (sbase[mid] <= sup) lo = mid;
         else hi = mid - 1;
       }
       *s_t = lo;
     }
     __syncthreads();
     t = *s_t;
-    const uint32_t i0 = tfirst[t] + (blockIdx.x - sbase[t]) * kSupItems;
+    const uint32_t i0 = tfirst[t] + (sup - sbase[t]) * kSupItems;
     const uint32_t ni = min((uint32_t)kSupItems, tlast[t] + 1 - i0);
     const uint32_t run = threadIdx.x;  // run j of item j / 16
     const uint32_t c = run < ni * kSubsPerItem ? sub_cnt[(size_t)i0 * kSubsPerItem + run] : 0u;
@@ -924,14 +926,14 @@ __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restric
                                                        const uint32_t* __restrict__ fmap,
                                                        const uint32_t* __restrict__ tlo,
                                                        const uint32_t* __restrict__ fcount,
-                                                       uint32_t* __restrict__ fhist) {
+                                                       uint32_t* __restrict__ fhist, uint32_t sup0) {
   __shared__ uint32_t s_h[kFineMax];
   __shared__ uint32_t s_spre[1025], s_part[1024];
   __shared__ int64_t s_ibeg[kSupItems];
   __shared__ int s_t;
   SupView v{s_spre, s_ibeg, 0, 0};
   for (int i = threadIdx.x; i < kFineMax; i += 1024) s_h[i] = 0;
-  v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t);
+  v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t, sup0 + blockIdx.x);
   const uint32_t lo = tlo[v.t], F = fcount[v.t];
   const uint32_t* map_t = fmap + (size_t)v.t * kCoarse;
   constexpr int U = 4;
@@ -958,7 +960,7 @@ __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restric
 // (se_i = keys in higher bins), a bucket starts at its smallest se.  Flags the tensor for
 // the exact redo when it has fewer than k candidates, and the call for the fallback sort
 // when a kept fine bin holds more than kBucketHalf keys.  status[1] |= redo, [2] |= overflow.
-__device__ void topk_plan_tensor(const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
+__device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
                                  const uint32_t* __restrict__ fhist, const uint32_t* __restrict__ bbase,
                                  int32_t* __restrict__ fbucket, uint32_t* __restrict__ bstart,
                                  BucketRec* __restrict__ brec, uint32_t* __restrict__ bfill,
@@ -971,8 +973,9 @@ __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk
                                                   uint32_t* __restrict__ bfill, const int64_t* __restrict__ kb2,
                                                   uint32_t* __restrict__ flag, uint32_t* __restrict__ status,
                                                   uint32_t* __restrict__ fse, int dbg, uint32_t* __restrict__ done,
-                                                  uint32_t* host, uint32_t seq) {
-  topk_plan_tensor(kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2, flag, status, fse, dbg);
+                                                  uint32_t* host, uint32_t seq, int32_t t0, uint32_t total) {
+  topk_plan_tensor((int)(t0 + blockIdx.x), kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2, flag, status,
+                   fse, dbg);
   // The last block to finish publishes the call's verdict straight into mapped, coherent host
   // memory (no copy packet in the stream, so the bucket kernels behind this one start at once):
   // the data words, then the sequence number with release semantics at system scope; the host
@@ -982,7 +985,7 @@ __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk
   __syncthreads();
   if (threadIdx.x == 0) {
     drain_vmem();
-    if (add_agent(done, 1u) == gridDim.x - 1) {
+    if (add_agent(done, 1u) == total - 1) {  // the call's last plan block, over every launch
       __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t s0 = atomicOr(&status[0], 0u), s1 = atomicOr(&status[1], 0u), s2 = atomicOr(&status[2], 0u);
       __hip_atomic_store(&host[0], s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -993,7 +996,7 @@ __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk
   }
 }
 
-__device__ void topk_plan_tensor(const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
+__device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
                                  const uint32_t* __restrict__ fhist, const uint32_t* __restrict__ bbase,
                                  int32_t* __restrict__ fbucket, uint32_t* __restrict__ bstart,
                                  BucketRec* __restrict__ brec, uint32_t* __restrict__ bfill,
@@ -1003,7 +1006,6 @@ __device__ void topk_plan_tensor(const int64_t* __restrict__ kk, const uint32_t*
   __shared__ uint32_t s_bs[kPlanMaxBuckets];
   __shared__ uint32_t part[1024];
   __shared__ uint32_t s_kend, s_nb, s_over;
-  const int t = blockIdx.x;
   const uint32_t F = fcount[t];
   const uint64_t k = (uint64_t)kk[t];
   const uint32_t b0 = bbase[t], nbmax = bbase[t + 1] - b0;
@@ -1097,14 +1099,14 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
                                                             const int64_t* __restrict__ tbegin,
                                                             float* __restrict__ r, uint64_t* __restrict__ bkeys,
                                                             const uint32_t* __restrict__ status,
-                                                            const uint32_t* __restrict__ thi) {
+                                                            const uint32_t* __restrict__ thi, uint32_t sup0) {
   if (status[1] | status[2]) return;  // the plan's verdict is a fallback: nothing to do
   __shared__ uint32_t s_b[kPlanMaxBuckets];
   __shared__ uint32_t s_spre[1025], s_part[1024];
   __shared__ int64_t s_ibeg[kSupItems];
   __shared__ int s_t;
   SupView v{s_spre, s_ibeg, 0, 0};
-  v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t);
+  v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t, sup0 + blockIdx.x);
   const int t = v.t;
   const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nb = bbase[t + 1] - b0, hi = thi[t];
   const int64_t base = tbegin[t];
@@ -1174,7 +1176,8 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
                                                              const uint32_t* __restrict__ fcount,
                                                              const uint32_t* __restrict__ fhist,
                                                              const uint32_t* __restrict__ fse,
-                                                             const uint32_t* __restrict__ thi, int dbg) {
+                                                             const uint32_t* __restrict__ thi, int dbg,
+                                                             uint32_t b0) {
   __shared__ union {
     typename BucketSort::storage_type sort;
     uint64_t xch[kSubBins];
@@ -1185,7 +1188,7 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
   } s_u;
   __shared__ uint32_t s_part[kBT];
   __shared__ uint32_t s_cmax;
-  const BucketRec rec = brec[blockIdx.x];
+  const BucketRec rec = brec[b0 + blockIdx.x];
   const uint32_t cnt = rec.count_tensor & 0xffffu;
   if (cnt == 0 || (status[1] | status[2])) return;  // block-uniform (a fallback verdict: nothing to do)
   const int t = (int)(rec.count_tensor >> 16);
@@ -1556,6 +1559,8 @@ struct HostSync {
   uint32_t* pinned = nullptr;  // host view
   uint32_t* dev = nullptr;     // device view of the same bytes
   uint32_t seq = 0;
+  hipStream_t side = nullptr;  // the pipeline's second stream (made on first use)
+  hipEvent_t fork = nullptr, join = nullptr;
 };
 
 // Wait for the verdict of call `seq`: spin on the mapped word (it lands as soon as the plan
@@ -1593,6 +1598,72 @@ HostSync* host_sync(int dev) {
     h.dev = static_cast<uint32_t*>(d);
   }
   return &h;
+}
+
+// The second stream and the fork / join events of the group pipeline (per device and thread).
+int pipe_streams(HostSync* h) {
+  if (h->side) return OMF_OK;
+  OMF_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+  OMF_HIP(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
+  OMF_HIP(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
+  return OMF_OK;
+}
+
+// Pipeline groups of the sampled path: contiguous tensor ranges of about equal element counts.
+// Each group's chain (sample -> fused pass -> fine histogram -> plan -> bucket scatter -> bucket
+// sort) is one run of launches on one of two streams, alternating, so that one group's
+// latency-bound kernels (the last sample blocks, the per-tensor plans, the bucket sorts) run
+// beside the next group's streaming pass instead of after the whole arena's.
+struct Group {
+  int32_t t0 = 0, t1 = 0;                           // tensors [t0, t1)
+  uint32_t sb0 = 0, nsb = 0, sub0 = 0, nsub = 0;    // sample blocks, fused-pass blocks
+  uint32_t sup0 = 0, nsup = 0, bk0 = 0, nbk = 0;    // super-items, bucket slots
+};
+
+int topk_group_count(const omf_plan* p) {
+  const char* e = std::getenv("OMF_TOPK_GROUPS");  // experiments
+  int g = e ? std::atoi(e) : 4;
+  if (omf_plan_access::arena_end(p) < ((int64_t)1 << 24)) g = 1;  // small arenas: launch-bound
+  return std::max(1, std::min(g, std::min(16, omf_plan_access::ntensors(p))));
+}
+
+std::vector<Group> make_groups(const std::vector<int64_t>& sizes, double ratio, int64_t max_runs, int G) {
+  const int32_t nt = (int32_t)sizes.size();
+  int64_t total = 0;
+  for (int64_t n : sizes) total += n;
+  std::vector<Group> gs;
+  Group cur;
+  uint32_t sb = 0, sub = 0, sup = 0, bk = 0;
+  int64_t cum = 0;
+  for (int32_t t = 0; t < nt; ++t) {
+    const int64_t n = sizes[t];
+    const int64_t stride = std::max<int64_t>(kSStride, (n + max_runs - 1) / max_runs);  // as setup_table
+    const uint32_t nsb = (uint32_t)(((n + stride - 1) / stride + kSRunsPerBlock - 1) / kSRunsPerBlock);
+    const int64_t ni = (n + kSub - 1) / kSub;  // as topk_setup
+    const uint32_t ns = (uint32_t)((ni + kSupItems - 1) / kSupItems);
+    const uint32_t nb = (uint32_t)bucket_slots(omf_topk_k(n, ratio));
+    cur.nsb += nsb;
+    cur.nsub += (uint32_t)(ni * kSubsPerItem);
+    cur.nsup += ns;
+    cur.nbk += nb;
+    sb += nsb;
+    sub += (uint32_t)(ni * kSubsPerItem);
+    sup += ns;
+    bk += nb;
+    cum += n;
+    const int g = (int)gs.size();
+    if (t == nt - 1 || (g < G - 1 && cum * G >= total * (int64_t)(g + 1))) {
+      cur.t1 = t + 1;
+      gs.push_back(cur);
+      cur = Group{};
+      cur.t0 = t + 1;
+      cur.sb0 = sb;
+      cur.sub0 = sub;
+      cur.sup0 = sup;
+      cur.bk0 = bk;
+    }
+  }
+  return gs;
 }
 
 int dbg_bits() {  // OMF_TOPK_DBG (experiments): 1 = no bucket sort, 2 = no residual zeroing
@@ -1809,15 +1880,11 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   if (!(ratio == ratio)) return fail(OMF_EINVAL, "ratio is NaN");
   const std::vector<int64_t>& sizes = omf_plan_access::sizes(plan);
   int64_t kmax = 0;
-  size_t nbuckets = 0;  // bucket-table slots of this ratio
-  size_t nsup = 0;      // super-items
   for (int64_t n : sizes) {
     const int64_t k = omf_topk_k(n, ratio);
     if (k > n) return fail(OMF_EINVAL, "selected index k out of range (k > numel): compress_ratio too large");
     if (n > 0x7fffffffLL) return fail(OMF_EINVAL, "tensor too large for 32-bit candidate indices");
     kmax = std::max(kmax, k);
-    nbuckets += (size_t)((k + kBucketHalf) / kBucketHalf + 1);
-    nsup += (size_t)(((n + kSub - 1) / kSub + kSupItems - 1) / kSupItems);
   }
   if (omf_plan_access::arena_end(plan) > 0xffffffffLL) return fail(OMF_EINVAL, "arena too large for the sort");
   if (((uintptr_t)x & 15) || (residual && ((uintptr_t)residual & 15)))
@@ -1882,43 +1949,64 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   kk = tb.kk; koff = tb.koff; tfirst = tb.tfirst; tlast = tb.tlast; bbase = tb.bbase; kb2 = tb.kb2; sbase = tb.sbase;
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
-    const dim3 sgrid((unsigned)nt), sblk(1024), fgrid((unsigned)(n_items * kSubsPerItem));
-    const dim3 rgrid((unsigned)tb.nsb);
-    if (residual_mode == 1)
-      hipLaunchKernelGGL((topk_sample<1>), rgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes,
-                         (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin, hist,
-                         item_cnt, thi, fmap, tlo, fcount, fhist);
-    else
-      hipLaunchKernelGGL((topk_sample<0>), rgrid, sblk, 0, st, x, residual, alpha, d_begins, d_sizes,
-                         (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin, hist,
-                         item_cnt, thi, fmap, tlo, fcount, fhist);
-    if (residual_mode == 1) {
-      hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt, item_cnt, cand);
-    } else {
-      if (residual_mode == 2)
-        hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi,
-                           sub_cnt, item_cnt, cand);
-      else
-        hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, st, x, residual, alpha, items, d_begins, tbin, thi,
-                           sub_cnt, item_cnt, cand);
-    }
-    // fast path: exact fine-bin histograms, bucket plan; one status read decides
-    const dim3 supgrid((unsigned)nsup), supblk(1024);
-    hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast, fmap,
-                       tlo, fcount, fhist);
-    // the plan's last block publishes the verdict to mapped host memory; the bucket kernels are
-    // enqueued before the host waits for it (they do nothing when the verdict is a fallback),
-    // so the GPU does not idle while the host reads it
-    hipLaunchKernelGGL(topk_plan, sgrid, sblk, 0, st, kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2,
-                       flag, status, fse, dbg_bits(), tb.done, hsync->dev, seq);
-    OMF_HIP(hipGetLastError());
     const bool forced = force_fallback();
-    if (!forced) {
-      hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, st, cand, items, sub_cnt, sbase, nt, tfirst, tlast,
-                         fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins, rz, sorted, status, thi);
-      hipLaunchKernelGGL(topk_bucket_sort, dim3((unsigned)nbuckets), dim3(kBT), 0, st, sorted, brec, kk, koff, d_begins,
-                         d_sizes, rz, values, indices, status, fmap, tlo, fcount, fhist, fse, thi, dbg_bits());
+    const std::vector<Group> groups = make_groups(omf_plan_access::sizes(plan), ratio, max_runs,
+                                                  topk_group_count(plan));
+    if (groups.size() > 1)
+      if (int r = pipe_streams(hsync)) return r;
+    const int dbg = dbg_bits();
+    for (size_t gi = 0; gi < groups.size(); ++gi) {
+      const Group& G = groups[gi];
+      // group 0 runs on the caller's stream; its sample launch (which clears the call's status
+      // words) is the fork point of the second stream
+      hipStream_t s = (gi & 1) ? hsync->side : st;
+      const dim3 sblk(1024);
+      if (G.nsb) {
+        if (residual_mode == 1)
+          hipLaunchKernelGGL((topk_sample<1>), dim3(G.nsb), sblk, 0, s, x, residual, alpha, d_begins, d_sizes,
+                             (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin,
+                             hist, item_cnt, thi, fmap, tlo, fcount, fhist, G.sb0);
+        else
+          hipLaunchKernelGGL((topk_sample<0>), dim3(G.nsb), sblk, 0, s, x, residual, alpha, d_begins, d_sizes,
+                             (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin,
+                             hist, item_cnt, thi, fmap, tlo, fcount, fhist, G.sb0);
+      }
+      if (gi == 0 && groups.size() > 1) {
+        OMF_HIP(hipEventRecord(hsync->fork, st));
+        OMF_HIP(hipStreamWaitEvent(hsync->side, hsync->fork, 0));
+      }
+      const dim3 fgrid(G.nsub);
+      if (residual_mode == 1)
+        hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt,
+                           item_cnt, cand, G.sub0);
+      else if (residual_mode == 2)
+        hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt,
+                           item_cnt, cand, G.sub0);
+      else
+        hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt,
+                           item_cnt, cand, G.sub0);
+      // fast path: exact fine-bin histograms, bucket plan
+      const dim3 supgrid(G.nsup), supblk(1024);
+      hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, s, cand, items, sub_cnt, sbase, nt, tfirst, tlast, fmap,
+                         tlo, fcount, fhist, G.sup0);
+      // the call's last plan block (over every group) publishes the verdict to mapped host
+      // memory; the bucket kernels are enqueued before the host waits for it (they do nothing
+      // when the verdict is a fallback), so the GPU does not idle while the host reads it
+      hipLaunchKernelGGL(topk_plan, dim3((unsigned)(G.t1 - G.t0)), sblk, 0, s, kk, fcount, fhist, bbase, fbucket,
+                         bstart, brec, bfill, kb2, flag, status, fse, dbg, tb.done, hsync->dev, seq, G.t0,
+                         (uint32_t)nt);
+      if (!forced) {
+        hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, s, cand, items, sub_cnt, sbase, nt, tfirst, tlast,
+                           fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins, rz, sorted, status, thi,
+                           G.sup0);
+        hipLaunchKernelGGL(topk_bucket_sort, dim3(G.nbk), dim3(kBT), 0, s, sorted, brec, kk, koff, d_begins, d_sizes,
+                           rz, values, indices, status, fmap, tlo, fcount, fhist, fse, thi, dbg, G.bk0);
+      }
       OMF_HIP(hipGetLastError());
+    }
+    if (groups.size() > 1) {  // join: the caller's stream continues after the second stream's work
+      OMF_HIP(hipEventRecord(hsync->join, hsync->side));
+      OMF_HIP(hipStreamWaitEvent(st, hsync->join, 0));
     }
     if (int rc = wait_status(hsync, seq, st)) return rc;
     uint32_t host_status[4];

@@ -349,6 +349,39 @@ def test_llama400m_topk_encode_then_tiled_decode(gpu):
     assert torch.equal(y, _scatter_ref(plan, vals, idx, ks))
 
 
+@pytest.mark.parametrize("groups", [2, 3, 4, 7])
+def test_topk_group_pipeline_matches_one_group(gpu, monkeypatch, groups):
+    """The sampled Top-K path run as a two-stream pipeline of tensor groups gives the same bytes
+    (values, indices, residual) as one group on the caller's stream, over three error-feedback
+    calls — and so does the forced fallback sort with the pipeline on."""
+    sizes = [1_500_000] * 9 + [3_000_017, 4096, 777_777, 2_000_000, 65_536, 1 << 21]
+    assert sum(sizes) >= 1 << 24  # the pipeline's minimum arena
+    plan = codec.Plan(sizes, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(31)
+    xs = [torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3 for _ in range(3)]
+
+    def run(n_groups, fallback=False):
+        monkeypatch.setenv("OMF_TOPK_GROUPS", str(n_groups))
+        if fallback:
+            monkeypatch.setenv("OMF_TOPK_FALLBACK", "1")
+        else:
+            monkeypatch.delenv("OMF_TOPK_FALLBACK", raising=False)
+        res = torch.zeros(plan.arena_end, device=gpu)
+        outs = []
+        for i, x in enumerate(xs):
+            v, ix, _ = plan.topk_encode(x, 0.01, residual=res, residual_mode=2 if i == 0 else 1, alpha=3.0)
+            outs.append((v.clone(), ix.clone()))
+        torch.cuda.synchronize()
+        return outs, res
+
+    ref_outs, ref_res = run(1)
+    for fb in (False, True):
+        outs, res = run(groups, fb)
+        for (v0, i0), (v1, i1) in zip(ref_outs, outs):
+            assert torch.equal(v0, v1) and torch.equal(i0, i1)
+        assert torch.equal(ref_res, res)
+
+
 # ---------------------------------------------------------------- grid encoder (strategy 4)
 
 def _oracle_check(plan, x, q, norms, s, seed, off, alpha=1.0, tensors=None):
