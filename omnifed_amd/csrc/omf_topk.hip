@@ -7,7 +7,7 @@
 // alpha = 1 leaves x's bits unchanged.
 //
 // Passes (all tensors of a plan per launch; <= 256 tensors of <= 2^25 elements):
-//   1. topk_sample      one aligned 16-element run of t' per max(256, n/16384) elements
+//   1. topk_sample      one aligned 16-element run of t' per max(256, n/2048) elements
 //                       (hashed position; a random 64-byte sector costs the same as one
 //                       element), 512 runs per block, into an 8192-bin histogram of the top
 //                       13 bits of |t'| (exponent + 5 mantissa bits); the last block of each
@@ -53,7 +53,10 @@ constexpr int kSBins = 1 << kSBits;
 constexpr int kSShift = 31 - kSBits;
 constexpr int kSRun = 16;       // a sample is a 64-byte run of 16 consecutive elements,
 constexpr int kSStride = 256;   // one run per >= 256 elements,
-constexpr int kSMaxRuns = 16384; // default: at most 16 Ki runs (256 Ki samples) per tensor (OMF_TOPK_SAMPLE_RUNS)
+// default: at most 2 Ki runs (32 Ki samples) per tensor (OMF_TOPK_SAMPLE_RUNS).  Llama-400M encode:
+// 1.024 ms at 2 Ki runs, 1.097 at 4 Ki, 1.142 at 8 Ki, 1.194 at 16 Ki (scripts/exp/tk_runs_sweep.py):
+// the sample's random sectors cost more than the tighter threshold saves in the bucket kernels.
+constexpr int kSMaxRuns = 2048;
 constexpr int kV = 16;
 constexpr int64_t kSub = (int64_t)kV * kThreads * 4;
 // Composite candidate key: index << 39 | tensor << 31 | (2^31 - 1 - |t'|bits).  Candidates are
@@ -1621,8 +1624,12 @@ struct Group {
 };
 
 int topk_group_count(const omf_plan* p) {
-  const char* e = std::getenv("OMF_TOPK_GROUPS");  // experiments
-  int g = e ? std::atoi(e) : 4;
+  // Off by default: measured on Llama-400M (scripts/exp/tk_pipe_sweep.py) the two streams'
+  // kernels do not overlap to any profit — 1.024 ms with one group, 1.036 / 1.139 / 1.328 ms
+  // with 2 / 4 / 8 (the concurrent streaming passes slow each other and every group adds its
+  // launches).  OMF_TOPK_GROUPS (experiments) turns it on.
+  const char* e = std::getenv("OMF_TOPK_GROUPS");
+  int g = e ? std::atoi(e) : 1;
   if (omf_plan_access::arena_end(p) < ((int64_t)1 << 24)) g = 1;  // small arenas: launch-bound
   return std::max(1, std::min(g, std::min(16, omf_plan_access::ntensors(p))));
 }
