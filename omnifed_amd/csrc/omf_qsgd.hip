@@ -996,18 +996,13 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
   __shared__ float s_norm[kGridNB];
   __shared__ double s_part[kGridNB][16];
   __shared__ uint32_t s_ok;
-  // Each thread's Philox words for its blocks (12 per block: 16 uniforms of 24 bits), made while
-  // its loads are in flight and parked here until the norms are known: the draws depend on the
-  // element positions only, and the quantisation after the barrier is then Philox-free.
-  // Word-major (conflict-free): s_u[(12 i + w) * 1024 + thread].  144 KiB of the CU's 160.
-  __shared__ uint32_t s_u[kGridNB * 12 * 1024];
   const EncArgs& e = a.e;
   const int lt = threadIdx.x & 255, qv = threadIdx.x >> 8, lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6, wq = wave & 3;
   const int64_t W = gridDim.x;
   float4 v[kGridNB][4];
   int64_t bb[kGridNB], be[kGridNB];
-  int32_t tt[kGridNB], ck[kGridNB];
+  int32_t tt[kGridNB];
   // phase 1: the blocks' x into registers, their wave partials published
 #pragma unroll
   for (int i = 0; i < kGridNB; ++i) {
@@ -1017,25 +1012,7 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
     bb[i] = it.begin + qv * kSpecBlk;
     be[i] = live ? min(bb[i] + kSpecBlk, it.end) : bb[i];  // empty range: loads read 0
     tt[i] = live ? it.tensor : -1;
-    ck[i] = it.chunk;
     grid_load_block(e, bb[i], be[i], lt, v[i]);
-  }
-#pragma unroll
-  for (int i = 0; i < kGridNB; ++i) {
-    // the block's first element within its tensor is chunk * 16 Ki + quarter * 4 Ki
-    const uint64_t G = (uint64_t)(((int64_t)ck[i] * kSub + (int64_t)qv * kSpecBlk) >> 12) * (uint64_t)kThreads +
-                       (uint64_t)lt;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const uint64_t ctr = 3 * G + c;
-      const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)tt[i], e.offset),
-                                    e.seed_lo, e.seed_hi);
-      uint32_t* dst = s_u + (size_t)(12 * i + 4 * c) * 1024 + threadIdx.x;
-      dst[0] = r.x;
-      dst[1024] = r.y;
-      dst[2048] = r.z;
-      dst[3072] = r.w;
-    }
   }
 #pragma unroll
   for (int i = 0; i < kGridNB; ++i) {
@@ -1098,9 +1075,15 @@ __global__ __launch_bounds__(1024) void qsgd_encode_grid(GridArgs a, const Item*
     const Divisor dv(norm, e.fmt);
     float4 uu[4];
     {
+      const uint64_t G = (uint64_t)((bb[i] - begins[tt[i]]) >> 12) * (uint64_t)kThreads + (uint64_t)lt;
       uint32_t w[12];
 #pragma unroll
-      for (int k = 0; k < 12; ++k) w[k] = s_u[(size_t)(12 * i + k) * 1024 + threadIdx.x];
+      for (int c = 0; c < 3; ++c) {
+        const uint64_t ctr = 3 * G + c;
+        const uint4 r = philox4x32_10(make_uint4((uint32_t)ctr, (uint32_t)(ctr >> 32), (uint32_t)tt[i], e.offset),
+                                      e.seed_lo, e.seed_hi);
+        w[4 * c] = r.x; w[4 * c + 1] = r.y; w[4 * c + 2] = r.z; w[4 * c + 3] = r.w;
+      }
 #pragma unroll
       for (int sl = 0; sl < 4; ++sl) uu[sl] = u24x4(w[3 * sl], w[3 * sl + 1], w[3 * sl + 2]);
     }
