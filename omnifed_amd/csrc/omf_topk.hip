@@ -864,23 +864,15 @@ struct SupView {
   int64_t* s_ibeg;    // [kSupItems] arena offsets of the items
   int t;
   uint32_t total;
-  __device__ __forceinline__ void init(const uint32_t* __restrict__ sbase, int32_t nt,
-                                       const uint32_t* __restrict__ tfirst, const uint32_t* __restrict__ tlast,
-                                       const Item* __restrict__ items, const uint32_t* __restrict__ sub_cnt,
-                                       uint32_t* s_part, int* s_t, uint32_t sup) {
-    if (threadIdx.x == 0) {  // the tensor: sbase[t] <= sup < sbase[t + 1]
-      int lo = 0, hi = nt - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (sbase[mid] <= sup) lo = mid;
-        else hi = mid - 1;
-      }
-      *s_t = lo;
-    }
-    __syncthreads();
-    t = *s_t;
-    const uint32_t i0 = tfirst[t] + (sup - sbase[t]) * kSupItems;
-    const uint32_t ni = min((uint32_t)kSupItems, tlast[t] + 1 - i0);
+  // supinfo[sup] = {tensor, first item, items} (a plan-owned table: no search), and the
+  // tensor's fine-bin map staged into s_map[kCoarse] (read per key by the callers).
+  __device__ __forceinline__ void init(const uint4* __restrict__ supinfo, const Item* __restrict__ items,
+                                       const uint32_t* __restrict__ sub_cnt, const uint32_t* __restrict__ fmap,
+                                       uint32_t* s_map, uint32_t* s_part, uint32_t sup) {
+    const uint4 si = supinfo[sup];
+    t = (int)si.x;
+    const uint32_t i0 = si.y, ni = si.z;
+    s_map[threadIdx.x] = fmap[(size_t)t * kCoarse + threadIdx.x];  // 1024 threads = kCoarse
     const uint32_t run = threadIdx.x;  // run j of item j / 16
     const uint32_t c = run < ni * kSubsPerItem ? sub_cnt[(size_t)i0 * kSubsPerItem + run] : 0u;
     if (threadIdx.x < ni) s_ibeg[threadIdx.x] = items[i0 + threadIdx.x].begin;
@@ -923,9 +915,7 @@ __global__ __launch_bounds__(kThreads) void topk_restore(const uint64_t* __restr
 __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restrict__ cand,
                                                        const Item* __restrict__ items,
                                                        const uint32_t* __restrict__ sub_cnt,
-                                                       const uint32_t* __restrict__ sbase, int32_t nt,
-                                                       const uint32_t* __restrict__ tfirst,
-                                                       const uint32_t* __restrict__ tlast,
+                                                       const uint4* __restrict__ supinfo,
                                                        const uint32_t* __restrict__ fmap,
                                                        const uint32_t* __restrict__ tlo,
                                                        const uint32_t* __restrict__ fcount,
@@ -933,12 +923,12 @@ __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restric
   __shared__ uint32_t s_h[kFineMax];
   __shared__ uint32_t s_spre[1025], s_part[1024];
   __shared__ int64_t s_ibeg[kSupItems];
-  __shared__ int s_t;
+  __shared__ uint32_t s_map[kCoarse];
   SupView v{s_spre, s_ibeg, 0, 0};
   for (int i = threadIdx.x; i < kFineMax; i += 1024) s_h[i] = 0;
-  v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t, sup0 + blockIdx.x);
+  v.init(supinfo, items, sub_cnt, fmap, s_map, s_part, sup0 + blockIdx.x);
   const uint32_t lo = tlo[v.t], F = fcount[v.t];
-  const uint32_t* map_t = fmap + (size_t)v.t * kCoarse;
+  const uint32_t* map_t = s_map;
   constexpr int U = 4;
   for (uint32_t e0 = threadIdx.x; e0 < v.total; e0 += U * 1024) {
     uint64_t key[U];
@@ -1088,9 +1078,7 @@ __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const ui
 __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __restrict__ cand,
                                                             const Item* __restrict__ items,
                                                             const uint32_t* __restrict__ sub_cnt,
-                                                            const uint32_t* __restrict__ sbase, int32_t nt,
-                                                            const uint32_t* __restrict__ tfirst,
-                                                            const uint32_t* __restrict__ tlast,
+                                                            const uint4* __restrict__ supinfo,
                                                             const uint32_t* __restrict__ fmap,
                                                             const uint32_t* __restrict__ tlo,
                                                             const uint32_t* __restrict__ fcount,
@@ -1107,15 +1095,15 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
   __shared__ uint32_t s_b[kPlanMaxBuckets];
   __shared__ uint32_t s_spre[1025], s_part[1024];
   __shared__ int64_t s_ibeg[kSupItems];
-  __shared__ int s_t;
+  __shared__ uint32_t s_map[kCoarse];
   SupView v{s_spre, s_ibeg, 0, 0};
-  v.init(sbase, nt, tfirst, tlast, items, sub_cnt, s_part, &s_t, sup0 + blockIdx.x);
+  v.init(supinfo, items, sub_cnt, fmap, s_map, s_part, sup0 + blockIdx.x);
   const int t = v.t;
   const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nb = bbase[t + 1] - b0, hi = thi[t];
   const int64_t base = tbegin[t];
   for (uint32_t j = threadIdx.x; j < nb; j += 1024) s_b[j] = 0;
   __syncthreads();
-  const uint32_t* map_t = fmap + (size_t)t * kCoarse;
+  const uint32_t* map_t = s_map;
   const int32_t* fb = fbucket + (size_t)t * kFineMax;
   constexpr int U = 4;
   for (int phase = 0; phase < 2; ++phase) {  // 0: count per bucket; 1: place
@@ -1795,6 +1783,7 @@ WsLayout layout_uncached(const omf_plan* p) {
 struct SetupTable {
   int64_t *kk, *koff, *kb2;
   uint32_t *tfirst, *tlast, *bbase, *sbase, *smap, *gh, *done, *arrive;
+  uint32_t* supinfo;  // per super-item {tensor, first item, items, 0}
   int32_t nsb;
 };
 
@@ -1821,6 +1810,18 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
       smap.push_back((uint32_t)r0);
     }
   }
+  std::vector<uint32_t> supinfo;  // as topk_setup's super-item bases
+  uint32_t item0 = 0;
+  for (int32_t t = 0; t < nt; ++t) {
+    const uint32_t ni = (uint32_t)((sizes[t] + kSub - 1) / kSub);
+    for (uint32_t i = 0; i < ni; i += kSupItems) {
+      supinfo.push_back((uint32_t)t);
+      supinfo.push_back(item0 + i);
+      supinfo.push_back(std::min<uint32_t>(kSupItems, ni - i));
+      supinfo.push_back(0u);
+    }
+    item0 += ni;
+  }
   size_t o = 0;
   const size_t o_kk = o; o = align256(o + 8 * (size_t)nt);
   const size_t o_koff = o; o = align256(o + 8 * ((size_t)nt + 1));
@@ -1830,6 +1831,7 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
   const size_t o_bb = o; o = align256(o + 4 * ((size_t)nt + 1));
   const size_t o_sb = o; o = align256(o + 4 * ((size_t)nt + 1));
   const size_t o_sm = o; o = align256(o + 4 * smap.size());
+  const size_t o_si = o; o = align256(o + 4 * supinfo.size());
   const size_t o_done = o; o = align256(o + 16);
   const size_t o_arr = o; o = align256(o + 4 * (size_t)nt);
   const size_t o_gh = o; o = align256(o + 4 * (size_t)nt * kSBins);
@@ -1848,6 +1850,7 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
   out->bbase = reinterpret_cast<uint32_t*>(d + o_bb);
   out->sbase = reinterpret_cast<uint32_t*>(d + o_sb);
   out->smap = reinterpret_cast<uint32_t*>(d + o_sm);
+  out->supinfo = reinterpret_cast<uint32_t*>(d + o_si);
   out->done = reinterpret_cast<uint32_t*>(d + o_done);
   out->arrive = reinterpret_cast<uint32_t*>(d + o_arr);
   out->gh = reinterpret_cast<uint32_t*>(d + o_gh);
@@ -1855,6 +1858,7 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
   if (fresh) {
     OMF_HIP(hipMemsetAsync(out->done, 0, o - o_done, st));  // the arrival counters and gh
     OMF_HIP(hipMemcpyAsync(out->smap, smap.data(), 4 * smap.size(), hipMemcpyHostToDevice, st));
+    OMF_HIP(hipMemcpyAsync(out->supinfo, supinfo.data(), 4 * supinfo.size(), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(topk_setup, dim3(1), dim3(kThreads), 0, st, omf_plan_access::d_sizes(p), nt, ratio, out->kk,
                        out->koff, out->tfirst, out->tlast, out->bbase, out->kb2, out->sbase, status, 0u);
     OMF_HIP(hipGetLastError());
@@ -1994,7 +1998,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
                            item_cnt, cand, G.sub0);
       // fast path: exact fine-bin histograms, bucket plan
       const dim3 supgrid(G.nsup), supblk(1024);
-      hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, s, cand, items, sub_cnt, sbase, nt, tfirst, tlast, fmap,
+      hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo, fmap,
                          tlo, fcount, fhist, G.sup0);
       // the call's last plan block (over every group) publishes the verdict to mapped host
       // memory; the bucket kernels are enqueued before the host waits for it (they do nothing
@@ -2003,7 +2007,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
                          bstart, brec, bfill, kb2, flag, status, fse, dbg, tb.done, hsync->dev, seq, G.t0,
                          (uint32_t)nt);
       if (!forced) {
-        hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, s, cand, items, sub_cnt, sbase, nt, tfirst, tlast,
+        hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo,
                            fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins, rz, sorted, status, thi,
                            G.sup0);
         hipLaunchKernelGGL(topk_bucket_sort, dim3(G.nbk), dim3(kBT), 0, s, sorted, brec, kk, koff, d_begins, d_sizes,
