@@ -26,7 +26,7 @@ def load(d, counter):
     return per
 
 
-TOPK_ENCODE = ("topk_sample_runs", "topk_sample_threshold", "topk_fused", "topk_fine_hist", "topk_plan",
+TOPK_ENCODE = ("topk_sample", "topk_fused", "topk_fine_hist", "topk_plan",
                "topk_bucket_scatter", "topk_bucket_sort")
 TOPK_DECODE = ("topk_dec_place", "topk_dec_tiles", "topk_dec_overflow")
 
