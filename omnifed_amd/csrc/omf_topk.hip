@@ -1661,9 +1661,16 @@ std::vector<Group> make_groups(const std::vector<int64_t>& sizes, double ratio, 
   return gs;
 }
 
-int dbg_bits() {  // OMF_TOPK_DBG (experiments): 1 = no bucket sort, 2 = no residual zeroing
+int dbg_bits() {  // OMF_TOPK_DBG: 4 = print the verdict flags, 8 = print over-full fine bins;
+  // experiment builds only (-DOMF_EXPERIMENTS; they change what an encode writes):
+  // 1 = no bucket sort, 2 = no residual zeroing
   const char* e = std::getenv("OMF_TOPK_DBG");
-  return e ? std::atoi(e) : 0;
+  const int d = e ? std::atoi(e) : 0;
+#ifdef OMF_EXPERIMENTS
+  return d;
+#else
+  return d & ~3;
+#endif
 }
 
 bool force_fallback() {

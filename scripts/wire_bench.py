@@ -28,7 +28,7 @@ comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=
 targets = {n: torch.empty_like(t) for n, t in upd.items()}
 
 
-def tm(fn, reps=3):
+def tm(fn, reps=7):
     fn()
     torch.cuda.synchronize()
     ts = []
