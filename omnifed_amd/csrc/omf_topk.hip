@@ -398,26 +398,26 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
 // to the lowest / highest fine bin).
 // fine_bin plus the key's position inside its fine bin: the low `wbits` bits of |t'| (0 bits
 // for the clamped bottom / top bins).
+// Branch-free, so the map load is never under a branch (hipcc waits for a load issued under a
+// branch at the branch's end, which serialises the loads of an unrolled loop).
+// Bit arithmetic only (hipcc turns selects here into branches, and waits for a load issued under
+// a branch at the branch's end, which serialised the loads of the unrolled loops that call this):
+// out-of-range coarse bins go to fine bin 0 (below) or F - 1 (above) with no low bits.
 __device__ __forceinline__ uint32_t fine_bin_pos(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t,
                                                  uint32_t F, uint32_t& low, uint32_t& wbits) {
   const int c = (int)(mag >> kSShift) - (int)lo;
-  low = 0;
-  wbits = 0;
-  if (c < 0) return 0u;
-  if (c >= kCoarse) return F - 1u;
-  const uint32_t m = map_t[c], r = m >> 16;
-  wbits = kSShift - r;
+  const uint32_t m = map_t[min(max(c, 0), kCoarse - 1)], r = m >> 16;
+  const uint32_t below = (uint32_t)(c >> 31), above = (uint32_t)((kCoarse - 1 - c) >> 31);  // all ones or 0
+  wbits = (kSShift - r) & ~(below | above);
   low = mag & ((1u << wbits) - 1u);
-  return (m & 0xffffu) + ((mag >> wbits) & ((1u << r) - 1u));
+  const uint32_t fb = (m & 0xffffu) + ((mag >> (kSShift - r)) & ((1u << r) - 1u));
+  return min((fb | above) & ~below, F - 1u);  // an in-range fine bin is < F
 }
 
 __device__ __forceinline__ uint32_t fine_bin(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t,
                                              uint32_t F) {
-  const int c = (int)(mag >> kSShift) - (int)lo;
-  if (c < 0) return 0u;
-  if (c >= kCoarse) return F - 1u;
-  const uint32_t m = map_t[c], r = m >> 16;
-  return (m & 0xffffu) + ((mag >> (kSShift - r)) & ((1u << r) - 1u));
+  uint32_t low, wbits;
+  return fine_bin_pos(mag, lo, map_t, F, low, wbits);
 }
 
 // Append the selected elements of one 8 Ki-element pass of an item to the item's region in
@@ -1151,8 +1151,6 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
 // sorted instead.  Sort key: (2^31-1-|t'|bits) << 33 | index << 1 | sign.
 constexpr int kSubBins = kBT * kBI;  // 4096
 constexpr uint32_t kMaxRun = 32;
-using BucketSort = rocprim::block_sort<uint64_t, kBT, kBI, rocprim::empty_type,
-                                       rocprim::block_sort_algorithm::merge_sort>;
 __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void topk_bucket_sort(const uint64_t* __restrict__ bkeys,
                                                              const BucketRec* __restrict__ brec,
                                                              const int64_t* __restrict__ kk,
@@ -1169,16 +1167,16 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
                                                              const uint32_t* __restrict__ fse,
                                                              const uint32_t* __restrict__ thi, int dbg,
                                                              uint32_t b0) {
+  // 40 KiB of LDS (four blocks per CU): the sub-bin counters, then offsets, are 16-bit fields
+  // packed two per word (a bucket holds <= 4096 keys), and the scan's wave totals borrow the first
+  // words of that array while it holds nothing live.
   __shared__ union {
-    typename BucketSort::storage_type sort;
     uint64_t xch[kSubBins];
     struct {
       uint64_t out[kSubBins];
-      uint32_t start[kSubBins];
+      uint32_t start2[kSubBins / 2];
     } cs;
   } s_u;
-  __shared__ uint32_t s_part[kBT];
-  __shared__ uint32_t s_cmax;
   const BucketRec rec = brec[b0 + blockIdx.x];
   const uint32_t cnt = rec.count_tensor & 0xffffu;
   if (cnt == 0 || (status[1] | status[2])) return;  // block-uniform (a fallback verdict: nothing to do)
@@ -1190,65 +1188,83 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
   const uint32_t* map_t = fmap + (size_t)t * kCoarse;
   const uint32_t* h_t = fhist + (size_t)t * kFineMax;
   const uint32_t* se_t = fse + (size_t)t * kFineMax;
-  if (threadIdx.x == 0) s_cmax = 0;
   // Sub-bin of a key = its rank slot if keys were spread evenly inside their fine bin: the fine
   // bin's first rank in the bucket (se - start) plus (c - 1 - low * c / 2^wbits) for a bin of
   // c keys, descending |t'|.  Sub-bins = the bucket's key count, about one key each.
+  // Three rounds of loads, each issued whole before any is used (no load under a branch): the
+  // keys (past the count: the last key again), their fine bins' maps, the bins' counts and ranks.
   uint64_t keys[kBI];
-  uint32_t sub[kBI];
+  uint32_t meta[kBI];  // sub-bin << 16 | slot in it (0xffffffff: no key)
+  uint32_t low[kBI], wb[kBI], fbin[kBI];
 #pragma unroll
-  for (int j = 0; j < kBI; ++j) {  // striped loads
+  for (int j = 0; j < kBI; ++j) keys[j] = src[min(threadIdx.x + (uint32_t)j * kBT, cnt - 1u)];  // striped
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) asm volatile("" : "+v"(keys[j]));
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) fbin[j] = fine_bin_pos((uint32_t)keys[j] & 0x7fffffffu, lo, map_t, F, low[j], wb[j]);
+  uint32_t cbv[kBI], sev[kBI];
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {
+    cbv[j] = h_t[fbin[j]];
+    sev[j] = se_t[fbin[j]];
+  }
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) asm volatile("" : "+v"(cbv[j]), "+v"(sev[j]));  // loaded here, not sunk under e < cnt
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {
     const uint32_t e = threadIdx.x + (uint32_t)j * kBT;
-    uint64_t sk = ~0ull;
-    sub[j] = 0xffffffffu;
-    if (e < cnt) {
-      const uint64_t key = src[e];
-      const uint32_t bits = (uint32_t)key, mag = bits & 0x7fffffffu;
-      sk = ((uint64_t)(0x7fffffffu - mag) << 33) | ((key >> 32) << 1) | (uint64_t)(bits >> 31);
-      uint32_t low, wbits;
-      const uint32_t fb = fine_bin_pos(mag, lo, map_t, F, low, wbits);
-      const uint32_t cb = h_t[fb], rel = se_t[fb] - st;
-      const uint32_t in = cb - 1u - (uint32_t)(((uint64_t)low * cb) >> wbits);
-      sub[j] = min(rel + in, cnt - 1u);
-    }
-    keys[j] = sk;
+    const uint32_t cb = cbv[j], rel = sev[j] - st;
+    const uint32_t bits = (uint32_t)keys[j], mag = bits & 0x7fffffffu;
+    const uint32_t in = cb - 1u - (uint32_t)(((uint64_t)low[j] * cb) >> wb[j]);
+    meta[j] = e < cnt ? min(rel + in, cnt - 1u) : 0xffffffffu;
+    keys[j] = e < cnt ? ((uint64_t)(0x7fffffffu - mag) << 33) | ((keys[j] >> 32) << 1) | (uint64_t)(bits >> 31) : ~0ull;
   }
-  for (int i = threadIdx.x; i < kSubBins; i += kBT) s_u.cs.start[i] = 0;
+  for (int i = threadIdx.x; i < kSubBins / 2; i += kBT) s_u.cs.start2[i] = 0;
   __syncthreads();
-  uint32_t meta[kBI];  // sub-bin << 16 | slot in it
 #pragma unroll
   for (int j = 0; j < kBI; ++j) {
-    meta[j] = 0xffffffffu;
-    if (sub[j] != 0xffffffffu) meta[j] = (sub[j] << 16) | atomicAdd(&s_u.cs.start[sub[j]], 1u);
+    if (meta[j] == 0xffffffffu) continue;
+    const uint32_t sb = meta[j], sh = 16u * (sb & 1u);
+    meta[j] = (sb << 16) | ((atomicAdd(&s_u.cs.start2[sb >> 1], 1u << sh) >> sh) & 0xffffu);
   }
   __syncthreads();
-  uint32_t c[kBI], loc = 0, cmx = 0;  // this thread's sub-bins kBI tid ..
+  uint32_t c[kBI], loc = 0, over = 0;  // this thread's sub-bins kBI tid ..
 #pragma unroll
-  for (int j = 0; j < kBI; ++j) {
-    c[j] = s_u.cs.start[threadIdx.x * kBI + j];
-    loc += c[j];
-    cmx = max(cmx, c[j]);
+  for (int j = 0; j < kBI; j += 2) {
+    const uint32_t w2 = s_u.cs.start2[(threadIdx.x * kBI + j) >> 1];
+    c[j] = w2 & 0xffffu;
+    c[j + 1] = w2 >> 16;
+    loc += c[j] + c[j + 1];
+    over |= (c[j] > kMaxRun || c[j + 1] > kMaxRun) ? 1u : 0u;
   }
-  if (cmx > kMaxRun) atomicMax(&s_cmax, cmx);
+  // one scan carries both the counts (< 2^20) and, above them, how many threads saw a sub-bin
+  // of more than kMaxRun keys; its first barrier orders every thread's reads of start2 before
+  // the wave totals land there
   uint32_t tot;
-  const uint32_t inc = block_scan_incl<kBT>(loc, s_part, tot);  // (its barriers publish s_cmax)
-  const bool merge = s_cmax > kMaxRun;  // block-uniform
+  const uint32_t inc = block_scan_incl<kBT>(loc | (over << 20), s_u.cs.start2, tot) & 0xfffffu;
+  const bool merge = (tot >> 20) != 0u;  // block-uniform
+  __syncthreads();  // every thread has read the wave totals
   if (!merge && !(dbg & 1)) {
     uint32_t run = inc - loc;
 #pragma unroll
-    for (int j = 0; j < kBI; ++j) {
-      s_u.cs.start[threadIdx.x * kBI + j] = run;
-      run += c[j];
+    for (int j = 0; j < kBI; j += 2) {
+      s_u.cs.start2[(threadIdx.x * kBI + j) >> 1] = run | ((run + c[j]) << 16);
+      run += c[j] + c[j + 1];
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kBI; ++j)
-      if (meta[j] != 0xffffffffu) s_u.cs.out[s_u.cs.start[meta[j] >> 16] + (meta[j] & 0xffffu)] = keys[j];
+      if (meta[j] != 0xffffffffu) {
+        const uint32_t sb = meta[j] >> 16;
+        const uint32_t at = (s_u.cs.start2[sb >> 1] >> (16u * (sb & 1u))) & 0xffffu;
+        s_u.cs.out[at + (meta[j] & 0xffffu)] = keys[j];
+      }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kBI; ++j) {  // insertion sort inside each sub-bin
       if (c[j] < 2) continue;
-      uint64_t* a = s_u.cs.out + s_u.cs.start[threadIdx.x * kBI + j];
+      const uint32_t sb = threadIdx.x * kBI + j;
+      uint64_t* a = s_u.cs.out + ((s_u.cs.start2[sb >> 1] >> (16u * (sb & 1u))) & 0xffffu);
       for (uint32_t x = 1; x < c[j]; ++x) {
         const uint64_t v = a[x];
         uint32_t y = x;
@@ -1259,13 +1275,25 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kBI; ++j) keys[j] = s_u.cs.out[threadIdx.x + j * kBT];
-  } else if (merge) {
-    __syncthreads();
-    BucketSort().sort(keys, s_u.sort);
-    __syncthreads();  // blocked (thread i: ranks kBI i ..) -> striped, for coalesced stores
+  } else if (merge) {  // rare (ties, clusters): a bitonic sort of the whole bucket in LDS
 #pragma unroll
-    for (int j = 0; j < kBI; ++j) s_u.xch[threadIdx.x * kBI + j] = keys[j];
+    for (int j = 0; j < kBI; ++j) s_u.xch[threadIdx.x + j * kBT] = keys[j];  // no key: ~0, sorts last
     __syncthreads();
+#pragma unroll 1
+    for (uint32_t size = 2; size <= (uint32_t)kSubBins; size <<= 1)
+#pragma unroll 1
+      for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+#pragma unroll 1
+        for (uint32_t i = threadIdx.x; i < (uint32_t)kSubBins / 2; i += kBT) {
+          const uint32_t a = 2 * i - (i & (stride - 1)), b = a + stride;  // a: bit `stride` clear
+          const uint64_t ka = s_u.xch[a], kb = s_u.xch[b];
+          if ((ka > kb) == ((a & size) == 0)) {  // ascending where bit `size` of a is clear
+            s_u.xch[a] = kb;
+            s_u.xch[b] = ka;
+          }
+        }
+        __syncthreads();
+      }
 #pragma unroll
     for (int j = 0; j < kBI; ++j) keys[j] = s_u.xch[threadIdx.x + j * kBT];
   }
@@ -1412,24 +1440,26 @@ __device__ __forceinline__ int dec_tensor_of(const int64_t* __restrict__ koff, i
 // Place one block of kDecChunk consecutive selected values into their super-tiles' buckets:
 // LDS counts over the block's super-tile range, one global reservation per touched super-tile,
 // then (position in the super-tile << 32 | value bits) at its slot, or into the overflow list
-// (arena position << 32 | value bits) past the bucket's capacity.
+// (arena position << 32 | value bits) past the bucket's capacity.  The block's first and last
+// tensor come from the plan's per-ratio table (blk_t); a block that spans several tensors (the
+// small ones) finds each value's tensor by a binary search of their koff staged in LDS.
+constexpr int kDecWin = 512;
 __global__ __launch_bounds__(kThreads) void topk_dec_place(const float* __restrict__ values,
                                                            const int64_t* __restrict__ indices,
                                                            const int64_t* __restrict__ sizes,
                                                            const int64_t* __restrict__ begins,
-                                                           const int64_t* __restrict__ koff, int nt, int64_t ktot,
+                                                           const int64_t* __restrict__ koff,
+                                                           const uint32_t* __restrict__ blk_t, int64_t ktot,
                                                            const uint32_t* __restrict__ cap_base,
                                                            uint32_t* __restrict__ fill, uint64_t* __restrict__ pairs,
                                                            uint32_t* __restrict__ ovf_cnt, uint64_t* __restrict__ ovf) {
   extern __shared__ uint32_t h[];  // the block's super-tile range (dynamic, <= kDecMaxSuper)
-  __shared__ int s_t[2];
+  __shared__ int64_t s_koff[kDecWin + 1];
   const int64_t j0 = (int64_t)blockIdx.x * kDecChunk, j1 = min(j0 + kDecChunk, ktot);
-  if (threadIdx.x == 0) {
-    s_t[0] = dec_tensor_of(koff, 0, nt - 1, j0);
-    s_t[1] = dec_tensor_of(koff, s_t[0], nt - 1, j1 - 1);
-  }
-  __syncthreads();
-  const int tf = s_t[0], tl = s_t[1];
+  const int tf = (int)blk_t[2 * blockIdx.x], tl = (int)blk_t[2 * blockIdx.x + 1];
+  const bool win = tl - tf < kDecWin;
+  if (tf != tl && win)
+    for (int i = threadIdx.x; i <= tl - tf; i += kThreads) s_koff[i] = koff[tf + i];
   const uint32_t s_lo = (uint32_t)(begins[tf] >> kDecSuperBits);
   const uint32_t nbin = (uint32_t)((begins[tl] + sizes[tl] - 1) >> kDecSuperBits) - s_lo + 1;
   for (uint32_t b = threadIdx.x; b < nbin; b += kThreads) h[b] = 0;
@@ -1444,13 +1474,45 @@ __global__ __launch_bounds__(kThreads) void topk_dec_place(const float* __restri
   }
   __syncthreads();  // h zeroed
   uint32_t rank[U];
+  if (tf == tl) {
+    const int64_t n = sizes[tf], b0 = begins[tf];
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t j = j0 + threadIdx.x + (int64_t)u * kThreads;
-    const int t = tf == tl ? tf : dec_tensor_of(koff, tf, tl, j);
-    const int64_t i = pos[u];
-    pos[u] = (j >= j1 || i < 0 || i >= sizes[t]) ? -1 : begins[t] + i;  // padding / out of range: skipped
-    rank[u] = pos[u] >= 0 ? atomicAdd(&h[(uint32_t)(pos[u] >> kDecSuperBits) - s_lo], 1u) : 0u;
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = j0 + threadIdx.x + (int64_t)u * kThreads;
+      const int64_t i = pos[u];
+      pos[u] = (j >= j1 || i < 0 || i >= n) ? -1 : b0 + i;  // padding / out of range: skipped
+      rank[u] = pos[u] >= 0 ? atomicAdd(&h[(uint32_t)(pos[u] >> kDecSuperBits) - s_lo], 1u) : 0u;
+    }
+  } else {
+    int tt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = min(j0 + threadIdx.x + (int64_t)u * kThreads, j1 - 1);
+      if (win) {  // koff[t] <= j < koff[t + 1], in LDS
+        int lo = 0, hi = tl - tf;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (s_koff[mid] <= j) lo = mid;
+          else hi = mid - 1;
+        }
+        tt[u] = tf + lo;
+      } else {
+        tt[u] = dec_tensor_of(koff, tf, tl, j);
+      }
+    }
+    int64_t n[U], b0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      n[u] = sizes[tt[u]];
+      b0[u] = begins[tt[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = j0 + threadIdx.x + (int64_t)u * kThreads;
+      const int64_t i = pos[u];
+      pos[u] = (j >= j1 || i < 0 || i >= n[u]) ? -1 : b0[u] + i;  // padding / out of range: skipped
+      rank[u] = pos[u] >= 0 ? atomicAdd(&h[(uint32_t)(pos[u] >> kDecSuperBits) - s_lo], 1u) : 0u;
+    }
   }
   __syncthreads();
   for (uint32_t b = threadIdx.x; b < nbin; b += kThreads)
@@ -2092,6 +2154,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
 struct DecTables {
   int64_t* koff = nullptr;
   uint32_t* cap_base = nullptr;
+  uint32_t* blk_t = nullptr;  // per place block: its first and last tensor
   int32_t nsuper = 0;
   uint64_t cap_total = 0;
 };
@@ -2108,8 +2171,10 @@ static int64_t decode_ktot(const omf_plan* plan, double ratio) {
 
 // Host computation of the tables (also sizes the workspace): bucket capacity = 2 x the
 // expected count of the super-tile (each tensor's k spread over its elements) + 256.
+static int64_t dec_place_blocks(int64_t ktot) { return std::max<int64_t>(1, (ktot + kDecChunk - 1) / kDecChunk); }
+
 static void dec_tables_host(const omf_plan* p, double ratio, std::vector<int64_t>& koff, std::vector<uint32_t>& cap_base,
-                            int32_t& nsuper) {
+                            int32_t& nsuper, std::vector<uint32_t>* blk_t = nullptr) {
   const std::vector<int64_t>& sizes = omf_plan_access::sizes(p);
   const int32_t nt = (int32_t)sizes.size();
   const int64_t ae = omf_plan_access::arena_end(p);
@@ -2131,6 +2196,19 @@ static void dec_tables_host(const omf_plan* p, double ratio, std::vector<int64_t
   for (int32_t q = 0; q < nsuper; ++q) {
     const uint64_t cap = std::min<uint64_t>((uint64_t)std::ceil(2.0 * expect[(size_t)q]) + 256, (uint64_t)1 << kDecSuperBits);
     cap_base[(size_t)q + 1] = cap_base[(size_t)q] + (uint32_t)cap;
+  }
+  if (blk_t) {  // the largest t with koff[t] <= j, as dec_tensor_of
+    const int64_t ktot = koff[(size_t)nt];
+    const int64_t nb = dec_place_blocks(ktot);
+    blk_t->assign(2 * (size_t)nb, 0);
+    auto tensor_of = [&](int64_t j) {
+      return (uint32_t)(std::upper_bound(koff.begin(), koff.begin() + nt, j) - koff.begin() - 1);
+    };
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t j0 = b * kDecChunk, j1 = std::max<int64_t>(std::min<int64_t>(j0 + kDecChunk, ktot), j0 + 1);
+      (*blk_t)[2 * (size_t)b] = tensor_of(j0);
+      (*blk_t)[2 * (size_t)b + 1] = tensor_of(j1 - 1);
+    }
   }
 }
 
@@ -2159,21 +2237,25 @@ static int dec_tables(omf_plan* p, double ratio, DecTables* out) {
   const int32_t nt = omf_plan_access::ntensors(p);
   const int64_t ae = omf_plan_access::arena_end(p);
   const int32_t nsuper = (int32_t)((ae + (1 << kDecSuperBits) - 1) >> kDecSuperBits);
-  const size_t bytes = align256(8 * ((size_t)nt + 1)) + 4 * ((size_t)nsuper + 1);
+  const int64_t nb = dec_place_blocks(decode_ktot(p, ratio));
+  const size_t o_cap = align256(8 * ((size_t)nt + 1)), o_blk = o_cap + align256(4 * ((size_t)nsuper + 1));
+  const size_t bytes = o_blk + 8 * (size_t)nb;
   bool fresh = false;
   uint64_t* host = nullptr;
   void* d = omf_plan_access::topk_table(p, ratio_key(ratio), bytes, &fresh, &host);
   if (!d) return fail(OMF_ENOMEM, "omf_topk_decode_arena: table allocation failed");
   out->koff = static_cast<int64_t*>(d);
-  out->cap_base = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d) + align256(8 * ((size_t)nt + 1)));
+  out->cap_base = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d) + o_cap);
+  out->blk_t = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d) + o_blk);
   out->nsuper = nsuper;
   if (fresh) {
     std::vector<int64_t> koff;
-    std::vector<uint32_t> cap_base;
+    std::vector<uint32_t> cap_base, blk_t;
     int32_t ns = 0;
-    dec_tables_host(p, ratio, koff, cap_base, ns);
+    dec_tables_host(p, ratio, koff, cap_base, ns, &blk_t);
     OMF_HIP(hipMemcpy(out->koff, koff.data(), 8 * koff.size(), hipMemcpyHostToDevice));
     OMF_HIP(hipMemcpy(out->cap_base, cap_base.data(), 4 * cap_base.size(), hipMemcpyHostToDevice));
+    OMF_HIP(hipMemcpy(out->blk_t, blk_t.data(), 4 * blk_t.size(), hipMemcpyHostToDevice));
     *host = cap_base.back();
   }
   out->cap_total = *host;
@@ -2223,10 +2305,10 @@ int omf_topk_decode_arena_ws(omf_plan* plan, double ratio, const float* values, 
     uint64_t* pairs = reinterpret_cast<uint64_t*>(w + d.pairs);
     uint64_t* ovf = reinterpret_cast<uint64_t*>(w + d.ovf);
     OMF_HIP(hipMemsetAsync(fill, 0, 4 * ((size_t)tb.nsuper + 1), st));
-    const dim3 gb((unsigned)std::max<int64_t>(1, (ktot + kDecChunk - 1) / kDecChunk));
+    const dim3 gb((unsigned)dec_place_blocks(ktot));
     hipLaunchKernelGGL(topk_dec_place, gb, dim3(kThreads), 4 * (size_t)tb.nsuper, st, values, indices,
                        omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (const int64_t*)tb.koff,
-                       (int)nt, ktot, (const uint32_t*)tb.cap_base, fill, pairs, ovf_cnt, ovf);
+                       (const uint32_t*)tb.blk_t, ktot, (const uint32_t*)tb.cap_base, fill, pairs, ovf_cnt, ovf);
     hipLaunchKernelGGL(topk_dec_tiles, dim3((unsigned)tb.nsuper), dim3(kDecTileThreads), 0, st, (const uint64_t*)pairs,
                        (const uint32_t*)tb.cap_base, (const uint32_t*)fill, y, ae);
     hipLaunchKernelGGL(topk_dec_overflow, dim3(64), dim3(kThreads), 0, st, (const uint32_t*)ovf_cnt,

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-3: bucket sort with batched loads (no load under a branch), 40 KiB LDS, bitonic rare path;
+# decode place blocks take their tensor range from a table (LDS search for multi-tensor blocks).
+set -o pipefail
+cd "$(dirname "$0")/.." && export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_topk_ps.py tests/test_gpu_r3.py tests/test_gpu_r2.py -x -q --timeout 200 \
+    --timeout-method thread -k "topk or Topk or TopK" > gpurun_out/r3n_tests.log 2>&1 || { tail -20 gpurun_out/r3n_tests.log; exit 1; }
+tail -1 gpurun_out/r3n_tests.log
+rm -rf gpurun_out/r3n_topk_prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r3n_topk_prof -o run -- \
+    python3 bench.py --codec topk --no-cpu-baseline --no-extras --steps 10 > gpurun_out/r3n_topk_prof.log 2>&1 || exit 3
+grep '^{' gpurun_out/r3n_topk_prof.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['ms_per_step'], d['roofline']['avg_launch_ms'], d['roofline']['decode_ms'])"

@@ -335,6 +335,32 @@ def test_topk_tiled_decode_matches_scatter(gpu):
     assert torch.equal(got2, _scatter_ref(plan, v2, ix, ks))
 
 
+@pytest.mark.parametrize("ntiny", [40, 700])
+def test_topk_tiled_decode_many_small_tensors(gpu, ntiny):
+    """A place block of the tiled decoder that spans many tensors finds each value's tensor by a
+    search of their first-value offsets — staged in LDS up to 512 tensors (40 tiny tensors), from
+    global memory beyond (700): both equal zeros + scatter, padding and out-of-range skipped."""
+    sizes = [100] * ntiny + [70001, 3, 250, 9000] + [100] * 5
+    plan = codec.Plan(sizes, device=gpu)
+    ratio = 0.01
+    ks = plan.topk_ks(ratio)
+    g = torch.Generator(device=gpu).manual_seed(31 + ntiny)
+    vals, idx = [], []
+    for t, (n, k) in enumerate(zip(sizes, ks)):
+        ix = torch.randperm(n, device=gpu, generator=g)[:k].to(torch.int64)
+        if t % 9 == 4:
+            ix[0] = -1  # padding
+        if t % 13 == 6:
+            ix[0] = n  # out of range
+        idx.append(ix)
+        vals.append(torch.randn(k, device=gpu, generator=g))
+    v, ix = torch.cat(vals), torch.cat(idx)
+    y = torch.full((plan.arena_end,), -3.0, device=gpu)
+    got = plan.topk_decode_arena(v, ix, ratio, y=y, mode=0)
+    torch.cuda.synchronize()
+    assert torch.equal(got, _scatter_ref(plan, v, ix, ks))
+
+
 def test_llama400m_topk_encode_then_tiled_decode(gpu):
     """Llama-400M, k = 1 %: the encoder's selection decoded by the tiled decoder equals zeros +
     scatter of the same (values, indices), over the whole arena."""
