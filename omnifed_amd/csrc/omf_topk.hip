@@ -1614,6 +1614,7 @@ struct HostSync {
   uint32_t seq = 0;
   hipStream_t side = nullptr;  // the pipeline's second stream (made on first use)
   hipEvent_t fork = nullptr, join = nullptr;
+  hipEvent_t fused[2] = {nullptr, nullptr};  // per stream: its latest group's streaming pass issued
 };
 
 // Wait for the verdict of call `seq`: spin on the mapped word (it lands as soon as the plan
@@ -1659,6 +1660,8 @@ int pipe_streams(HostSync* h) {
   OMF_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
   OMF_HIP(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
   OMF_HIP(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
+  OMF_HIP(hipEventCreateWithFlags(&h->fused[0], hipEventDisableTiming));
+  OMF_HIP(hipEventCreateWithFlags(&h->fused[1], hipEventDisableTiming));
   return OMF_OK;
 }
 
@@ -1674,10 +1677,10 @@ struct Group {
 };
 
 int topk_group_count(const omf_plan* p) {
-  // Off by default: measured on Llama-400M (scripts/exp/tk_pipe_sweep.py) the two streams'
-  // kernels do not overlap to any profit — 1.024 ms with one group, 1.036 / 1.139 / 1.328 ms
-  // with 2 / 4 / 8 (the concurrent streaming passes slow each other and every group adds its
-  // launches).  OMF_TOPK_GROUPS (experiments) turns it on.
+  // Off by default: measured on Llama-400M (scripts/exp/tk_env_ab.py) more groups only add time —
+  // 1.089 ms with one group, 1.156 / 1.192 / 1.266 ms with 2 / 3 / 4 (the latency-bound kernels
+  // do not shrink with their group, and their random stores slow the streaming pass beside them).
+  // OMF_TOPK_GROUPS (experiments) turns it on.
   const char* e = std::getenv("OMF_TOPK_GROUPS");
   int g = e ? std::atoi(e) : 1;
   if (omf_plan_access::arena_end(p) < ((int64_t)1 << 24)) g = 1;  // small arenas: launch-bound
@@ -2055,6 +2058,10 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
         OMF_HIP(hipEventRecord(hsync->fork, st));
         OMF_HIP(hipStreamWaitEvent(hsync->side, hsync->fork, 0));
       }
+      // The streaming passes run one after another: group g's waits for group g-1's (on the
+      // other stream), so that g-1's latency-bound tail (fine histogram, plan, bucket kernels)
+      // runs beside g's streaming pass rather than two passes sharing the memory system.
+      if (gi > 0) OMF_HIP(hipStreamWaitEvent(s, hsync->fused[(gi - 1) & 1], 0));
       const dim3 fgrid(G.nsub);
       if (residual_mode == 1)
         hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt,
@@ -2065,6 +2072,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       else
         hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt,
                            item_cnt, cand, G.sub0);
+      if (groups.size() > 1) OMF_HIP(hipEventRecord(hsync->fused[gi & 1], s));
       // fast path: exact fine-bin histograms, bucket plan
       const dim3 supgrid(G.nsup), supblk(1024);
       hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo, fmap,
