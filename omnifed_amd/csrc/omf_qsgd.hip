@@ -811,10 +811,9 @@ __device__ __forceinline__ bool spec_norm_wait(const SpecArgs& a, int32_t t, flo
 }
 
 // The finish launch: its first nfold workgroups fold the partials (spec_fold); the rest fix the
-// listed quads, one thread per listed-quad position (8 per wave slot, 7 used): (the slot
-// header), then (the quad's index, recorded x and draws, the block's item) with the tensor's
-// norm granule, then the exact level from the shared element math (Markstein division) and
-// its store.  A block whose tensor the fold marked bad (norm outside the bracket, a slot
+// listed quads, one thread per wave slot: (the slot header), then (the block's item) with the
+// tensor's norm granule, then per listed quad its index, recorded x and draws, the exact level
+// from the shared element math (Markstein division) and its store.  A block whose tensor the fold marked bad (norm outside the bracket, a slot
 // overflow, a deferred tensor) is requantised whole from x by its workgroup (the rare path).
 template <int WIDTH>
 __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const SpecFoldItem* __restrict__ fold_items,
@@ -827,17 +826,17 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
     if (!(a.dbg & 16u)) spec_fold(a, fold_items[blockIdx.x]);  // test hook: no fold, the fix waits expire
     return;
   }
-  constexpr int LPS = 8;                          // threads per wave slot
-  constexpr int SPW = kThreads / LPS;             // wave slots per workgroup (32)
-  constexpr int BPW = SPW / kWaves;               // blocks per workgroup (8)
+  // One thread per wave slot (its listed quads in turn: usually none or one), 64 blocks per
+  // workgroup: the fix is a few dependent round trips per thread, so its cost is the number of
+  // workgroup generations, not the quads (8 threads per slot took 8x the workgroups: +8-10 us).
+  constexpr int BPW = kThreads / kWaves;  // blocks per workgroup (64)
   __shared__ uint32_t s_rep[BPW];
   __shared__ float s_rep_norm[BPW];  // the granule's norm (norm_out is written in this launch)
   __shared__ uint32_t s_nrep;
   const EncArgs& e = a.e;
   const int64_t fb = (int64_t)blockIdx.x - nfold;
   if (threadIdx.x == 0) s_nrep = 0u;
-  const int64_t ws = fb * SPW + threadIdx.x / LPS;  // global wave slot
-  const int j = threadIdx.x & (LPS - 1);
+  const int64_t ws = fb * kThreads + threadIdx.x;  // global wave slot
   const int64_t blk = ws / kWaves;
   const int w = (int)(ws % kWaves);
   bool rep = false;
@@ -846,19 +845,19 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
     const uint32_t head = heads[ws];
     const uint32_t cnt = head & 0xffu;
     const int32_t t = (int32_t)(head >> 8);
-    const bool leader = w == 0 && j == 0;  // one status check per block
-    if (((uint32_t)j < cnt || leader) && !(a.dbg & 8u)) {
-      const uint32_t q = slots[blk * kSpecSlot + kSpecPerWave * w + j];
-      const float4* rec = recs + 2 * (ws * kSpecPerWave + j);
-      const float4 xr = rec[0], ur = rec[1];
+    const bool leader = w == 0;  // one status check per block
+    if ((cnt > 0u || leader) && !(a.dbg & 8u)) {
       const Item it = items[blk >> 2];
       float norm;
       bool bad;
       if (spec_norm_wait(a, t, norm, bad)) {
-        if ((uint32_t)j < cnt) {
-          const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
+        const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
+        const Divisor dv(norm);
+        for (uint32_t j = 0; j < cnt; ++j) {
+          const uint32_t q = slots[blk * kSpecSlot + kSpecPerWave * w + j];
+          const float4* rec = recs + 2 * (ws * kSpecPerWave + j);
           int32_t qq[4];
-          qsgd_quad<false>(xr, ur, Divisor(norm), e.levels, false, qq);
+          qsgd_quad<false>(rec[0], rec[1], dv, e.levels, false, qq);
           if (!(a.dbg & 4u)) store_quad<WIDTH>(e, 4 * (int64_t)q, end, qq);
         }
         rep = leader && bad;
@@ -2101,7 +2100,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
       return OMF_OK;
     }
     const int32_t nfold = (int32_t)p->n_spec_fold;
-    const dim3 gfin((unsigned)(nfold + (p->n_spec_blocks + 7) / 8));  // fix: 8 blocks per workgroup
+    const dim3 gfin((unsigned)(nfold + (p->n_spec_blocks + kThreads / kWaves - 1) / (kThreads / kWaves)));  // fix: 64 blocks per workgroup
     if (width == 1)
       hipLaunchKernelGGL(qsgd_spec_finish<1>, gfin, blk, 0, st, sa, (const SpecFoldItem*)sa.fold_items, nfold,
                          (const Item*)a.items, (const int64_t*)sa.begins, (const uint32_t*)sa.slots,
