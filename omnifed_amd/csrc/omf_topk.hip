@@ -14,7 +14,7 @@
 //                       tensor takes the bin whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of
 //                       the S samples as the threshold (below the k-th magnitude with ~6 sigma
 //                       of margin; tensors too small to sample keep every element), a "sure"
-//                       bin (above it with the same margin) and the fine-bin map.
+//                       bin (about the k-th magnitude, 1.5 sigma above) and the fine-bin map.
 //   2. topk_fused       ONE streaming pass: read x (+ residual), write the residual, append
 //                       every |t'| at or above the threshold as index << 32 | bits(t') to the
 //                       1 Ki-element sub-chunk's own range (one block scan, no atomics).
@@ -223,7 +223,8 @@ constexpr int kSRunsPerBlock = 512;
 // the threshold bin — the bin whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of the S samples
 // (0 = every element, for tensors too small to sample) — the "sure" bin, and the fine-bin map.
 // Also clears the tensor's redo histogram, its items' candidate counts and its fine bins.
-__device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, const int64_t* __restrict__ kk,
+__device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, float2 sure_zc,
+                                        const int64_t* __restrict__ kk,
                                         const uint32_t* __restrict__ tfirst, const uint32_t* __restrict__ tlast,
                                         uint32_t* __restrict__ tbin, uint32_t* __restrict__ hist,
                                         uint32_t* __restrict__ item_cnt, uint32_t* __restrict__ thi,
@@ -261,9 +262,10 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, con
       if (above < target && above + c[j] >= target) s_thr = PER * threadIdx.x + j;  // exactly one match
       above += c[j];
     }
-    // The "sure" bin: every bin from it up holds, with ~6 sigma of margin, fewer than k
-    // elements in total, so its elements are selected (the fused pass zeroes their residual).
-    const double sure = m - 6.0 * sqrt(m) - 32.0;
+    // The "sure" bin: every bin from it up holds, with a margin of sure_zc (1.5 sigma + 2 by
+    // default), fewer than k elements in total, so its elements are taken as selected (the fused
+    // pass zeroes their residual; the bucket kernels give a sure key past rank k its t' back).
+    const double sure = m - (double)sure_zc.x * sqrt(m) - (double)sure_zc.y;
     if (sure >= 1.0) {
       const uint32_t ts = (uint32_t)sure;
       above = above0;
@@ -333,7 +335,7 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ item_cnt,
                                                     uint32_t* __restrict__ thi, uint32_t* __restrict__ fmap,
                                                     uint32_t* __restrict__ tlo, uint32_t* __restrict__ fcount,
-                                                    uint32_t* __restrict__ fhist, uint32_t blk0) {
+                                                    uint32_t* __restrict__ fhist, uint32_t blk0, float2 sure_zc) {
   constexpr int U = kSRunsPerBlock / 256;  // runs per lane group, all loads in flight at once
   __shared__ uint32_t h[kSBins];
   __shared__ uint32_t s_last;
@@ -391,7 +393,7 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   if (!s_last) return;
   for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = atomicExch(&g[b], 0u);  // read + clear for the next call
   __syncthreads();
-  sample_threshold_tensor(t, n, h, kk, tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
+  sample_threshold_tensor(t, n, h, sure_zc, kk, tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
 }
 
 // Fine bin of a candidate magnitude (monotone in mag; below / above the mapped range clamp
@@ -518,7 +520,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
   const uint32_t lim = (uint32_t)(min(b + kSubPer, it.end) - b);
   const uint32_t o = 4u * threadIdx.x;
   // EF modes store t' - t' (0, or NaN for an infinite t') for the "sure" elements (bin >= hi:
-  // selected with ~6 sigma of margin) and t' for the rest; the bucket kernels then zero only
+  // taken as selected, sure_margin()) and t' for the rest; the bucket kernels then zero only
   // the selected keys below the sure bin (and restore a sure key that was not selected).
   float vv[4] = {0.f, 0.f, 0.f, 0.f};
   uint32_t selm = 0;
@@ -1867,6 +1869,20 @@ int64_t sample_max_runs() {
   return v >= 64 && v <= (1 << 20) ? (int64_t)v : (int64_t)kSMaxRuns;
 }
 
+// The "sure" bin's margin below the expected rank-k sample count m: m - z sqrt(m) - c (a
+// performance knob only: any sure bin gives the same selection — a sure key that is not selected
+// after all gets its t' back).  Every selected key below the sure bin costs the bucket sort a
+// random 4-byte residual store, every sure key past rank k one more: Llama-400M bucket sort 92 us
+// at (6, 32), 67 at (1.5, 2), 66 at (1, 0) (scripts/gpu_r3r.sh).  OMF_TOPK_SURE="z,c" overrides it.
+float2 sure_margin() {
+  float2 zc = make_float2(1.5f, 2.0f);
+  if (const char* e = std::getenv("OMF_TOPK_SURE")) {
+    float z = 0.f, c = 0.f;
+    if (std::sscanf(e, "%f,%f", &z, &c) == 2 && z >= 0.f && c >= 0.f) zc = make_float2(z, c);
+  }
+  return zc;
+}
+
 constexpr uint64_t kSetupTag = 0x5E7A9B1C00000000ull;
 
 int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uint32_t* status, SetupTable* out) {
@@ -2028,6 +2044,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   // the per-(plan, ratio) constant tables: made by topk_setup on the first call at this ratio
   SetupTable tb;
   const int64_t max_runs = sample_max_runs();
+  const float2 sure_zc = sure_margin();
   if (int r = setup_table(plan, ratio, max_runs, st, status, &tb)) return r;
   kk = tb.kk; koff = tb.koff; tfirst = tb.tfirst; tlast = tb.tlast; bbase = tb.bbase; kb2 = tb.kb2; sbase = tb.sbase;
   size_t tmp_bytes = L.tmp_bytes;
@@ -2048,11 +2065,11 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
         if (residual_mode == 1)
           hipLaunchKernelGGL((topk_sample<1>), dim3(G.nsb), sblk, 0, s, x, residual, alpha, d_begins, d_sizes,
                              (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin,
-                             hist, item_cnt, thi, fmap, tlo, fcount, fhist, G.sb0);
+                             hist, item_cnt, thi, fmap, tlo, fcount, fhist, G.sb0, sure_zc);
         else
           hipLaunchKernelGGL((topk_sample<0>), dim3(G.nsb), sblk, 0, s, x, residual, alpha, d_begins, d_sizes,
                              (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin,
-                             hist, item_cnt, thi, fmap, tlo, fcount, fhist, G.sb0);
+                             hist, item_cnt, thi, fmap, tlo, fcount, fhist, G.sb0, sure_zc);
       }
       if (gi == 0 && groups.size() > 1) {
         OMF_HIP(hipEventRecord(hsync->fork, st));

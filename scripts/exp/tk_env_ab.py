@@ -13,8 +13,9 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from omnifed_amd import codec, shapes  # noqa: E402
 
-var, vals_s = sys.argv[1].split("=")
-variants = vals_s.split(",")
+var, vals_s = sys.argv[1].split("=", 1)
+# variants separated by ',' (or by ';' when a value itself needs commas: write those as ':')
+variants = [v.replace(":", ",") for v in vals_s.split(";")] if ";" in vals_s else vals_s.split(",")
 rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 7
 dev = torch.device("cuda", 0)
 sizes = [shapes.numel(s) for _, s in shapes.model_shapes("llama400m")]

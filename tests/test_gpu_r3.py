@@ -408,6 +408,35 @@ def test_topk_group_pipeline_matches_one_group(gpu, monkeypatch, groups):
         assert torch.equal(ref_res, res)
 
 
+@pytest.mark.parametrize("sure", ["0,0", "0.5,0", "6,32", "40,0"])
+def test_topk_sure_margin_does_not_change_the_selection(gpu, monkeypatch, sure):
+    """The "sure" bin (keys whose residual the fused pass zeroes at once) is a performance knob:
+    with no margin about half the tensors take more sure keys than k (the bucket kernels give
+    those their t' back), with a huge one none is sure — values, indices and the residual over
+    three error-feedback calls equal the default's."""
+    sizes = [1_500_000, 4096, 3_000_017, 777_777, 65_536, 2_000_000, 300]
+    plan = codec.Plan(sizes, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(37)
+    xs = [torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3 for _ in range(3)]
+
+    def run():
+        res = torch.zeros(plan.arena_end, device=gpu)
+        outs = []
+        for i, x in enumerate(xs):
+            v, ix, _ = plan.topk_encode(x, 0.01, residual=res, residual_mode=2 if i == 0 else 1, alpha=2.0)
+            outs.append((v.clone(), ix.clone()))
+        torch.cuda.synchronize()
+        return outs, res
+
+    monkeypatch.delenv("OMF_TOPK_SURE", raising=False)
+    ref_outs, ref_res = run()
+    monkeypatch.setenv("OMF_TOPK_SURE", sure)
+    outs, res = run()
+    for (v0, i0), (v1, i1) in zip(ref_outs, outs):
+        assert torch.equal(v0, v1) and torch.equal(i0, i1)
+    assert torch.equal(ref_res, res)
+
+
 # ---------------------------------------------------------------- grid encoder (strategy 4)
 
 def _oracle_check(plan, x, q, norms, s, seed, off, alpha=1.0, tensors=None):
