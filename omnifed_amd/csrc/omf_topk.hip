@@ -247,10 +247,10 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, flo
   }();
   const double m = (double)kk[t] * (double)S / (double)max(n, (int64_t)1);
   const double want = m + 6.0 * sqrt(m) + 32.0;
-  __shared__ uint32_t s_thr, s_hi, s_min, s_max;
+  __shared__ uint32_t s_thr, s_hikey, s_min, s_max;
   if (threadIdx.x == 0) {
     s_thr = 0;
-    s_hi = kSBins;
+    s_hikey = 0x80000000u;  // above every magnitude key: nothing sure
     s_min = kSBins;
     s_max = 0;
   }
@@ -270,7 +270,13 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, flo
       const uint32_t ts = (uint32_t)sure;
       above = above0;
       for (int j = PER - 1; j >= 0; --j) {
-        if (above <= ts && above + c[j] > ts) s_hi = PER * threadIdx.x + j + 1;  // exactly one crossing
+        if (above <= ts && above + c[j] > ts) {  // exactly one crossing: bin b holds rank ts
+          // the sure magnitude inside bin b, interpolated linearly (magnitude is linear in the
+          // key bits within a bin): the top (ts - above) / c of the bin's samples are sure
+          const uint32_t b = PER * threadIdx.x + j;
+          const double f = (double)(ts - above) / (double)c[j];
+          s_hikey = ((b + 1u) << kSShift) - (uint32_t)(f * (double)(1u << kSShift));
+        }
         above += c[j];
       }
     }
@@ -317,7 +323,7 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, flo
   fmap[(size_t)t * kCoarse + threadIdx.x] = off | (rbits << 16);
   if (threadIdx.x == 0) {
     tbin[t] = thr;
-    thi[t] = max(s_hi, thr + 1);
+    thi[t] = max(s_hikey, (thr + 1u) << kSShift);  // a magnitude key: sure keys are candidates
     tlo[t] = lo;
     fcount[t] = F;
   }
@@ -519,7 +525,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
   const int64_t base = tbegin[it.tensor];
   const uint32_t lim = (uint32_t)(min(b + kSubPer, it.end) - b);
   const uint32_t o = 4u * threadIdx.x;
-  // EF modes store t' - t' (0, or NaN for an infinite t') for the "sure" elements (bin >= hi:
+  // EF modes store t' - t' (0, or NaN for an infinite t') for the "sure" elements (|t'| key >= hi:
   // taken as selected, sure_margin()) and t' for the rest; the bucket kernels then zero only
   // the selected keys below the sure bin (and restore a sure key that was not selected).
   float vv[4] = {0.f, 0.f, 0.f, 0.f};
@@ -547,7 +553,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
   if (MODE != 0) {
     float rr[4];
 #pragma unroll
-    for (int c = 0; c < 4; ++c) rr[c] = (mag_key(vv[c]) >> kSShift) >= hi ? __fsub_rn(vv[c], vv[c]) : vv[c];
+    for (int c = 0; c < 4; ++c) rr[c] = mag_key(vv[c]) >= hi ? __fsub_rn(vv[c], vv[c]) : vv[c];
     if (full) store_nt(r + b + o, make_float4(rr[0], rr[1], rr[2], rr[3]));
     else
       for (uint32_t c = 0; c < 4 && o + c < lim; ++c) r[b + o + c] = rr[c];
@@ -1124,7 +1130,7 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
       for (int u = 0; u < U; ++u) {
         if (e0 + (uint32_t)u * 1024 >= v.total) continue;
         if (j[u] < 0) {  // below the k-th key's bin: not selected (a "sure" key gets its t' back)
-          if (phase == 1 && r && (((uint32_t)key[u] & 0x7fffffffu) >> kSShift) >= hi)
+          if (phase == 1 && r && ((uint32_t)key[u] & 0x7fffffffu) >= hi)
             r[base + (key[u] >> 32)] = __uint_as_float((uint32_t)key[u]);
           continue;
         }
@@ -1308,7 +1314,7 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
     const uint32_t idx = (uint32_t)(sk >> 1) & 0x3ffffffu;
     if ((int64_t)idx >= n) continue;  // never expected (a padding key inside the bucket's count)
     const float v = __uint_as_float(((uint32_t)(sk & 1u) << 31) | (0x7fffffffu - (uint32_t)(sk >> 33)));
-    const bool sure = ((0x7fffffffu - (uint32_t)(sk >> 33)) >> kSShift) >= hi;
+    const bool sure = (0x7fffffffu - (uint32_t)(sk >> 33)) >= hi;
     if (rank < k) {
       values[o + rank] = v;
       indices[o + rank] = (int64_t)idx;
