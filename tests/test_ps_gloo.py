@@ -108,9 +108,9 @@ def _free_port():
     return p
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("mode", ["reduce", "gather"])
-def test_weighted_sum_world2(mode):
-    world = 2
+def test_weighted_sum_world2(mode, world):
     ctx = mp.get_context("spawn")
     qq = ctx.Queue()
     port = _free_port()
@@ -166,10 +166,11 @@ def _weighted_worker(rank, world, port, mode, q_out):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("mode", ["gather", "reduce"])
-def test_weighted_round_world2(mode):
-    """Σ_i decode(Q(w_i·x_i)) / Σ_i w_i over two ranks, the weights applied before encoding."""
-    world = 2
+def test_weighted_round_world2(mode, world):
+    """Σ_i decode(Q(w_i·x_i)) / Σ_i w_i over two and four ranks, the weights applied before
+    encoding: gather mode bit-exact in rank order, reduce mode within the any-order fp64 bound."""
     ctx = mp.get_context("spawn")
     qq = ctx.Queue()
     port = _free_port()
