@@ -25,7 +25,12 @@
  *  - Reentrant: no global mutable state.  A plan is driven by one host thread at
  *    a time; its stateful launches (encode, norms, fused PS step) may go to any
  *    stream: a launch on a different stream than the plan's previous one is
- *    ordered after it on the device (hipStreamWaitEvent), never run concurrently.
+ *    ordered after everything enqueued so far on that previous stream (an event
+ *    recorded there at the switch, hipStreamWaitEvent), never run concurrently.
+ *    The previous stream must therefore still exist when the plan moves to
+ *    another stream (PyTorch's pooled streams always do): before destroying the
+ *    stream of a plan's last stateful launch, call omf_plan_check on it (which
+ *    synchronises it and drops the plan's reference to it).
  *
  * Data layout ("update arena"): the named tensors of one client, flattened in
  * named_parameters() order into one fp32 buffer, tensor t occupying elements

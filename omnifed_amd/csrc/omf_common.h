@@ -11,6 +11,12 @@ namespace omf {
 constexpr int kThreads = 256;           // 4 wave64 per workgroup
 constexpr int kWaves = kThreads / 64;
 
+// Events that only order launches between streams of one device: no timing and no system-scope
+// fence.  Recording an event with the default system-scope release writes back and invalidates
+// the caches, and the next kernel on the stream started ~6 us later (rocprofv3 kernel trace, every
+// encode call of round 3); the kernels' own completion already releases at device scope.
+constexpr unsigned kOrderEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
+
 // Thread-local error string behind omf_last_error().
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);

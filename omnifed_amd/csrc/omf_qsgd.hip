@@ -1368,14 +1368,20 @@ struct omf_plan {
   bool last_valid = false;
 };
 
-// Order this launch after the plan's previous stateful launch when the stream changes.
+// Order this launch after the plan's previous stateful launch when the stream changes: the event is
+// recorded on the previous stream at the switch (it covers everything enqueued there so far, the
+// plan's launches included), not after every call — an event packet between two kernels of one
+// stream idled the GPU ~5 us per encode even without a system-scope fence (rocprofv3 kernel trace).
+// So the previous stream must still exist when the plan moves to another one (include/omf_codec.h).
 static int plan_enter(omf_plan* p, hipStream_t st) {
-  if (p->last_valid && p->last_stream != st) OMF_HIP(hipStreamWaitEvent(st, p->last_ev, 0));
+  if (p->last_valid && p->last_stream != st) {
+    if (!p->last_ev) OMF_HIP(hipEventCreateWithFlags(&p->last_ev, kOrderEventFlags));
+    OMF_HIP(hipEventRecord(p->last_ev, p->last_stream));
+    OMF_HIP(hipStreamWaitEvent(st, p->last_ev, 0));
+  }
   return OMF_OK;
 }
 static int plan_leave(omf_plan* p, hipStream_t st) {
-  if (!p->last_ev) OMF_HIP(hipEventCreateWithFlags(&p->last_ev, hipEventDisableTiming));
-  OMF_HIP(hipEventRecord(p->last_ev, st));
   p->last_stream = st;
   p->last_valid = true;
   return OMF_OK;
@@ -1954,6 +1960,9 @@ int omf_plan_check(omf_plan* plan, void* stream) {
   if (!plan) return fail(OMF_EINVAL, "omf_plan_check: plan is NULL");
   DeviceGuard g(plan->device);
   OMF_HIP(hipStreamSynchronize((hipStream_t)stream));
+  // the plan's launches on this stream are complete: a later call on another stream needs no
+  // ordering against it (and the stream may now be destroyed)
+  if (plan->last_valid && plan->last_stream == (hipStream_t)stream) plan->last_valid = false;
   uint32_t err = 0;
   OMF_HIP(hipMemcpy(&err, plan->d_sync + 4, 4, hipMemcpyDeviceToHost));
   if (err) OMF_HIP(hipMemset(plan->d_sync + 4, 0, 4));  // report each event once

@@ -1666,10 +1666,10 @@ HostSync* host_sync(int dev) {
 int pipe_streams(HostSync* h) {
   if (h->side) return OMF_OK;
   OMF_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-  OMF_HIP(hipEventCreateWithFlags(&h->fork, hipEventDisableTiming));
-  OMF_HIP(hipEventCreateWithFlags(&h->join, hipEventDisableTiming));
-  OMF_HIP(hipEventCreateWithFlags(&h->fused[0], hipEventDisableTiming));
-  OMF_HIP(hipEventCreateWithFlags(&h->fused[1], hipEventDisableTiming));
+  OMF_HIP(hipEventCreateWithFlags(&h->fork, kOrderEventFlags));
+  OMF_HIP(hipEventCreateWithFlags(&h->join, kOrderEventFlags));
+  OMF_HIP(hipEventCreateWithFlags(&h->fused[0], kOrderEventFlags));
+  OMF_HIP(hipEventCreateWithFlags(&h->fused[1], kOrderEventFlags));
   return OMF_OK;
 }
 
