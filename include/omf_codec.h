@@ -62,7 +62,7 @@ extern "C" {
 typedef struct omf_plan omf_plan;
 
 /* ABI version (major*100 + minor). */
-#define OMF_ABI_VERSION 104
+#define OMF_ABI_VERSION 105
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -301,7 +301,10 @@ int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, con
  * HBM as partial-line read-modify-writes).  Same bytes as omf_topk_decode_arena (indices unique
  * per tensor; the reference's zeros().scatter_ leaves a duplicate's last value, which neither
  * decoder promises).  The first call of a plan at a ratio uploads the plan's bucket tables
- * (synchronous, once).  Modes 1/2 and arenas over 2^30 elements ignore the workspace. */
+ * (synchronous, once).  Modes 1/2 and arenas over 2^30 elements ignore the workspace.
+ * The workspace must be zero-filled before its first use (its bucket counters); every call
+ * leaves them zero again, so it needs no clearing between calls (a workspace used by one call
+ * at a time: one per stream). */
 size_t omf_topk_decode_workspace_bytes(const omf_plan* plan, double ratio);
 int omf_topk_decode_arena_ws(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
                              int32_t mode, void* ws, size_t ws_bytes, void* stream);

@@ -75,7 +75,7 @@ class CodecError(RuntimeError):
     pass
 
 
-ABI_VERSION = 104  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+ABI_VERSION = 105  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
 
 
 def lib() -> ctypes.CDLL:

@@ -440,8 +440,8 @@ class Plan:
                 need = self._dec_need[key] = int(L.omf_topk_decode_workspace_bytes(self._h, key))
             with self._lock:
                 ws = self._dec_ws.get(st)
-                if ws is None or ws.numel() < need:
-                    ws = torch.empty(need, dtype=torch.uint8, device=dev)
+                if ws is None or ws.numel() < need:  # zero-filled once; every call leaves it so
+                    ws = torch.zeros(need, dtype=torch.uint8, device=dev)
                     self._dec_ws[st] = ws
                 check(L.omf_topk_decode_arena_ws(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), 0,
                                                  _ptr(ws), ctypes.c_size_t(ws.numel()), ctypes.c_void_p(st)),

@@ -1545,14 +1545,20 @@ __global__ __launch_bounds__(kThreads) void topk_dec_place(const float* __restri
 // 16-byte non-temporal stores (the arena's partial last sub-tile element by element).
 __global__ __launch_bounds__(kDecTileThreads) void topk_dec_tiles(const uint64_t* __restrict__ pairs,
                                                                   const uint32_t* __restrict__ cap_base,
-                                                                  const uint32_t* __restrict__ fill,
+                                                                  uint32_t* __restrict__ fill,
                                                                   float* __restrict__ y, int64_t arena_end) {
   __shared__ float4 tile[(1 << kDecSubBits) / 4];
   __shared__ uint64_t stage[kDecStage];
+  __shared__ uint32_t s_fill;
   float* tf = reinterpret_cast<float*>(tile);
   const uint32_t s = blockIdx.x;
   const uint32_t base = cap_base[s];
-  const uint32_t cnt = min(fill[s], cap_base[s + 1] - base);
+  if (threadIdx.x == 0) {  // read the bucket's count and leave it zero for the next call
+    s_fill = fill[s];
+    fill[s] = 0u;
+  }
+  __syncthreads();
+  const uint32_t cnt = min(s_fill, cap_base[s + 1] - base);
   const bool staged = cnt <= (uint32_t)kDecStage;
   const uint64_t* src = staged ? stage : pairs + base;
   if (staged)
@@ -1583,14 +1589,16 @@ __global__ __launch_bounds__(kDecTileThreads) void topk_dec_tiles(const uint64_t
   }
 }
 
-// The overflow list after the tiles (normally empty: one wave of each block reads the count).
-__global__ __launch_bounds__(kThreads) void topk_dec_overflow(const uint32_t* __restrict__ ovf_cnt,
+// The overflow list after the tiles (normally empty; one block), its count left zero for the next call.
+__global__ __launch_bounds__(kThreads) void topk_dec_overflow(uint32_t* __restrict__ ovf_cnt,
                                                               const uint64_t* __restrict__ ovf, float* __restrict__ y) {
   const uint32_t n = *ovf_cnt;
-  for (uint32_t j = blockIdx.x * kThreads + threadIdx.x; j < n; j += gridDim.x * kThreads) {
+  for (uint32_t j = threadIdx.x; j < n; j += kThreads) {
     const uint64_t pr = ovf[j];
     y[pr >> 32] = __uint_as_float((uint32_t)pr);
   }
+  __syncthreads();  // every thread has read the count
+  if (threadIdx.x == 0 && n) *ovf_cnt = 0u;
 }
 
 }  // namespace
@@ -2335,15 +2343,16 @@ int omf_topk_decode_arena_ws(omf_plan* plan, double ratio, const float* values, 
     uint32_t* ovf_cnt = fill + tb.nsuper;
     uint64_t* pairs = reinterpret_cast<uint64_t*>(w + d.pairs);
     uint64_t* ovf = reinterpret_cast<uint64_t*>(w + d.ovf);
-    OMF_HIP(hipMemsetAsync(fill, 0, 4 * ((size_t)tb.nsuper + 1), st));
+    // fill[] and the overflow count start at zero (a zero-filled workspace) and every call leaves
+    // them so: topk_dec_tiles clears its bucket's count, topk_dec_overflow the overflow count (a
+    // memset here was two fill kernels, ~10 us per decode)
     const dim3 gb((unsigned)dec_place_blocks(ktot));
     hipLaunchKernelGGL(topk_dec_place, gb, dim3(kThreads), 4 * (size_t)tb.nsuper, st, values, indices,
                        omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (const int64_t*)tb.koff,
                        (const uint32_t*)tb.blk_t, ktot, (const uint32_t*)tb.cap_base, fill, pairs, ovf_cnt, ovf);
     hipLaunchKernelGGL(topk_dec_tiles, dim3((unsigned)tb.nsuper), dim3(kDecTileThreads), 0, st, (const uint64_t*)pairs,
-                       (const uint32_t*)tb.cap_base, (const uint32_t*)fill, y, ae);
-    hipLaunchKernelGGL(topk_dec_overflow, dim3(64), dim3(kThreads), 0, st, (const uint32_t*)ovf_cnt,
-                       (const uint64_t*)ovf, y);
+                       (const uint32_t*)tb.cap_base, fill, y, ae);
+    hipLaunchKernelGGL(topk_dec_overflow, dim3(1), dim3(kThreads), 0, st, ovf_cnt, (const uint64_t*)ovf, y);
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }
