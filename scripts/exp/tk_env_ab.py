@@ -41,7 +41,9 @@ for v in variants:
     res.copy_(r0)
     enc(1)
     torch.cuda.synchronize()
-    outs[v] = (vals.clone(), idx.clone(), res.clone())
+    p.topk_decode_arena(vals, idx, 0.01, y=y, mode=0)
+    torch.cuda.synchronize()
+    outs[v] = (vals.clone(), idx.clone(), res.clone(), y.clone())
 same = all(all(torch.equal(a, b) for a, b in zip(outs[variants[0]], outs[v])) for v in variants[1:])
 print(json.dumps({"identical_outputs": same}), flush=True)
 del outs
