@@ -69,7 +69,10 @@ constexpr int kSortBits = 39;
 constexpr int kCoarse = 1024;         // coarse (sample-resolution) bins mapped per tensor
 constexpr int kFineMax = 16384;       // fine bins per tensor
 constexpr int kFineMaxBits = 18;      // a coarse bin splits by at most the rest of the mantissa
-constexpr int kFineMargin = 8;        // a fine bin expects <= kBucketHalf / 8 elements
+#ifndef OMF_FINE_MARGIN  // experiment builds may override it (scripts/exp/tk_margin_ab.sh)
+#define OMF_FINE_MARGIN 8
+#endif
+constexpr int kFineMargin = OMF_FINE_MARGIN;  // a fine bin expects <= kBucketHalf / 8 elements
 constexpr int kBucketHalf = 2048;
 constexpr int kBT = 512;              // bucket-sort block: 512 threads x 8 keys = 2 kBucketHalf
 constexpr int kBI = 8;
