@@ -220,7 +220,13 @@ __device__ __forceinline__ int64_t sample_stride(int64_t n, int64_t max_runs) {
 // (sample_threshold_tensor), so no second launch and no tail of one-block-per-tensor work
 // after the last sample.  smap: per block, (tensor, first run).  Block 0 also clears this
 // call's status words.
-constexpr int kSRunsPerBlock = 512;
+// 2 Ki runs per block = one block per tensor at the default sample size: its LDS histogram is the
+// tensor's, so it derives the threshold at once, with no global flush (Llama-400M: 54 -> 37 us
+// against 512 runs per block, scripts/exp/tk_sblock_ab.sh); larger samples still split.
+#ifndef OMF_SRUNS_PER_BLOCK  // experiment builds may override it
+#define OMF_SRUNS_PER_BLOCK 2048
+#endif
+constexpr int kSRunsPerBlock = OMF_SRUNS_PER_BLOCK;
 
 // The tensor's threshold from its sample histogram h (LDS, kSBins, loaded; 1024 threads):
 // the threshold bin — the bin whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of the S samples
@@ -383,6 +389,11 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
       if (rel[u] + c < n) atomicAdd(&h[mag_key(tprime<MODE>(xs[c], rs[c], alpha)) >> kSShift], 1u);
   }
   __syncthreads();
+  const uint32_t nblk = (uint32_t)((nr + kSRunsPerBlock - 1) / kSRunsPerBlock);
+  if (nblk == 1) {  // the tensor's whole sample is in this block's histogram (the usual case)
+    sample_threshold_tensor(t, n, h, sure_zc, kk, tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
+    return;
+  }
   uint32_t* g = gh + (size_t)t * kSBins;
   for (int b = threadIdx.x; b < kSBins; b += 1024)
     if (h[b]) atomicAdd(&g[b], h[b]);
@@ -393,7 +404,6 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   drain_vmem();
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t nblk = (uint32_t)((nr + kSRunsPerBlock - 1) / kSRunsPerBlock);
     const bool last = add_agent(&arrive[t], 1u) == nblk - 1;
     if (last) __hip_atomic_store(&arrive[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next call
     s_last = last ? 1u : 0u;
@@ -406,11 +416,8 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
 }
 
 // Fine bin of a candidate magnitude (monotone in mag; below / above the mapped range clamp
-// to the lowest / highest fine bin).
-// fine_bin plus the key's position inside its fine bin: the low `wbits` bits of |t'| (0 bits
-// for the clamped bottom / top bins).
-// Branch-free, so the map load is never under a branch (hipcc waits for a load issued under a
-// branch at the branch's end, which serialises the loads of an unrolled loop).
+// to the lowest / highest fine bin), and the key's position inside its fine bin: the low `wbits`
+// bits of |t'| (0 bits for the clamped bottom / top bins).
 // Bit arithmetic only (hipcc turns selects here into branches, and waits for a load issued under
 // a branch at the branch's end, which serialised the loads of the unrolled loops that call this):
 // out-of-range coarse bins go to fine bin 0 (below) or F - 1 (above) with no low bits.
