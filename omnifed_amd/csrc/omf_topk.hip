@@ -421,15 +421,26 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
 // Bit arithmetic only (hipcc turns selects here into branches, and waits for a load issued under
 // a branch at the branch's end, which serialised the loads of the unrolled loops that call this):
 // out-of-range coarse bins go to fine bin 0 (below) or F - 1 (above) with no low bits.
-__device__ __forceinline__ uint32_t fine_bin_pos(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t,
-                                                 uint32_t F, uint32_t& low, uint32_t& wbits) {
+__device__ __forceinline__ uint32_t fine_map_entry(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t) {
   const int c = (int)(mag >> kSShift) - (int)lo;
-  const uint32_t m = map_t[min(max(c, 0), kCoarse - 1)], r = m >> 16;
+  return map_t[min(max(c, 0), kCoarse - 1)];
+}
+
+// The fine bin from the coarse bin's map entry m (fine_map_entry).
+__device__ __forceinline__ uint32_t fine_bin_from(uint32_t mag, uint32_t lo, uint32_t m, uint32_t F, uint32_t& low,
+                                                  uint32_t& wbits) {
+  const int c = (int)(mag >> kSShift) - (int)lo;
+  const uint32_t r = m >> 16;
   const uint32_t below = (uint32_t)(c >> 31), above = (uint32_t)((kCoarse - 1 - c) >> 31);  // all ones or 0
   wbits = (kSShift - r) & ~(below | above);
   low = mag & ((1u << wbits) - 1u);
   const uint32_t fb = (m & 0xffffu) + ((mag >> (kSShift - r)) & ((1u << r) - 1u));
   return min((fb | above) & ~below, F - 1u);  // an in-range fine bin is < F
+}
+
+__device__ __forceinline__ uint32_t fine_bin_pos(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t,
+                                                 uint32_t F, uint32_t& low, uint32_t& wbits) {
+  return fine_bin_from(mag, lo, fine_map_entry(mag, lo, map_t), F, low, wbits);
 }
 
 __device__ __forceinline__ uint32_t fine_bin(uint32_t mag, uint32_t lo, const uint32_t* __restrict__ map_t,
@@ -1169,7 +1180,10 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
 // sorted instead.  Sort key: (2^31-1-|t'|bits) << 33 | index << 1 | sign.
 constexpr int kSubBins = kBT * kBI;  // 4096
 constexpr uint32_t kMaxRun = 32;
-__global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void topk_bucket_sort(const uint64_t* __restrict__ bkeys,
+#ifndef OMF_SORT_WAVES  // waves per SIMD the bucket sort is compiled for (experiment builds may override)
+#define OMF_SORT_WAVES 6
+#endif
+__global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(OMF_SORT_WAVES))) void topk_bucket_sort(const uint64_t* __restrict__ bkeys,
                                                              const BucketRec* __restrict__ brec,
                                                              const int64_t* __restrict__ kk,
                                                              const int64_t* __restrict__ koff,
@@ -1213,18 +1227,22 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
   // keys (past the count: the last key again), their fine bins' maps, the bins' counts and ranks.
   uint64_t keys[kBI];
   uint32_t meta[kBI];  // sub-bin << 16 | slot in it (0xffffffff: no key)
-  uint32_t low[kBI], wb[kBI], fbin[kBI];
+  uint32_t mv[kBI];  // each key's coarse-bin map entry (its fine bin and low bits follow from it)
 #pragma unroll
   for (int j = 0; j < kBI; ++j) keys[j] = src[min(threadIdx.x + (uint32_t)j * kBT, cnt - 1u)];  // striped
 #pragma unroll
   for (int j = 0; j < kBI; ++j) asm volatile("" : "+v"(keys[j]));
 #pragma unroll
-  for (int j = 0; j < kBI; ++j) fbin[j] = fine_bin_pos((uint32_t)keys[j] & 0x7fffffffu, lo, map_t, F, low[j], wb[j]);
+  for (int j = 0; j < kBI; ++j) mv[j] = fine_map_entry((uint32_t)keys[j] & 0x7fffffffu, lo, map_t);
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) asm volatile("" : "+v"(mv[j]));
   uint32_t cbv[kBI], sev[kBI];
 #pragma unroll
   for (int j = 0; j < kBI; ++j) {
-    cbv[j] = h_t[fbin[j]];
-    sev[j] = se_t[fbin[j]];
+    uint32_t low, wb;
+    const uint32_t fb = fine_bin_from((uint32_t)keys[j] & 0x7fffffffu, lo, mv[j], F, low, wb);
+    cbv[j] = h_t[fb];
+    sev[j] = se_t[fb];
   }
 #pragma unroll
   for (int j = 0; j < kBI; ++j) asm volatile("" : "+v"(cbv[j]), "+v"(sev[j]));  // loaded here, not sunk under e < cnt
@@ -1233,7 +1251,9 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(6))) void t
     const uint32_t e = threadIdx.x + (uint32_t)j * kBT;
     const uint32_t cb = cbv[j], rel = sev[j] - st;
     const uint32_t bits = (uint32_t)keys[j], mag = bits & 0x7fffffffu;
-    const uint32_t in = cb - 1u - (uint32_t)(((uint64_t)low[j] * cb) >> wb[j]);
+    uint32_t low, wb;
+    (void)fine_bin_from(mag, lo, mv[j], F, low, wb);
+    const uint32_t in = cb - 1u - (uint32_t)(((uint64_t)low * cb) >> wb);
     meta[j] = e < cnt ? min(rel + in, cnt - 1u) : 0xffffffffu;
     keys[j] = e < cnt ? ((uint64_t)(0x7fffffffu - mag) << 33) | ((keys[j] >> 32) << 1) | (uint64_t)(bits >> 31) : ~0ull;
   }

@@ -408,12 +408,16 @@ def test_topk_group_pipeline_matches_one_group(gpu, monkeypatch, groups):
         assert torch.equal(ref_res, res)
 
 
-@pytest.mark.parametrize("sure", ["0,0", "0.5,0", "6,32", "40,0"])
-def test_topk_sure_margin_does_not_change_the_selection(gpu, monkeypatch, sure):
+@pytest.mark.parametrize("knob,value", [("OMF_TOPK_SURE", "0,0"), ("OMF_TOPK_SURE", "0.5,0"),
+                                        ("OMF_TOPK_SURE", "6,32"), ("OMF_TOPK_SURE", "40,0"),
+                                        ("OMF_TOPK_SAMPLE_RUNS", "4096"), ("OMF_TOPK_SAMPLE_RUNS", "512")])
+def test_topk_sure_margin_does_not_change_the_selection(gpu, monkeypatch, knob, value):
     """The "sure" bin (keys whose residual the fused pass zeroes at once) is a performance knob:
     with no margin about half the tensors take more sure keys than k (the bucket kernels give
     those their t' back), with a huge one none is sure — values, indices and the residual over
-    three error-feedback calls equal the default's."""
+    three error-feedback calls equal the default's.  So does the sample size: 4 Ki runs per tensor
+    take two sample blocks that flush into the tensor's global histogram (the default 2 Ki is one
+    block deriving the threshold from its own), 512 a coarser threshold."""
     sizes = [1_500_000, 4096, 3_000_017, 777_777, 65_536, 2_000_000, 300]
     plan = codec.Plan(sizes, device=gpu)
     g = torch.Generator(device=gpu).manual_seed(37)
@@ -428,9 +432,9 @@ def test_topk_sure_margin_does_not_change_the_selection(gpu, monkeypatch, sure):
         torch.cuda.synchronize()
         return outs, res
 
-    monkeypatch.delenv("OMF_TOPK_SURE", raising=False)
+    monkeypatch.delenv(knob, raising=False)
     ref_outs, ref_res = run()
-    monkeypatch.setenv("OMF_TOPK_SURE", sure)
+    monkeypatch.setenv(knob, value)
     outs, res = run()
     for (v0, i0), (v1, i1) in zip(ref_outs, outs):
         assert torch.equal(v0, v1) and torch.equal(i0, i1)
