@@ -28,8 +28,9 @@ comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=
 targets = {n: torch.empty_like(t) for n, t in upd.items()}
 
 
-def tm(fn, reps=7):
-    fn()
+def tm(fn, reps=7, warm=3):
+    for _ in range(warm):  # steady state: the retained host memory and the copy threads warmed up
+        fn()
     torch.cuda.synchronize()
     ts = []
     for _ in range(reps):
