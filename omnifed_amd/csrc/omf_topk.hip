@@ -9,12 +9,13 @@
 // Passes (all tensors of a plan per launch; <= 256 tensors of <= 2^25 elements):
 //   1. topk_sample      one aligned 16-element run of t' per max(256, n/2048) elements
 //                       (hashed position; a random 64-byte sector costs the same as one
-//                       element), 512 runs per block, into an 8192-bin histogram of the top
-//                       13 bits of |t'| (exponent + 5 mantissa bits); the last block of each
-//                       tensor takes the bin whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of
+//                       element), up to 2 Ki runs per block (one block per tensor at the
+//                       default sample size), into an 8192-bin histogram of the top 13 bits of
+//                       |t'| (exponent + 5 mantissa bits); the tensor's block (or the last of
+//                       its blocks) takes the bin whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of
 //                       the S samples as the threshold (below the k-th magnitude with ~6 sigma
 //                       of margin; tensors too small to sample keep every element), a "sure"
-//                       bin (about the k-th magnitude, 1.5 sigma above) and the fine-bin map.
+//                       magnitude (about the k-th, 1.5 sigma above) and the fine-bin map.
 //   2. topk_fused       ONE streaming pass: read x (+ residual), write the residual, append
 //                       every |t'| at or above the threshold as index << 32 | bits(t') to the
 //                       1 Ki-element sub-chunk's own range (one block scan, no atomics).
@@ -27,7 +28,8 @@
 //                       of (index << 39 | tensor << 31 | 2^31-1 - |t'|bits), a gather.
 // Larger plans take the exact path (histogram of every t', collection, a segmented
 // descending sort of (|t'|bits << 32 | ~index) per tensor).
-// Decode is a scatter (mode 0 zero-fill, 1 overlay, 2 scatter-add).
+// Decode is a scatter (mode 0 zero-fill, 1 overlay, 2 scatter-add); the arena zero-fill decode
+// with a workspace is tiled (topk_dec_place / topk_dec_tiles / topk_dec_overflow).
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -1459,12 +1461,18 @@ __global__ __launch_bounds__(kThreads) void topk_scatter_arena(const float* __re
 // each 8 Ki-element sub-tile in LDS (zeros + its values) and streams it out with 16-byte
 // non-temporal stores; a last kernel applies the (normally empty) overflow list.
 constexpr int kDecSuperBits = 16;
-constexpr int kDecSubBits = 13;
+#ifndef OMF_DEC_SUB_BITS  // experiment builds may override it (scripts/exp/tk_dec_ab.sh)
+#define OMF_DEC_SUB_BITS 13
+#endif
+constexpr int kDecSubBits = OMF_DEC_SUB_BITS;
 constexpr int kDecSubs = 1 << (kDecSuperBits - kDecSubBits);
 constexpr int kDecMaxSuper = 16384;  // LDS bins of a place block (arenas <= 2^30 elements)
 constexpr int kDecChunk = 4096;      // selected values per place block
 constexpr int kDecTileThreads = 512;
-constexpr int kDecStage = 2048;      // bucket entries a tile workgroup stages in LDS (more: read from L2)
+#ifndef OMF_DEC_STAGE
+#define OMF_DEC_STAGE 2048
+#endif
+constexpr int kDecStage = OMF_DEC_STAGE;  // bucket entries a tile workgroup stages in LDS (more: read from L2)
 
 __device__ __forceinline__ int dec_tensor_of(const int64_t* __restrict__ koff, int lo, int hi, int64_t j) {
   while (lo < hi) {  // koff[t] <= j < koff[t + 1]
