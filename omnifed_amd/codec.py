@@ -45,7 +45,14 @@ def packed_bits(levels: int) -> int:
     return (2 * levels).bit_length()
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def _stream(device: torch.device) -> int:
+    """The current stream's handle (the raw getter: ~0.1 us per call against ~2 us for
+    ``torch.cuda.current_stream(device).cuda_stream``, which builds a Stream object)."""
+    if _raw_stream is not None:
+        return _raw_stream(device.index)
     return torch.cuda.current_stream(device).cuda_stream
 
 
