@@ -44,7 +44,7 @@ def _assert_within_bound(got, terms, total):
     t64 = torch.stack([t.double() for t in terms])
     exact = t64.sum(0) / float(total)
     bound = weighted_sum_error_bound(t64.abs().sum(0), exact, len(terms), total)
-    err = (torch.from_numpy(np.asarray(got, np.float32)).double() - exact).abs()
+    err = (torch.from_numpy(np.array(got, np.float32)).double() - exact).abs()
     assert bool((err <= bound).all()), float((err - bound).max())
 
 
@@ -108,7 +108,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])  # 8: the driver's largest node, rehearsed on gloo
 @pytest.mark.parametrize("mode", ["reduce", "gather"])
 def test_weighted_sum_world2(mode, world):
     ctx = mp.get_context("spawn")
@@ -166,10 +166,10 @@ def _weighted_worker(rank, world, port, mode, q_out):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("mode", ["gather", "reduce"])
 def test_weighted_round_world2(mode, world):
-    """Σ_i decode(Q(w_i·x_i)) / Σ_i w_i over two and four ranks, the weights applied before
+    """Σ_i decode(Q(w_i·x_i)) / Σ_i w_i over two, four and eight ranks, the weights applied before
     encoding: gather mode bit-exact in rank order, reduce mode within the any-order fp64 bound."""
     ctx = mp.get_context("spawn")
     qq = ctx.Queue()
