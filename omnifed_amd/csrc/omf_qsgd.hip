@@ -1396,6 +1396,12 @@ const void* flat_items(const omf_plan* p, int64_t* n) {
 int32_t ntensors(const omf_plan* p) { return p->nt; }
 int device(const omf_plan* p) { return p->device; }
 int64_t arena_end(const omf_plan* p) { return p->arena_end; }
+// The decoder's block table (tensor id | bit 31 = the block lies inside it) and its block size.
+const uint32_t* dec_blocks(const omf_plan* p, int64_t* n, int64_t* block_elems) {
+  *n = p->n_dec_blocks;
+  *block_elems = kDecBlk;
+  return p->d_dec_binfo;
+}
 const int64_t* d_sizes(const omf_plan* p) { return p->d_sizes; }
 const int64_t* d_begins(const omf_plan* p) { return p->d_begins; }
 const std::vector<int64_t>& sizes(const omf_plan* p) { return p->sizes; }

@@ -74,69 +74,91 @@ __global__ __launch_bounds__(kThreads) void qsgd_pack(const void* __restrict__ q
   }
 }
 
-// Decode: each thread unpacks its 32 elements (b words), then the workgroup transposes
-// through LDS (33-word rows: conflict-free both ways) so the fp32 stores are lane-contiguous
-// 16-byte non-temporal stores, like qsgd_decode_flat's.
+// Decode over the arena, one workgroup per 8 Ki-element block (two blocks of the plan's 4 Ki
+// decoder table, omf_qsgd.hip qsgd_decode_arena): every lane's b packed words go out first, their
+// addresses depending on blockIdx only, with the block's tensor and norm as scalar loads in
+// flight (the item-indexed version waited for its item and norm, then walked its item pass by
+// pass: 0.38 ms on Llama-400M).  Each thread unpacks its 32 elements into LDS; the workgroup
+// transposes them (33-word rows: conflict-free both ways) so the fp32 stores are lane-contiguous
+// 16-byte non-temporal stores.  A block not inside one tensor finds each 32-element group's
+// tensor (offsets are multiples of 64: a group never spans two) and writes only its elements;
+// padding keeps what y held.
+constexpr int64_t kTableBlk = 4096;  // elements per decoder-table block (omf_qsgd.hip kDecBlk)
+
 template <int B, bool ACC, bool POW2>
 __global__ __launch_bounds__(kThreads) void qsgd_decode_packed(const uint32_t* __restrict__ packed,
-                                                               const Item* __restrict__ items,
-                                                               const float* __restrict__ norm, float* __restrict__ y,
-                                                               int32_t L, int32_t b_rt, float levels, float inv_levels) {
-  constexpr int G = 32 * kThreads;  // elements per pass
+                                                               const uint32_t* __restrict__ binfo, int64_t nbinfo,
+                                                               const float* __restrict__ norm,
+                                                               const int64_t* __restrict__ begins,
+                                                               const int64_t* __restrict__ sizes, int32_t nt,
+                                                               int64_t arena_end, float* __restrict__ y, int32_t L,
+                                                               int32_t b_rt, float levels, float inv_levels) {
+  constexpr int G = 32 * kThreads;  // elements per block
+  static_assert(G == 2 * kTableBlk, "two table blocks per workgroup");
   __shared__ float tile[kThreads * 33];
+  __shared__ int32_t s_lim[kThreads];
   const int b = B ? B : b_rt;
-  const Item it = items[blockIdx.x];
-  const float nrm = norm[it.tensor];
+  const int64_t base = (int64_t)blockIdx.x * G;
+  const int64_t e0 = base + 32 * (int64_t)threadIdx.x;
+  // unconditional loads, clamped to the packed arena's last group
+  const uint32_t* p = packed + min(e0 >> 5, (arena_end - 1) >> 5) * (int64_t)b;
+  uint32_t wd[B ? B : 32];
+  if (B) {
+#pragma unroll
+    for (int i = 0; i < (B ? B : 1); ++i) wd[i] = __builtin_nontemporal_load(p + i);
+  } else {
+    for (int i = 0; i < b; ++i) wd[i] = p[i];
+  }
+  const int64_t k0 = 2 * (int64_t)blockIdx.x;
+  const uint32_t i0 = binfo[k0];
+  const uint32_t i1 = k0 + 1 < nbinfo ? binfo[k0 + 1] : 0u;
+  const int32_t t0 = (int32_t)(i0 & 0x7fffffffu);
+  const bool whole = (i0 >> 31) && i1 == i0;  // both table blocks inside tensor t0
+  float nrm;
+  if (whole) {
+    nrm = norm[t0];
+  } else {
+    int32_t t = t0;  // the last tensor starting at or before the block
+    while (t + 1 < nt && e0 >= begins[t + 1]) ++t;
+    const int64_t lim = min((int64_t)32, begins[t] + sizes[t] - e0);
+    s_lim[threadIdx.x] = lim > 0 ? (int32_t)lim : 0;  // 0: padding, or past the arena
+    nrm = lim > 0 ? norm[t] : 0.0f;
+  }
   const uint64_t mask = (1ull << b) - 1ull;
-  for (int64_t base = it.begin; base < it.end; base += G) {
-    const int64_t e0 = base + 32 * (int64_t)threadIdx.x;
-    if (e0 < it.end) {
-      const uint32_t* p = packed + (e0 >> 5) * (int64_t)b;
-      uint32_t wd[B ? B : 32];
-      if (B) {
+  uint64_t acc = 0;
+  int nb = 0, w = 0;
 #pragma unroll
-        for (int i = 0; i < (B ? B : 1); ++i) wd[i] = p[i];  // every word up front
-      } else {
-        for (int i = 0; i < b; ++i) wd[i] = p[i];
-      }
-      uint64_t acc = 0;
-      int nb = 0, w = 0;
-#pragma unroll
-      for (int i = 0; i < 32; ++i) {
-        if (nb < b) {
-          acc |= (uint64_t)wd[w++] << nb;
-          nb += 32;
-        }
-        const int32_t qi = (int32_t)(acc & mask) - L;
-        acc >>= b;
-        nb -= b;
-        const float nq = __fmul_rn(nrm, (float)qi);  // qsgd_decode_flat's arithmetic
-        tile[threadIdx.x * 33 + i] = POW2 ? __fmul_rn(nq, inv_levels) : nq / levels;
-      }
+  for (int i = 0; i < 32; ++i) {
+    if (nb < b) {
+      acc |= (uint64_t)wd[w++] << nb;
+      nb += 32;
     }
-    __syncthreads();
-    const int64_t lim = min((int64_t)G, it.end - base);
+    const int32_t qi = (int32_t)(acc & mask) - L;
+    acc >>= b;
+    nb -= b;
+    const float nq = __fmul_rn(nrm, (float)qi);  // qsgd_decode_arena's arithmetic
+    tile[threadIdx.x * 33 + i] = POW2 ? __fmul_rn(nq, inv_levels) : nq / levels;
+  }
+  __syncthreads();
 #pragma unroll
-    for (int v = 0; v < 8; ++v) {
-      const int e = 4 * (v * kThreads + (int)threadIdx.x);  // element of this pass
-      if (e >= lim) continue;
-      float f[4];
+  for (int v = 0; v < 8; ++v) {
+    const int e = 4 * (v * kThreads + (int)threadIdx.x);  // element of this block
+    float f[4];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) f[c] = tile[((e + c) >> 5) * 33 + ((e + c) & 31)];
-      float* yo = y + base + e;
-      if (e + 4 <= lim) {
-        float4 o = make_float4(f[0], f[1], f[2], f[3]);
-        if (ACC) {
-          const float4 prev = *reinterpret_cast<const float4*>(yo);
-          o.x = __fadd_rn(prev.x, o.x); o.y = __fadd_rn(prev.y, o.y);
-          o.z = __fadd_rn(prev.z, o.z); o.w = __fadd_rn(prev.w, o.w);
-        }
-        store_nt(yo, o);
-      } else {
-        for (int c = 0; c < 4 && e + c < lim; ++c) yo[c] = ACC ? __fadd_rn(yo[c], f[c]) : f[c];
+    for (int c = 0; c < 4; ++c) f[c] = tile[((e + c) >> 5) * 33 + ((e + c) & 31)];
+    float* yo = y + base + e;
+    const int l = whole ? 4 : s_lim[e >> 5] - (e & 31);  // elements of the quad to write
+    if (l >= 4) {
+      float4 o = make_float4(f[0], f[1], f[2], f[3]);
+      if (ACC) {
+        const f32x4_t pv = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(yo));
+        o.x = __fadd_rn(pv[0], o.x); o.y = __fadd_rn(pv[1], o.y);
+        o.z = __fadd_rn(pv[2], o.z); o.w = __fadd_rn(pv[3], o.w);
       }
+      store_nt(yo, o);
+    } else {
+      for (int c = 0; c < l; ++c) yo[c] = ACC ? __fadd_rn(yo[c], f[c]) : f[c];
     }
-    __syncthreads();  // the tile is rewritten by the next pass
   }
 }
 
@@ -162,10 +184,12 @@ void dispatch_pack(int b, dim3 g, hipStream_t st, const void* q, const Item* ite
 }
 
 template <bool ACC, bool POW2>
-void dispatch_decode(int b, dim3 g, hipStream_t st, const uint32_t* packed, const Item* items, const float* norm,
+void dispatch_decode(int b, dim3 g, hipStream_t st, const uint32_t* packed, const uint32_t* binfo, int64_t nbinfo,
+                     const float* norm, const int64_t* begins, const int64_t* sizes, int32_t nt, int64_t arena_end,
                      float* y, int32_t L, float levels, float inv) {
-#define OMF_DP(BB) \
-  hipLaunchKernelGGL((qsgd_decode_packed<BB, ACC, POW2>), g, dim3(kThreads), 0, st, packed, items, norm, y, L, b, levels, inv)
+#define OMF_DP(BB)                                                                                              \
+  hipLaunchKernelGGL((qsgd_decode_packed<BB, ACC, POW2>), g, dim3(kThreads), 0, st, packed, binfo, nbinfo, norm, \
+                     begins, sizes, nt, arena_end, y, L, b, levels, inv)
   switch (b) {
     case 2: OMF_DP(2); break;
     case 3: OMF_DP(3); break;
@@ -186,6 +210,11 @@ void dispatch_decode(int b, dim3 g, hipStream_t st, const uint32_t* packed, cons
 namespace omf_plan_access {
 const void* flat_items(const omf_plan* p, int64_t* n);
 int device(const omf_plan* p);
+int32_t ntensors(const omf_plan* p);
+int64_t arena_end(const omf_plan* p);
+const int64_t* d_sizes(const omf_plan* p);
+const int64_t* d_begins(const omf_plan* p);
+const uint32_t* dec_blocks(const omf_plan* p, int64_t* n, int64_t* block_elems);
 }  // namespace omf_plan_access
 
 extern "C" {
@@ -229,19 +258,26 @@ int omf_qsgd_decode_packed(omf_plan* plan, const uint32_t* packed, int32_t level
   DeviceGuard g(omf_plan_access::device(plan));
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   int64_t n_items = 0;
-  const Item* items = static_cast<const Item*>(omf_plan_access::flat_items(plan, &n_items));
-  if (n_items == 0) return OMF_OK;
-  const dim3 grid((unsigned)n_items);
+  (void)omf_plan_access::flat_items(plan, &n_items);
+  if (n_items == 0) return OMF_OK;  // no element to decode
+  int64_t nbinfo = 0, tblk = 0;
+  const uint32_t* binfo = omf_plan_access::dec_blocks(plan, &nbinfo, &tblk);
+  if (tblk != kTableBlk) return fail(OMF_EINVAL, "omf_qsgd_decode_packed: decoder table block size mismatch (library build)");
+  const int64_t end = omf_plan_access::arena_end(plan);
+  const dim3 grid((unsigned)((end + 2 * kTableBlk - 1) / (2 * kTableBlk)));
   hipStream_t st = (hipStream_t)stream;
   const bool pow2 = (levels & (levels - 1)) == 0;
   const float lv = (float)levels, inv = pow2 ? 1.0f / (float)levels : 0.0f;
+  const int64_t* bg = omf_plan_access::d_begins(plan);
+  const int64_t* sz = omf_plan_access::d_sizes(plan);
+  const int32_t nt = omf_plan_access::ntensors(plan);
+#define OMF_DD(A, P) dispatch_decode<A, P>(b, grid, st, packed, binfo, nbinfo, norm, bg, sz, nt, end, y, levels, lv, inv)
   if (accumulate) {
-    if (pow2) dispatch_decode<true, true>(b, grid, st, packed, items, norm, y, levels, lv, inv);
-    else dispatch_decode<true, false>(b, grid, st, packed, items, norm, y, levels, lv, inv);
+    if (pow2) OMF_DD(true, true); else OMF_DD(true, false);
   } else {
-    if (pow2) dispatch_decode<false, true>(b, grid, st, packed, items, norm, y, levels, lv, inv);
-    else dispatch_decode<false, false>(b, grid, st, packed, items, norm, y, levels, lv, inv);
+    if (pow2) OMF_DD(false, true); else OMF_DD(false, false);
   }
+#undef OMF_DD
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }

@@ -99,3 +99,31 @@ def test_packed_wire_is_smaller(gpu):
         packed = encode_updates_dict(upd, build_global_compressor(enabled=True, scheme="qsgd", bit_width=bits,
                                                                   device=gpu, packed_wire=True))
         assert len(packed[0].values_data) == int(len(plain[0].values_data) * ratio)
+
+
+@pytest.mark.parametrize("levels", [5, 16, 100000])  # non-power-of-two, int8 s = 4, runtime width
+def test_packed_decode_many_tensors_keeps_padding(gpu, levels):
+    """The arena-indexed packed decoder on many small and ragged tensors (blocks that cross
+    tensor boundaries, tensors shorter than a group, a partial last group): bit-identical to
+    the int8/int32 decode on every tensor, and the arena padding keeps what y held, plain and
+    accumulating."""
+    rng = np.random.default_rng(levels)
+    sizes = [int(v) for v in rng.integers(1, 300, 150)] + [8192, 8191, 40000, 33, 1 << 16, 97]
+    plan = codec.Plan(sizes, device=gpu)
+    width = codec.storage_width(levels)
+    qt = torch.int8 if width == 8 else torch.int32
+    q = torch.from_numpy(rng.integers(-levels, levels + 1, plan.arena_end)).to(qt).to(gpu)
+    norms = torch.from_numpy(rng.random(plan.nt, dtype=np.float32) + 0.5).to(gpu)
+    packed = plan.qsgd_pack(q, width, levels)
+    pad = torch.ones(plan.arena_end, dtype=torch.bool)
+    for o, n in zip(plan.offsets, plan.sizes):
+        pad[o:o + n] = False
+    pad = pad.to(gpu)
+    y_ref = plan.qsgd_decode(q, width, levels, norms, y_out=torch.full((plan.arena_end,), 7.0, device=gpu))
+    for accumulate in (False, True):
+        y = torch.full((plan.arena_end,), 7.0, device=gpu)
+        plan.qsgd_decode_packed(packed, levels, norms, y_out=y, accumulate=accumulate)
+        want = y_ref + 7.0 if accumulate else y_ref
+        for o, n in zip(plan.offsets, plan.sizes):
+            assert torch.equal(y[o:o + n], want[o:o + n]), (levels, accumulate, n)
+        assert bool((y[pad] == 7.0).all()), (levels, accumulate)
