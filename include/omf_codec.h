@@ -232,8 +232,10 @@ int omf_div_f32(float* y, int64_t n, float divisor, void* stream);
  * Level q in [-L, L] -> code q + L in b = omf_qsgd_packed_bits(L) = ceil(log2(2L+1))
  * bits, LSB-first: element i of a tensor at bits [i*b, (i+1)*b) of its stream; tensor t's
  * stream starts at 32-bit word offsets[t] * b / 32 of the packed arena, ceil(arena_end / 32) * b
- * words (the plan's offsets are multiples of 64; 32 elements = b words, the last partial
- * group of a tensor included, its padding packed as code 0).
+ * words (32 elements = b words, the last partial group of a tensor included, its padding
+ * packed as code 0; groups of arena padding are neither written nor decoded).  Both calls
+ * need every tensor offset to be a multiple of 32 elements (OMF_EINVAL otherwise; the
+ * Python arena_layout's are multiples of 64).
  * omf_qsgd_pack: payload (width 8 or 32, as omf_qsgd_encode wrote it) -> packed arena.
  * omf_qsgd_decode_packed: y = fl32(fl32(norm * (code - L)) / L), bit-identical to
  * omf_qsgd_decode of the unpacked payload (accumulate: y += that).

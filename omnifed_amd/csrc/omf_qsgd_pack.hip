@@ -6,12 +6,14 @@
 // b = ceil(log2(2L + 1)) bits (s = 4: 6 bits instead of 8; s = 8: 10 instead of 32),
 // LSB-first little-endian: element i of a tensor occupies bits [i*b, (i+1)*b) of the
 // tensor's stream.  In a plan's packed arena, tensor t's stream starts at 32-bit word
-// offset_t * b / 32 (arena offsets are multiples of 64 elements, so this is exact), so 32
-// consecutive elements are exactly b words and one thread packs or unpacks them alone.
+// offset_t * b / 32 (the offsets must be multiples of 32 elements, else OMF_EINVAL;
+// arena_layout's are multiples of 64), so 32 consecutive elements are exactly b words, lie in
+// one tensor, and one thread packs or unpacks them alone.
 // Decoding the codes gives the same floats as decoding the levels (qsgd_decode_flat's
 // arithmetic: fl32(fl32(norm * q) / L)).
 #include <algorithm>
 #include <cstdint>
+#include <vector>
 
 #include "../../include/omf_codec.h"
 #include "omf_common.h"
@@ -20,57 +22,99 @@ using namespace omf;
 
 namespace {
 
-struct Item {  // the plan's flat items (omf_qsgd.hip): 16 Ki-element sub-chunks
-  int64_t begin, end;
-  int32_t tensor, kind, chunk, pad;
-};
+constexpr int64_t kTableBlk = 4096;  // elements per decoder-table block (omf_qsgd.hip kDecBlk)
+constexpr int kGroupBlk = 32 * kThreads;  // elements per workgroup of the pack and the decode
+static_assert(kGroupBlk == 2 * kTableBlk, "two table blocks per workgroup");
 
+// A thread's 32-element group: the whole workgroup inside one tensor (both table blocks marked
+// inside the same tensor), or the group's own tensor found from the block's first one (offsets
+// are multiples of 32: a group never spans two tensors).  Returns the elements of the group in
+// its tensor (0 = padding, or past the arena) and that tensor.
+__device__ __forceinline__ int group_tensor(const uint32_t* __restrict__ binfo, int64_t nbinfo,
+                                            const int64_t* __restrict__ begins, const int64_t* __restrict__ sizes,
+                                            int32_t nt, int64_t e0, bool* whole, int32_t* tensor) {
+  const int64_t k0 = 2 * (int64_t)blockIdx.x;
+  const uint32_t i0 = binfo[k0];
+  const uint32_t i1 = k0 + 1 < nbinfo ? binfo[k0 + 1] : 0u;
+  int32_t t = (int32_t)(i0 & 0x7fffffffu);  // the last tensor starting at or before the block
+  *whole = (i0 >> 31) && i1 == i0;
+  if (*whole) {
+    *tensor = t;
+    return 32;
+  }
+  while (t + 1 < nt && e0 >= begins[t + 1]) ++t;
+  *tensor = t;
+  const int64_t lim = min((int64_t)32, begins[t] + sizes[t] - e0);
+  return lim > 0 ? (int)lim : 0;
+}
+
+// Pack over the arena, one workgroup per 8 Ki-element block: each thread packs its 32-element
+// group into b words.  The payload loads are issued before the block's table entry arrives,
+// clamped to the last whole group of the arena (a thread whose group is whole in its tensor
+// reads exactly its own elements); a group a tensor ends inside reloads its elements one by
+// one and packs code 0 after them; padding groups are not written.
 // B: compile-time code width (2..10, s = 0..8), or 0 = the runtime width b.
 template <int WIDTH, int B>
-__global__ __launch_bounds__(kThreads) void qsgd_pack(const void* __restrict__ q, const Item* __restrict__ items,
+__global__ __launch_bounds__(kThreads) void qsgd_pack(const void* __restrict__ q, const uint32_t* __restrict__ binfo,
+                                                      int64_t nbinfo, const int64_t* __restrict__ begins,
+                                                      const int64_t* __restrict__ sizes, int32_t nt, int64_t arena_end,
                                                       int32_t L, int32_t b_rt, uint32_t* __restrict__ out) {
   const int b = B ? B : b_rt;
-  const Item it = items[blockIdx.x];
-  for (int64_t e0 = it.begin + 32 * (int64_t)threadIdx.x; e0 < it.end; e0 += 32 * (int64_t)kThreads) {
-    const int nv = (int)min((int64_t)32, it.end - e0);
-    int32_t lv[32];
+  const int64_t e0 = (int64_t)blockIdx.x * kGroupBlk + 32 * (int64_t)threadIdx.x;
+  const int64_t qmax = ((arena_end >> 5) - 1) << 5;  // the last whole group (< 0: none)
+  const int64_t ec = max((int64_t)0, min(e0, qmax));
+  int32_t lv[32];
+  if (qmax >= 0) {  // uniform
     if (WIDTH == 1) {
-      const int8_t* q8 = static_cast<const int8_t*>(q) + e0;
-      if (nv == 32) {
-        const uint4 w0 = *reinterpret_cast<const uint4*>(q8), w1 = *reinterpret_cast<const uint4*>(q8 + 16);
-        const uint32_t w[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const int8_t* q8 = static_cast<const int8_t*>(q) + ec;
+      const i32x4_t w0 = *reinterpret_cast<const i32x4_t*>(q8);
+      const i32x4_t w1 = *reinterpret_cast<const i32x4_t*>(q8 + 16);
+      const uint32_t w[8] = {(uint32_t)w0[0], (uint32_t)w0[1], (uint32_t)w0[2], (uint32_t)w0[3],
+                             (uint32_t)w1[0], (uint32_t)w1[1], (uint32_t)w1[2], (uint32_t)w1[3]};
 #pragma unroll
-        for (int i = 0; i < 32; ++i) lv[i] = (int32_t)(int8_t)(w[i >> 2] >> (8 * (i & 3)));
-      } else {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) lv[i] = i < nv ? (int32_t)q8[i] : -L;
-      }
+      for (int i = 0; i < 32; ++i) lv[i] = (int32_t)(int8_t)(w[i >> 2] >> (8 * (i & 3)));
     } else {
-      const int32_t* q32 = static_cast<const int32_t*>(q) + e0;
-      if (nv == 32) {
+      const int32_t* q32 = static_cast<const int32_t*>(q) + ec;
 #pragma unroll
-        for (int v = 0; v < 8; ++v) {
-          const int4 w = *reinterpret_cast<const int4*>(q32 + 4 * v);
-          lv[4 * v] = w.x; lv[4 * v + 1] = w.y; lv[4 * v + 2] = w.z; lv[4 * v + 3] = w.w;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < 32; ++i) lv[i] = i < nv ? q32[i] : -L;
+      for (int v = 0; v < 8; ++v) {
+        const i32x4_t w = *reinterpret_cast<const i32x4_t*>(q32 + 4 * v);
+        lv[4 * v] = w[0]; lv[4 * v + 1] = w[1]; lv[4 * v + 2] = w[2]; lv[4 * v + 3] = w[3];
       }
     }
-    uint32_t* o = out + (e0 >> 5) * (int64_t)b;
-    uint64_t acc = 0;
-    int nb = 0, w = 0;
+  }
+  bool whole;
+  int32_t t;
+  const int nv = group_tensor(binfo, nbinfo, begins, sizes, nt, e0, &whole, &t);
+  if (nv == 0) return;
+  if (nv < 32) {  // the tensor ends inside this group (its elements only; codes 0 after them)
 #pragma unroll
-    for (int i = 0; i < 32; ++i) {
-      acc |= (uint64_t)(uint32_t)(lv[i] + L) << nb;  // padding (i >= nv) packs code 0
-      nb += b;
-      if (nb >= 32) {
-        o[w++] = (uint32_t)acc;
-        acc >>= 32;
-        nb -= 32;
-      }
+    for (int i = 0; i < 32; ++i)
+      lv[i] = i < nv ? (WIDTH == 1 ? (int32_t)(static_cast<const int8_t*>(q)[e0 + i])
+                                   : static_cast<const int32_t*>(q)[e0 + i])
+                     : -L;
+  }
+  uint32_t* o = out + (e0 >> 5) * (int64_t)b;
+  uint32_t wd[B ? B : 32];
+  uint64_t acc = 0;
+  int nb = 0, w = 0;
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    acc |= (uint64_t)(uint32_t)(lv[i] + L) << nb;
+    nb += b;
+    if (nb >= 32) {
+      if (B) wd[w++] = (uint32_t)acc;  // static index once unrolled
+      else o[w++] = (uint32_t)acc;     // runtime width: straight to memory
+      acc >>= 32;
+      nb -= 32;
     }
+  }
+  if (B && B % 2 == 0) {  // b words at a multiple of 8 bytes: 8-byte stores
+#pragma unroll
+    for (int i = 0; i < (B ? B : 2); i += 2)
+      *reinterpret_cast<uint2*>(o + i) = make_uint2(wd[i], wd[i + 1]);
+  } else if (B) {
+#pragma unroll
+    for (int i = 0; i < (B ? B : 1); ++i) o[i] = wd[i];
   }
 }
 
@@ -83,8 +127,6 @@ __global__ __launch_bounds__(kThreads) void qsgd_pack(const void* __restrict__ q
 // 16-byte non-temporal stores.  A block not inside one tensor finds each 32-element group's
 // tensor (offsets are multiples of 64: a group never spans two) and writes only its elements;
 // padding keeps what y held.
-constexpr int64_t kTableBlk = 4096;  // elements per decoder-table block (omf_qsgd.hip kDecBlk)
-
 template <int B, bool ACC, bool POW2>
 __global__ __launch_bounds__(kThreads) void qsgd_decode_packed(const uint32_t* __restrict__ packed,
                                                                const uint32_t* __restrict__ binfo, int64_t nbinfo,
@@ -93,8 +135,7 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_packed(const uint32_t* _
                                                                const int64_t* __restrict__ sizes, int32_t nt,
                                                                int64_t arena_end, float* __restrict__ y, int32_t L,
                                                                int32_t b_rt, float levels, float inv_levels) {
-  constexpr int G = 32 * kThreads;  // elements per block
-  static_assert(G == 2 * kTableBlk, "two table blocks per workgroup");
+  constexpr int G = kGroupBlk;
   __shared__ float tile[kThreads * 33];
   __shared__ int32_t s_lim[kThreads];
   const int b = B ? B : b_rt;
@@ -109,21 +150,11 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_packed(const uint32_t* _
   } else {
     for (int i = 0; i < b; ++i) wd[i] = p[i];
   }
-  const int64_t k0 = 2 * (int64_t)blockIdx.x;
-  const uint32_t i0 = binfo[k0];
-  const uint32_t i1 = k0 + 1 < nbinfo ? binfo[k0 + 1] : 0u;
-  const int32_t t0 = (int32_t)(i0 & 0x7fffffffu);
-  const bool whole = (i0 >> 31) && i1 == i0;  // both table blocks inside tensor t0
-  float nrm;
-  if (whole) {
-    nrm = norm[t0];
-  } else {
-    int32_t t = t0;  // the last tensor starting at or before the block
-    while (t + 1 < nt && e0 >= begins[t + 1]) ++t;
-    const int64_t lim = min((int64_t)32, begins[t] + sizes[t] - e0);
-    s_lim[threadIdx.x] = lim > 0 ? (int32_t)lim : 0;  // 0: padding, or past the arena
-    nrm = lim > 0 ? norm[t] : 0.0f;
-  }
+  bool whole;
+  int32_t t;
+  const int lim = group_tensor(binfo, nbinfo, begins, sizes, nt, e0, &whole, &t);
+  if (!whole) s_lim[threadIdx.x] = lim;
+  const float nrm = lim > 0 ? norm[t] : 0.0f;
   const uint64_t mask = (1ull << b) - 1ull;
   uint64_t acc = 0;
   int nb = 0, w = 0;
@@ -162,34 +193,44 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_packed(const uint32_t* _
   }
 }
 
+// The plan's arena as the pack and the decode walk it.
+struct ArenaArgs {
+  const uint32_t* binfo;
+  int64_t nbinfo;
+  const int64_t* begins;
+  const int64_t* sizes;
+  int32_t nt;
+  int64_t arena_end;
+};
+
 template <int WIDTH, int B>
-void launch_pack(dim3 g, hipStream_t st, const void* q, const Item* items, int32_t L, int32_t b, uint32_t* out) {
-  hipLaunchKernelGGL((qsgd_pack<WIDTH, B>), g, dim3(kThreads), 0, st, q, items, L, b, out);
+void launch_pack(dim3 g, hipStream_t st, const void* q, const ArenaArgs& a, int32_t L, int32_t b, uint32_t* out) {
+  hipLaunchKernelGGL((qsgd_pack<WIDTH, B>), g, dim3(kThreads), 0, st, q, a.binfo, a.nbinfo, a.begins, a.sizes, a.nt,
+                     a.arena_end, L, b, out);
 }
 
 template <int WIDTH>
-void dispatch_pack(int b, dim3 g, hipStream_t st, const void* q, const Item* items, int32_t L, uint32_t* out) {
+void dispatch_pack(int b, dim3 g, hipStream_t st, const void* q, const ArenaArgs& a, int32_t L, uint32_t* out) {
   switch (b) {
-    case 2: launch_pack<WIDTH, 2>(g, st, q, items, L, b, out); break;
-    case 3: launch_pack<WIDTH, 3>(g, st, q, items, L, b, out); break;
-    case 4: launch_pack<WIDTH, 4>(g, st, q, items, L, b, out); break;
-    case 5: launch_pack<WIDTH, 5>(g, st, q, items, L, b, out); break;
-    case 6: launch_pack<WIDTH, 6>(g, st, q, items, L, b, out); break;
-    case 7: launch_pack<WIDTH, 7>(g, st, q, items, L, b, out); break;
-    case 8: launch_pack<WIDTH, 8>(g, st, q, items, L, b, out); break;
-    case 9: launch_pack<WIDTH, 9>(g, st, q, items, L, b, out); break;
-    case 10: launch_pack<WIDTH, 10>(g, st, q, items, L, b, out); break;
-    default: launch_pack<WIDTH, 0>(g, st, q, items, L, b, out); break;
+    case 2: launch_pack<WIDTH, 2>(g, st, q, a, L, b, out); break;
+    case 3: launch_pack<WIDTH, 3>(g, st, q, a, L, b, out); break;
+    case 4: launch_pack<WIDTH, 4>(g, st, q, a, L, b, out); break;
+    case 5: launch_pack<WIDTH, 5>(g, st, q, a, L, b, out); break;
+    case 6: launch_pack<WIDTH, 6>(g, st, q, a, L, b, out); break;
+    case 7: launch_pack<WIDTH, 7>(g, st, q, a, L, b, out); break;
+    case 8: launch_pack<WIDTH, 8>(g, st, q, a, L, b, out); break;
+    case 9: launch_pack<WIDTH, 9>(g, st, q, a, L, b, out); break;
+    case 10: launch_pack<WIDTH, 10>(g, st, q, a, L, b, out); break;
+    default: launch_pack<WIDTH, 0>(g, st, q, a, L, b, out); break;
   }
 }
 
 template <bool ACC, bool POW2>
-void dispatch_decode(int b, dim3 g, hipStream_t st, const uint32_t* packed, const uint32_t* binfo, int64_t nbinfo,
-                     const float* norm, const int64_t* begins, const int64_t* sizes, int32_t nt, int64_t arena_end,
+void dispatch_decode(int b, dim3 g, hipStream_t st, const uint32_t* packed, const ArenaArgs& a, const float* norm,
                      float* y, int32_t L, float levels, float inv) {
-#define OMF_DP(BB)                                                                                              \
-  hipLaunchKernelGGL((qsgd_decode_packed<BB, ACC, POW2>), g, dim3(kThreads), 0, st, packed, binfo, nbinfo, norm, \
-                     begins, sizes, nt, arena_end, y, L, b, levels, inv)
+#define OMF_DP(BB)                                                                                               \
+  hipLaunchKernelGGL((qsgd_decode_packed<BB, ACC, POW2>), g, dim3(kThreads), 0, st, packed, a.binfo, a.nbinfo, norm, \
+                     a.begins, a.sizes, a.nt, a.arena_end, y, L, b, levels, inv)
   switch (b) {
     case 2: OMF_DP(2); break;
     case 3: OMF_DP(3); break;
@@ -208,14 +249,34 @@ void dispatch_decode(int b, dim3 g, hipStream_t st, const uint32_t* packed, cons
 }  // namespace
 
 namespace omf_plan_access {
-const void* flat_items(const omf_plan* p, int64_t* n);
 int device(const omf_plan* p);
 int32_t ntensors(const omf_plan* p);
 int64_t arena_end(const omf_plan* p);
 const int64_t* d_sizes(const omf_plan* p);
 const int64_t* d_begins(const omf_plan* p);
+const std::vector<int64_t>& offsets(const omf_plan* p);
 const uint32_t* dec_blocks(const omf_plan* p, int64_t* n, int64_t* block_elems);
 }  // namespace omf_plan_access
+
+namespace {
+
+// The plan's arena for the packed wire, or an error: every tensor offset a multiple of 32
+// elements (a tensor's stream then starts on a word, and a 32-element group lies in one tensor).
+int packed_arena(const omf_plan* plan, ArenaArgs* a, dim3* grid) {
+  for (const int64_t o : omf_plan_access::offsets(plan))
+    if (o & 31) return fail(OMF_EINVAL, "the packed wire needs tensor offsets that are multiples of 32 elements");
+  int64_t tblk = 0;
+  a->binfo = omf_plan_access::dec_blocks(plan, &a->nbinfo, &tblk);
+  if (tblk != kTableBlk) return fail(OMF_EINVAL, "packed wire: decoder table block size mismatch (library build)");
+  a->begins = omf_plan_access::d_begins(plan);
+  a->sizes = omf_plan_access::d_sizes(plan);
+  a->nt = omf_plan_access::ntensors(plan);
+  a->arena_end = omf_plan_access::arena_end(plan);
+  *grid = dim3((unsigned)((a->arena_end + kGroupBlk - 1) / kGroupBlk));
+  return OMF_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -235,15 +296,14 @@ int omf_qsgd_pack(omf_plan* plan, const void* q, int32_t width, int32_t levels, 
   if (width == 8 && levels > 127) return fail(OMF_EINVAL, "an int8 payload holds levels <= 127");
   if (!q || !packed) return fail(OMF_EINVAL, "q and packed must be non-NULL");
   if (((uintptr_t)q & 15) || ((uintptr_t)packed & 3)) return fail(OMF_EINVAL, "q must be 16-byte, packed 4-byte aligned");
+  ArenaArgs a;
+  dim3 grid;
+  if (const int rc = packed_arena(plan, &a, &grid)) return rc;
   DeviceGuard g(omf_plan_access::device(plan));
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
-  int64_t n_items = 0;
-  const Item* items = static_cast<const Item*>(omf_plan_access::flat_items(plan, &n_items));
-  if (n_items == 0) return OMF_OK;
-  const dim3 grid((unsigned)n_items);
   hipStream_t st = (hipStream_t)stream;
-  if (width == 8) dispatch_pack<1>(b, grid, st, q, items, levels, packed);
-  else dispatch_pack<4>(b, grid, st, q, items, levels, packed);
+  if (width == 8) dispatch_pack<1>(b, grid, st, q, a, levels, packed);
+  else dispatch_pack<4>(b, grid, st, q, a, levels, packed);
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }
@@ -255,23 +315,15 @@ int omf_qsgd_decode_packed(omf_plan* plan, const uint32_t* packed, int32_t level
   if (b < 0 || b > 32) return fail(OMF_EINVAL, "levels must be in [1, 2^31 - 1)");
   if (!packed || !norm || !y) return fail(OMF_EINVAL, "packed, norm and y must be non-NULL");
   if (((uintptr_t)y & 15) || ((uintptr_t)packed & 3)) return fail(OMF_EINVAL, "y must be 16-byte, packed 4-byte aligned");
+  ArenaArgs a;
+  dim3 grid;
+  if (const int rc = packed_arena(plan, &a, &grid)) return rc;
   DeviceGuard g(omf_plan_access::device(plan));
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
-  int64_t n_items = 0;
-  (void)omf_plan_access::flat_items(plan, &n_items);
-  if (n_items == 0) return OMF_OK;  // no element to decode
-  int64_t nbinfo = 0, tblk = 0;
-  const uint32_t* binfo = omf_plan_access::dec_blocks(plan, &nbinfo, &tblk);
-  if (tblk != kTableBlk) return fail(OMF_EINVAL, "omf_qsgd_decode_packed: decoder table block size mismatch (library build)");
-  const int64_t end = omf_plan_access::arena_end(plan);
-  const dim3 grid((unsigned)((end + 2 * kTableBlk - 1) / (2 * kTableBlk)));
   hipStream_t st = (hipStream_t)stream;
   const bool pow2 = (levels & (levels - 1)) == 0;
   const float lv = (float)levels, inv = pow2 ? 1.0f / (float)levels : 0.0f;
-  const int64_t* bg = omf_plan_access::d_begins(plan);
-  const int64_t* sz = omf_plan_access::d_sizes(plan);
-  const int32_t nt = omf_plan_access::ntensors(plan);
-#define OMF_DD(A, P) dispatch_decode<A, P>(b, grid, st, packed, binfo, nbinfo, norm, bg, sz, nt, end, y, levels, lv, inv)
+#define OMF_DD(A, P) dispatch_decode<A, P>(b, grid, st, packed, a, norm, y, levels, lv, inv)
   if (accumulate) {
     if (pow2) OMF_DD(true, true); else OMF_DD(true, false);
   } else {

@@ -115,6 +115,11 @@ def test_packed_decode_many_tensors_keeps_padding(gpu, levels):
     q = torch.from_numpy(rng.integers(-levels, levels + 1, plan.arena_end)).to(qt).to(gpu)
     norms = torch.from_numpy(rng.random(plan.nt, dtype=np.float32) + 0.5).to(gpu)
     packed = plan.qsgd_pack(q, width, levels)
+    ph = packed.cpu().numpy().view(np.uint8)
+    qh = q.cpu().numpy()
+    b = codec.packed_bits(levels)
+    for o, n in zip(plan.offsets, plan.sizes):  # the pack against the numpy restatement
+        assert ph[o * b // 8:o * b // 8 + (n * b + 7) // 8].tobytes() == bitpack.pack(qh[o:o + n], levels), n
     pad = torch.ones(plan.arena_end, dtype=torch.bool)
     for o, n in zip(plan.offsets, plan.sizes):
         pad[o:o + n] = False
@@ -127,3 +132,14 @@ def test_packed_decode_many_tensors_keeps_padding(gpu, levels):
         for o, n in zip(plan.offsets, plan.sizes):
             assert torch.equal(y[o:o + n], want[o:o + n]), (levels, accumulate, n)
         assert bool((y[pad] == 7.0).all()), (levels, accumulate)
+
+
+def test_packed_wire_needs_offsets_on_groups_of_32(gpu):
+    """Offsets that are multiples of 4 but not of 32 are a valid plan, not a packed arena."""
+    plan = codec.Plan([100, 50], offsets=[0, 100], device=gpu)
+    q = torch.zeros(plan.arena_end + 12, dtype=torch.int8, device=gpu)
+    with pytest.raises(ValueError, match="multiples of 32"):
+        plan.qsgd_pack(q, 8, 16)
+    with pytest.raises(ValueError, match="multiples of 32"):
+        plan.qsgd_decode_packed(torch.zeros(plan.packed_words(16), dtype=torch.int32, device=gpu), 16,
+                                torch.ones(2, device=gpu))
