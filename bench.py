@@ -53,6 +53,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-topk", action="store_true", help="skip the Top-K object of the QSGD line")
     ap.add_argument("--no-extras", action="store_true", help="skip PCIe-inclusive and PS timings")
+    ap.add_argument("--dist", action="store_true",
+                    help="N = 1 in a one-rank RCCL group: also runs the PS weighted-sum / Top-K aggregate leg "
+                         "(the N > 1 code path; no scaling is implied)")
     return ap.parse_args()
 
 
@@ -79,9 +82,16 @@ def spawn_ranks(n: int) -> int:
     return next((c for c in codes if c != 0), 0)
 
 
-def init_dist(torch, dist):
+def init_dist(torch, dist, force: bool = False):
+    """The rank's process group (RCCL).  ``force`` at world size 1: a one-rank group with a loopback
+    rendezvous, so the N > 1 aggregate leg runs on one GPU (``--dist``)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world <= 1:
+        if force:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            torch.cuda.set_device(0)
+            dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
         return 0, 1, 0
     # the rank's GPU first: RCCL binds its communicator (and barrier) to the current device
     local = int(os.environ.get("LOCAL_RANK", os.environ.get("RANK", "0")))
@@ -251,7 +261,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    rank, world, local = init_dist(torch, dist)
+    rank, world, local = init_dist(torch, dist, args.dist)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from omnifed_amd import codec, shapes
@@ -439,7 +449,7 @@ def main():
                                     "algorithmic_GBs": round((8 + 2 * w) * N / pt / 1e9, 2),
                                     "fp32_gradient_GBs": round(4 * N / pt / 1e9, 2)}
         del xh, qh, yh, xd
-    if not args.no_extras and world > 1:
+    if not args.no_extras and dist.is_initialized():
         from omnifed_amd.ps import GpuOps, qsgd_weighted_round, topk_sparse_aggregate, total_weight
 
         ops = GpuOps(plan, seed=seed)

@@ -62,7 +62,7 @@ extern "C" {
 typedef struct omf_plan omf_plan;
 
 /* ABI version (major*100 + minor). */
-#define OMF_ABI_VERSION 105
+#define OMF_ABI_VERSION 106
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -268,6 +268,14 @@ int omf_qsgd_decode_packed(omf_plan* plan, const uint32_t* packed, int32_t level
  * the device-wide sort.
  */
 int64_t omf_topk_k(int64_t numel, double ratio);
+/* Test / experiment hook of the plan's Top-K encoder (never needed in production; the defaults
+ * come from the OMF_TOPK_* environment, read once at the plan's first Top-K call).  Every
+ * setting changes only how the exact selection is found, never what it is: groups (>= 1) = the
+ * two-stream group pipeline, force_fallback (0 / 1) = always the device-wide radix sort,
+ * sample_runs (0 = default, or 64..2^20) = sampled runs per tensor, sure_z / sure_c = the sure
+ * bin's margin.  A negative argument keeps the current setting. */
+int omf_plan_set_topk(omf_plan* plan, int32_t groups, int32_t force_fallback, int64_t sample_runs, float sure_z,
+                      float sure_c);
 size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio);
 int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,
                     float alpha, float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream);
@@ -310,6 +318,31 @@ int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, con
 size_t omf_topk_decode_workspace_bytes(const omf_plan* plan, double ratio);
 int omf_topk_decode_arena_ws(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
                              int32_t mode, void* ws, size_t ws_bytes, void* stream);
+
+/*
+ * The whole-arena decode of ONE received message, whose per-tensor selection sizes are whatever
+ * its layers carry (k_t = len(values_data) / 4) rather than a ratio's: the per-layer
+ * _decode_topk_layer loop of decode_updates_dict (global_grpc_compression.py:140-160, 214-223),
+ * the PS's accumulate of a Top-K update (global_grpc_server.py:108-111, 147-153: with mode 2) and
+ * the client downlink overlay (global_grpc_client.py:98-111: mode 1) in one call.
+ * counts: HOST array of ntensors, 0 <= counts[t] <= sizes[t] (0: the tensor is absent from the
+ * message — mode 0 leaves it zero, modes 1 / 2 untouched); values / indices packed in plan order
+ * at K_t = sum_{u<t} counts[u].  Otherwise as omf_topk_decode_arena_ws (modes, workspace of
+ * omf_topk_decode_counts_workspace_bytes(plan, counts) bytes for the tiled mode 0, or NULL).
+ * The plan keeps the tables of the last 8 count vectors it saw (uploaded on first use).
+ */
+size_t omf_topk_decode_counts_workspace_bytes(const omf_plan* plan, const int64_t* counts);
+int omf_topk_decode_counts(omf_plan* plan, const int64_t* counts, const float* values, const int64_t* indices,
+                           float* y, int32_t mode, void* ws, size_t ws_bytes, void* stream);
+/*
+ * Index check of a received selection (layout as omf_topk_decode_counts), before it is decoded:
+ * the reference decoder indexes with numpy (`dense[indices] = values`,
+ * global_grpc_compression.py:154/158), which wraps an index in [-n_t, 0) to i + n_t — rewritten
+ * here in place in the DEVICE array `indices` — and raises IndexError for one outside
+ * [-n_t, n_t).  *bad (device int32) receives the lowest such tensor t, or 0x7f7f7f7f (>= ntensors)
+ * when every index is in range.  Asynchronous on `stream`.
+ */
+int omf_topk_check_indices(omf_plan* plan, const int64_t* counts, int64_t* indices, int32_t* bad, void* stream);
 
 #ifdef __cplusplus
 }

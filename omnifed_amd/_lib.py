@@ -59,12 +59,17 @@ SIGNATURES = {
     "omf_qsgd_pack": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
     "omf_qsgd_decode_packed": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
     "omf_topk_k": (_c_i64, [_c_i64, _c_f64]),
+    "omf_plan_set_topk": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i64, _c_f32, _c_f32]),
     "omf_topk_workspace_bytes": (_c_size, [_c_p, _c_f64]),
     "omf_topk_encode": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_f64, _c_f32, _c_p, _c_p, _c_p, _c_size, _c_p]),
     "omf_topk_decode": (ctypes.c_int, [_c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i32, _c_p]),
     "omf_topk_decode_arena": (ctypes.c_int, [_c_p, _c_f64, _c_p, _c_p, _c_p, _c_i32, _c_p]),
     "omf_topk_decode_workspace_bytes": (_c_size, [_c_p, _c_f64]),
     "omf_topk_decode_arena_ws": (ctypes.c_int, [_c_p, _c_f64, _c_p, _c_p, _c_p, _c_i32, _c_p, _c_size, _c_p]),
+    "omf_topk_decode_counts_workspace_bytes": (_c_size, [_c_p, ctypes.POINTER(_c_i64)]),
+    "omf_topk_decode_counts": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64), _c_p, _c_p, _c_p, _c_i32, _c_p, _c_size,
+                                              _c_p]),
+    "omf_topk_check_indices": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64), _c_p, _c_p, _c_p]),
 }
 
 _lock = threading.Lock()
@@ -75,7 +80,7 @@ class CodecError(RuntimeError):
     pass
 
 
-ABI_VERSION = 105  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+ABI_VERSION = 106  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
 
 
 def lib() -> ctypes.CDLL:

@@ -115,6 +115,7 @@ class Plan:
         self._topk_ws: Dict[int, torch.Tensor] = {}  # per stream: launches on two streams never share one
         self._dec_ws: Dict[int, torch.Tensor] = {}   # tiled Top-K decode workspace, per stream
         self._dec_need: Dict[float, int] = {}
+        self._counts_cache: Dict[tuple, tuple] = {}
         self._topk_cache: Dict[float, tuple] = {}
         # the library's choice (by arena size, or OMF_ENCODE_STRATEGY)
         self.strategy = STRATEGIES[int(L.omf_plan_encode_strategy(h))]
@@ -155,11 +156,21 @@ class Plan:
         payload of that launch is invalid).  Returns False if an encoder had to recompute a
         norm (results exact, but the grid was not co-resident).  Every product entry point
         calls it at the synchronisation it already makes."""
-        rc = lib().omf_plan_check(self._h, ctypes.c_void_p(stream if stream is not None else _stream(self.device)))
+        with self._lock:  # the plan's host state (its last stream, the flags it clears) is shared by threads
+            rc = lib().omf_plan_check(self._h, ctypes.c_void_p(stream if stream is not None else _stream(self.device)))
         if rc == 1:
             return False
         check(rc, "omf_plan_check")
         return True
+
+    def set_topk(self, groups: int = -1, fallback: int = -1, sample_runs: int = -1, sure=None) -> None:
+        """Test / experiment hook of the Top-K encoder (omf_plan_set_topk): the group pipeline,
+        the forced radix-sort fallback, the sample size (0 = default), the sure margin (z, c).
+        None of them changes the selection; -1 / None keeps a setting."""
+        z, c = (-1.0, -1.0) if sure is None else (float(sure[0]), float(sure[1]))
+        with self._lock:
+            check(lib().omf_plan_set_topk(self._h, int(groups), int(fallback), int(sample_runs), z, c),
+                  "omf_plan_set_topk")
 
     def set_debug(self, ring: int = 0, spec: int = 0, lds_wait_us: int = 0) -> None:
         """Test / experiment hook (omf_plan_set_debug): switches that change what an encode
@@ -203,7 +214,8 @@ class Plan:
         """Diagnostics of the last bracketed encode (omf_plan_spec_stats; synchronises)."""
         out = (ctypes.c_int64 * 4)()
         st = stream if stream is not None else _stream(self.device)
-        check(lib().omf_plan_spec_stats(self._h, ctypes.c_void_p(st), out), "omf_plan_spec_stats")
+        with self._lock:
+            check(lib().omf_plan_spec_stats(self._h, ctypes.c_void_p(st), out), "omf_plan_spec_stats")
         return dict(zip(("whole", "deferred", "listed", "full_slots"), (int(v) for v in out)))
 
     @property
@@ -446,16 +458,84 @@ class Plan:
             if need is None:
                 need = self._dec_need[key] = int(L.omf_topk_decode_workspace_bytes(self._h, key))
             with self._lock:
-                ws = self._dec_ws.get(st)
-                if ws is None or ws.numel() < need:  # zero-filled once; every call leaves it so
-                    ws = torch.zeros(need, dtype=torch.uint8, device=dev)
-                    self._dec_ws[st] = ws
-                check(L.omf_topk_decode_arena_ws(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), 0,
-                                                 _ptr(ws), ctypes.c_size_t(ws.numel()), ctypes.c_void_p(st)),
-                      "omf_topk_decode_arena_ws")
+                ws = self._dec_workspace(st, need)
+                rc = L.omf_topk_decode_arena_ws(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), 0,
+                                                _ptr(ws), ctypes.c_size_t(ws.numel()), ctypes.c_void_p(st))
+                if rc != 0:
+                    self._dec_ws.pop(st, None)  # its counters may be left non-zero: start afresh
+                check(rc, "omf_topk_decode_arena_ws")
             return y
-        check(L.omf_topk_decode_arena(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), int(mode),
-                                      ctypes.c_void_p(st)), "omf_topk_decode_arena")
+        with self._lock:
+            check(L.omf_topk_decode_arena(self._h, float(ratio), _ptr(values), _ptr(indices), _ptr(y), int(mode),
+                                          ctypes.c_void_p(st)), "omf_topk_decode_arena")
+        return y
+
+    def _dec_workspace(self, st: int, need: int) -> torch.Tensor:
+        """The tiled decode's workspace of stream ``st`` (caller holds ``self._lock``): zero-filled
+        once (every call leaves its counters zero), the fill ordered before its first use on ``st``."""
+        ws = self._dec_ws.get(st)
+        if ws is None or ws.numel() < need:
+            ws = torch.zeros(max(need, 256), dtype=torch.uint8, device=self.device)
+            torch.cuda.current_stream(self.device).synchronize()  # the fill ran on the current stream
+            self._dec_ws[st] = ws
+        return ws
+
+    def _counts(self, counts: Sequence[int]):
+        """(ctypes int64 array, total) of a per-tensor count vector (cached: a message layout
+        repeats every round)."""
+        key = tuple(int(c) for c in counts)
+        c = self._counts_cache.get(key)
+        if c is None:
+            if len(key) != self.nt:
+                raise ValueError(f"counts: {len(key)} entries, plan has {self.nt} tensors")
+            arr = (ctypes.c_int64 * self.nt)(*key)
+            need = int(lib().omf_topk_decode_counts_workspace_bytes(self._h, arr))
+            if need == 0:
+                raise ValueError("counts must satisfy 0 <= counts[t] <= sizes[t]")
+            if len(self._counts_cache) >= 16:
+                self._counts_cache.pop(next(iter(self._counts_cache)))
+            c = self._counts_cache[key] = (arr, sum(key), need)
+        return c
+
+    def topk_check_indices(self, counts: Sequence[int], indices: torch.Tensor,
+                           stream: Optional[int] = None) -> torch.Tensor:
+        """omf_topk_check_indices: wrap indices in [-n_t, 0) in place (numpy's negative indexing of the
+        reference decoder) and return a device int32 holding the lowest tensor with an index outside
+        [-n_t, n_t) (>= nt when there is none).  Asynchronous."""
+        arr, ktot, _ = self._counts(counts)
+        dev = self.device
+        _need(indices, "indices", torch.int64, dev, ktot, 8)
+        bad = torch.empty(1, dtype=torch.int32, device=dev)
+        st = stream if stream is not None else _stream(dev)
+        with self._lock:
+            check(lib().omf_topk_check_indices(self._h, arr, _ptr(indices), _ptr(bad), ctypes.c_void_p(st)),
+                  "omf_topk_check_indices")
+        return bad
+
+    def topk_decode_counts(self, counts: Sequence[int], values: torch.Tensor, indices: torch.Tensor,
+                           y: Optional[torch.Tensor] = None, mode: int = 0, stream: Optional[int] = None) -> torch.Tensor:
+        """Decode one received message's Top-K selection (per-tensor sizes ``counts``, packed in plan
+        order) into the arena ``y``: mode 0 zeros + set (tiled), 1 overlay, 2 scatter-add; one call."""
+        arr, ktot, need = self._counts(counts)
+        dev = self.device
+        _need(values, "values", torch.float32, dev, ktot, 4)
+        _need(indices, "indices", torch.int64, dev, ktot, 8)
+        if mode not in (0, 1, 2):
+            raise ValueError("mode must be 0, 1 or 2")
+        if y is None:
+            if mode != 0:
+                raise ValueError("mode 1/2 need y")
+            y = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
+        _need(y, "y", torch.float32, dev, self.arena_end, 16 if mode == 0 else 4)
+        st = stream if stream is not None else _stream(dev)
+        L = lib()
+        with self._lock:
+            ws = self._dec_workspace(st, need) if mode == 0 else None
+            rc = L.omf_topk_decode_counts(self._h, arr, _ptr(values), _ptr(indices), _ptr(y), int(mode), _ptr(ws),
+                                          ctypes.c_size_t(0 if ws is None else ws.numel()), ctypes.c_void_p(st))
+            if rc != 0 and ws is not None:
+                self._dec_ws.pop(st, None)
+            check(rc, "omf_topk_decode_counts")
         return y
 
 

@@ -17,6 +17,17 @@ constexpr int kWaves = kThreads / 64;
 // encode call of round 3); the kernels' own completion already releases at device scope.
 constexpr unsigned kOrderEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
 
+// Top-K encoder settings of a plan (omf_topk.hip): read from the OMF_TOPK_* environment once, at
+// the plan's first Top-K call, and settable by the omf_plan_set_topk test / experiment hook.
+struct TopkKnobs {
+  bool init = false;
+  int32_t groups = 1;          // two-stream group pipeline (off: measured slower)
+  int32_t dbg = 0;             // OMF_TOPK_DBG diagnostics
+  int32_t force_fallback = 0;  // always take the device-wide radix-sort path (tests of that path)
+  int64_t sample_runs = 0;     // sampled runs per tensor at most (0: the default, 2 Ki)
+  float sure_z = 1.5f, sure_c = 2.0f;  // the "sure" bin's margin below the expected rank-k count
+};
+
 // Thread-local error string behind omf_last_error().
 void set_error(const std::string& msg);
 int fail(int code, const std::string& msg);

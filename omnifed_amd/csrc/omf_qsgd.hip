@@ -1359,8 +1359,10 @@ struct omf_plan {
     uint64_t key;
     void* dev;
     uint64_t host;
+    std::vector<int64_t> counts;  // tables keyed by explicit per-tensor counts: the exact counts
   };
   std::vector<TopkTable> topk_tables;
+  omf::TopkKnobs topk_knobs;
   // Launches that use the sync block / granules are ordered across streams: a launch on a
   // stream other than the previous one first waits for the previous launch's event.
   hipEvent_t last_ev = nullptr;
@@ -1417,12 +1419,45 @@ void* topk_table(omf_plan* p, uint64_t key, size_t bytes, bool* fresh, uint64_t*
     }
   void* d = nullptr;
   if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
-  p->topk_tables.push_back({key, d, 0});
+  p->topk_tables.push_back({key, d, 0, {}});
+  *host = &p->topk_tables.back().host;
+  *fresh = true;
+  return d;
+}
+// The same for tables keyed by an explicit per-tensor count vector (a received Top-K message's
+// k_t): matched on the exact counts.  At most kMaxCountTables are kept; making one more frees the
+// oldest (hipFree waits for the device, so no queued launch still reads it).
+void* topk_table_counts(omf_plan* p, const int64_t* counts, size_t bytes, bool* fresh, uint64_t** host) {
+  constexpr uint64_t kCountsKey = 0xC0C0C0C0C0C0C0C0ull;
+  constexpr int kMaxCountTables = 8;
+  *fresh = false;
+  const size_t nt = (size_t)p->nt;
+  int held = 0;
+  for (auto& e : p->topk_tables) {
+    if (e.key != kCountsKey) continue;
+    ++held;
+    if (e.counts.size() == nt && std::equal(e.counts.begin(), e.counts.end(), counts)) {
+      *host = &e.host;
+      return e.dev;
+    }
+  }
+  if (held >= kMaxCountTables) {
+    for (auto it = p->topk_tables.begin(); it != p->topk_tables.end(); ++it)
+      if (it->key == kCountsKey) {
+        (void)hipFree(it->dev);
+        p->topk_tables.erase(it);
+        break;
+      }
+  }
+  void* d = nullptr;
+  if (hipMalloc(&d, bytes) != hipSuccess) return nullptr;
+  p->topk_tables.push_back({kCountsKey, d, 0, std::vector<int64_t>(counts, counts + nt)});
   *host = &p->topk_tables.back().host;
   *fresh = true;
   return d;
 }
 const std::vector<int64_t>& offsets(const omf_plan* p) { return p->offsets; }
+omf::TopkKnobs& topk_knobs(omf_plan* p) { return p->topk_knobs; }
 }  // namespace omf_plan_access
 
 static size_t round16(size_t b) { return (b + 15) & ~(size_t)15; }

@@ -39,6 +39,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <thread>
 #include <vector>
 
 #include "../../include/omf_codec.h"
@@ -1394,61 +1395,62 @@ __global__ __launch_bounds__(kThreads) void topk_scatter(const float* __restrict
 }
 
 // Whole-arena decode of one client's selection (values/indices packed per tensor at
-// K_t = sum_{u<t} k_u, tensor-local indices): y[begin_t + idx] = v (mode 0/1) or += v (2).
-// Indices are unique within a client, so the read-modify-write needs no atomics.
+// koff[t] = sum_{u<t} k_u, tensor-local indices): y[begin_t + idx] = v (mode 0/1) or += v (2).
+// Indices are unique within a client, so the read-modify-write needs no atomics.  koff comes from
+// the plan's decode table (a ratio's k_t, or a received message's counts; k_t may be 0).
 constexpr int kArenaMaxTensors = 4096;
+
+// The tensor t with koff[t] <= j < koff[t + 1] among [0, nt): the largest t with koff[t] <= j
+// (a tensor with no values shares its koff with the next one, which is then the larger t).
+__device__ __forceinline__ int koff_tensor(const int64_t* koff, int nt, int64_t j) {
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (koff[mid] <= j) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
 __global__ __launch_bounds__(kThreads) void topk_scatter_arena(const float* __restrict__ values,
                                                                const int64_t* __restrict__ indices,
                                                                const int64_t* __restrict__ sizes,
-                                                               const int64_t* __restrict__ begins, int nt,
-                                                               double ratio, int64_t ktot, float* __restrict__ y,
-                                                               int add) {
+                                                               const int64_t* __restrict__ begins,
+                                                               const int64_t* __restrict__ koff_g, int nt,
+                                                               int64_t ktot, float* __restrict__ y, int add) {
   __shared__ int64_t koff[kArenaMaxTensors + 1];
-  __shared__ int64_t s_part[kThreads];
-  {  // k_t exactly as omf_topk_k, prefix-summed by the whole block (16 tensors per thread)
-    constexpr int PER = kArenaMaxTensors / kThreads;
-    int64_t kv[PER], loc = 0;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int t = threadIdx.x * PER + j;
-      int64_t k = 0;
-      if (t < nt) {
-        k = (int64_t)((double)sizes[t] * ratio);
-        if (k < 1) k = 1;
-      }
-      kv[j] = k;
-      loc += k;
-    }
-    s_part[threadIdx.x] = loc;
-    __syncthreads();
-    for (int o = 1; o < kThreads; o <<= 1) {  // inclusive scan (once per block)
-      const int64_t add = threadIdx.x >= (unsigned)o ? s_part[threadIdx.x - o] : 0;
-      __syncthreads();
-      s_part[threadIdx.x] += add;
-      __syncthreads();
-    }
-    int64_t run = s_part[threadIdx.x] - loc;
-#pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const int t = threadIdx.x * PER + j;
-      if (t <= nt) koff[t] = run;
-      run += kv[j];
-    }
-    if (threadIdx.x == kThreads - 1) koff[nt] = s_part[kThreads - 1];
-  }
+  for (int t = threadIdx.x; t <= nt; t += kThreads) koff[t] = koff_g[t];
   __syncthreads();
   for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < ktot; j += (int64_t)gridDim.x * kThreads) {
-    int lo = 0, hi = nt - 1;  // the tensor t with koff[t] <= j < koff[t + 1]
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (koff[mid] <= j) lo = mid;
-      else hi = mid - 1;
-    }
+    const int t = koff_tensor(koff, nt, j);
     const int64_t i = indices[j];
-    if (i < 0 || i >= sizes[lo]) continue;  // padding (-1) or out of range: skipped
-    float* p = y + begins[lo] + i;
+    if (i < 0 || i >= sizes[t]) continue;  // padding (-1) or out of range: skipped
+    float* p = y + begins[t] + i;
     *p = add ? __fadd_rn(*p, values[j]) : values[j];
   }
+}
+
+// Index check of a received selection, before anything is decoded: numpy's indexing of the
+// reference decoder (`dense[indices] = values`, global_grpc_compression.py:154/158) wraps an index
+// in [-n, 0) to i + n (rewritten here in place) and raises IndexError for one outside [-n, n).
+// The lowest tensor holding such an index is atomicMin'ed into *bad (one atomic per wave).
+__global__ __launch_bounds__(kThreads) void topk_check_idx(int64_t* __restrict__ indices,
+                                                           const int64_t* __restrict__ sizes,
+                                                           const int64_t* __restrict__ koff_g, int nt, int64_t ktot,
+                                                           int32_t* __restrict__ bad) {
+  __shared__ int64_t koff[kArenaMaxTensors + 1];
+  for (int t = threadIdx.x; t <= nt; t += kThreads) koff[t] = koff_g[t];
+  __syncthreads();
+  int lowest = 0x7fffffff;
+  for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < ktot; j += (int64_t)gridDim.x * kThreads) {
+    const int t = koff_tensor(koff, nt, j);
+    const int64_t i = indices[j], n = sizes[t];
+    if (i >= n || i < -n) lowest = min(lowest, t);
+    else if (i < 0) indices[j] = i + n;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) lowest = min(lowest, __shfl_xor(lowest, o, 64));
+  if ((threadIdx.x & 63) == 0 && lowest != 0x7fffffff) atomicMin(bad, lowest);
 }
 
 // ---------------------------------------------------------------- tiled zero-fill decode (mode 0)
@@ -1653,30 +1655,37 @@ const int64_t* d_begins(const omf_plan* p);
 const std::vector<int64_t>& sizes(const omf_plan* p);
 const std::vector<int64_t>& offsets(const omf_plan* p);
 void* topk_table(omf_plan* p, uint64_t key, size_t bytes, bool* fresh, uint64_t** host);
+void* topk_table_counts(omf_plan* p, const int64_t* counts, size_t bytes, bool* fresh, uint64_t** host);
+omf::TopkKnobs& topk_knobs(omf_plan* p);
 }  // namespace omf_plan_access
 
 namespace {
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// OMF_TOPK_FALLBACK=1: always take the device-wide radix-sort path (tests of that path).
 // Per host thread and device: a 16-byte status buffer in mapped, coherent host memory that
 // topk_plan's last block writes (never freed: a few bytes per thread that calls the encoder).
 struct HostSync {
   uint32_t* pinned = nullptr;  // host view
   uint32_t* dev = nullptr;     // device view of the same bytes
   uint32_t seq = 0;
+  double verdict_us = 0.0;     // recent launch-to-verdict time (fast to fall, slow to rise)
   hipStream_t side = nullptr;  // the pipeline's second stream (made on first use)
   hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t fused[2] = {nullptr, nullptr};  // per stream: its latest group's streaming pass issued
 };
 
-// Wait for the verdict of call `seq`: spin on the mapped word (it lands as soon as the plan
-// kernel's successor runs; an event or a copy packet would add tens of µs, and every µs the
-// host spends here is a µs the next call's launches come later).  If it has not come after
-// 200 ms, synchronise the stream (which reports a failed launch or fault) and look again.
-int wait_status(HostSync* h, uint32_t seq, hipStream_t st) {
-  const auto t0 = std::chrono::steady_clock::now();
+// Wait for the verdict of call `seq` (launched at t0).  The verdict lands as soon as the plan kernel
+// ends (~90 % into the call; the bucket kernels are queued behind it, so the GPU stays busy while
+// the host reads it).  The host first sleeps for 60 % of the recent launch-to-verdict time — the
+// thread is descheduled instead of spinning a core for ~0.8 ms a call — then spins on the mapped
+// word (an event or a copy packet would add tens of us).  If it has not come after 200 ms,
+// synchronise the stream (which reports a failed launch or fault) and look again.
+int wait_status(HostSync* h, uint32_t seq, hipStream_t st, std::chrono::steady_clock::time_point t0) {
+  if (h->verdict_us > 200.0) {
+    const auto nap = std::chrono::microseconds((int64_t)(0.6 * h->verdict_us));
+    if (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq) std::this_thread::sleep_until(t0 + nap);
+  }
   while (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq) {
     if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
       OMF_HIP(hipStreamSynchronize(st));
@@ -1686,6 +1695,8 @@ int wait_status(HostSync* h, uint32_t seq, hipStream_t st) {
     }
     __builtin_ia32_pause();
   }
+  const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  h->verdict_us = (h->verdict_us == 0.0 || us < h->verdict_us) ? us : 0.9 * h->verdict_us + 0.1 * us;
   return OMF_OK;
 }
 HostSync* host_sync(int dev) {
@@ -1730,13 +1741,11 @@ struct Group {
   uint32_t sup0 = 0, nsup = 0, bk0 = 0, nbk = 0;    // super-items, bucket slots
 };
 
-int topk_group_count(const omf_plan* p) {
+int topk_group_count(const omf_plan* p, const TopkKnobs& kn) {
   // Off by default: measured on Llama-400M (scripts/exp/tk_env_ab.py) more groups only add time —
   // 1.089 ms with one group, 1.156 / 1.192 / 1.266 ms with 2 / 3 / 4 (the latency-bound kernels
   // do not shrink with their group, and their random stores slow the streaming pass beside them).
-  // OMF_TOPK_GROUPS (experiments) turns it on.
-  const char* e = std::getenv("OMF_TOPK_GROUPS");
-  int g = e ? std::atoi(e) : 1;
+  int g = kn.groups;
   if (omf_plan_access::arena_end(p) < ((int64_t)1 << 24)) g = 1;  // small arenas: launch-bound
   return std::max(1, std::min(g, std::min(16, omf_plan_access::ntensors(p))));
 }
@@ -1780,21 +1789,37 @@ std::vector<Group> make_groups(const std::vector<int64_t>& sizes, double ratio, 
   return gs;
 }
 
-int dbg_bits() {  // OMF_TOPK_DBG: 4 = print the verdict flags, 8 = print over-full fine bins;
-  // experiment builds only (-DOMF_EXPERIMENTS; they change what an encode writes):
-  // 1 = no bucket sort, 2 = no residual zeroing
-  const char* e = std::getenv("OMF_TOPK_DBG");
-  const int d = e ? std::atoi(e) : 0;
+// The plan's Top-K settings: the OMF_TOPK_* environment read once, at its first Top-K call
+// (OMF_TOPK_GROUPS, OMF_TOPK_DBG, OMF_TOPK_FALLBACK, OMF_TOPK_SAMPLE_RUNS, OMF_TOPK_SURE="z,c"),
+// unless omf_plan_set_topk set them first.
+const TopkKnobs& knobs(omf_plan* p) {
+  TopkKnobs& k = omf_plan_access::topk_knobs(p);
+  if (k.init) return k;
+  k.init = true;
+  if (const char* e = std::getenv("OMF_TOPK_GROUPS")) k.groups = std::max(1, std::atoi(e));
+  if (const char* e = std::getenv("OMF_TOPK_DBG")) {
+    // 4 = print the verdict flags, 8 = print over-full fine bins; experiment builds only
+    // (-DOMF_EXPERIMENTS; they change what an encode writes): 1 = no bucket sort, 2 = no residual zeroing
+    const int d = std::atoi(e);
 #ifdef OMF_EXPERIMENTS
-  return d;
+    k.dbg = d;
 #else
-  return d & ~3;
+    k.dbg = d & ~3;
 #endif
-}
-
-bool force_fallback() {
-  const char* e = std::getenv("OMF_TOPK_FALLBACK");
-  return e && e[0] == '1';
+  }
+  if (const char* e = std::getenv("OMF_TOPK_FALLBACK")) k.force_fallback = e[0] == '1';
+  if (const char* e = std::getenv("OMF_TOPK_SAMPLE_RUNS")) {
+    const long long v = std::atoll(e);
+    if (v >= 64 && v <= (1 << 20)) k.sample_runs = v;
+  }
+  if (const char* e = std::getenv("OMF_TOPK_SURE")) {
+    float z = 0.f, c = 0.f;
+    if (std::sscanf(e, "%f,%f", &z, &c) == 2 && z >= 0.f && c >= 0.f) {
+      k.sure_z = z;
+      k.sure_c = c;
+    }
+  }
+  return k;
 }
 
 bool global_path(const omf_plan* p) {
@@ -1914,26 +1939,15 @@ struct SetupTable {
 };
 
 // Runs sampled per tensor at most (a performance knob only: the selection is exact for any
-// sample; OMF_TOPK_SAMPLE_RUNS overrides it for experiments).
-int64_t sample_max_runs() {
-  const char* e = std::getenv("OMF_TOPK_SAMPLE_RUNS");
-  const long long v = e ? std::atoll(e) : 0;
-  return v >= 64 && v <= (1 << 20) ? (int64_t)v : (int64_t)kSMaxRuns;
-}
+// sample; TopkKnobs::sample_runs overrides it for experiments).
+int64_t sample_max_runs(const TopkKnobs& kn) { return kn.sample_runs ? kn.sample_runs : (int64_t)kSMaxRuns; }
 
 // The "sure" bin's margin below the expected rank-k sample count m: m - z sqrt(m) - c (a
 // performance knob only: any sure bin gives the same selection — a sure key that is not selected
 // after all gets its t' back).  Every selected key below the sure bin costs the bucket sort a
 // random 4-byte residual store, every sure key past rank k one more: Llama-400M bucket sort 92 us
-// at (6, 32), 67 at (1.5, 2), 66 at (1, 0) (scripts/gpu_r3r.sh).  OMF_TOPK_SURE="z,c" overrides it.
-float2 sure_margin() {
-  float2 zc = make_float2(1.5f, 2.0f);
-  if (const char* e = std::getenv("OMF_TOPK_SURE")) {
-    float z = 0.f, c = 0.f;
-    if (std::sscanf(e, "%f,%f", &z, &c) == 2 && z >= 0.f && c >= 0.f) zc = make_float2(z, c);
-  }
-  return zc;
-}
+// at (6, 32), 67 at (1.5, 2), 66 at (1, 0) (round 3, rocprofv3).  TopkKnobs::sure_z / sure_c.
+float2 sure_margin(const TopkKnobs& kn) { return make_float2(kn.sure_z, kn.sure_c); }
 
 constexpr uint64_t kSetupTag = 0x5E7A9B1C00000000ull;
 
@@ -2016,6 +2030,21 @@ int64_t omf_topk_k(int64_t numel, double ratio) {
   return k < 1 ? 1 : k;
 }
 
+int omf_plan_set_topk(omf_plan* plan, int32_t groups, int32_t force_fallback, int64_t sample_runs, float sure_z,
+                      float sure_c) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (sample_runs > 0 && (sample_runs < 64 || sample_runs > (1 << 20)))
+    return fail(OMF_EINVAL, "omf_plan_set_topk: sample_runs must be 0 (default) or in [64, 2^20]");
+  (void)knobs(plan);  // the environment's values first, so a negative argument keeps them
+  TopkKnobs& k = omf_plan_access::topk_knobs(plan);
+  if (groups >= 1) k.groups = groups;
+  if (force_fallback >= 0) k.force_fallback = force_fallback != 0;
+  if (sample_runs >= 0) k.sample_runs = sample_runs;
+  if (sure_z >= 0.f) k.sure_z = sure_z;
+  if (sure_c >= 0.f) k.sure_c = sure_c;
+  return OMF_OK;
+}
+
 size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio) {
   (void)ratio;
   if (!plan) return 0;
@@ -2093,20 +2122,22 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   HostSync* hsync = host_sync(omf_plan_access::device(plan));
   if (!hsync) return fail(OMF_EHIP, "omf_topk_encode: pinned status buffer");
   const uint32_t seq = ++hsync->seq == 0 ? ++hsync->seq : hsync->seq;
+  const auto t_call = std::chrono::steady_clock::now();
   // the per-(plan, ratio) constant tables: made by topk_setup on the first call at this ratio
   SetupTable tb;
-  const int64_t max_runs = sample_max_runs();
-  const float2 sure_zc = sure_margin();
+  const TopkKnobs& kn = knobs(plan);
+  const int64_t max_runs = sample_max_runs(kn);
+  const float2 sure_zc = sure_margin(kn);
   if (int r = setup_table(plan, ratio, max_runs, st, status, &tb)) return r;
   kk = tb.kk; koff = tb.koff; tfirst = tb.tfirst; tlast = tb.tlast; bbase = tb.bbase; kb2 = tb.kb2; sbase = tb.sbase;
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
-    const bool forced = force_fallback();
+    const bool forced = kn.force_fallback != 0;
     const std::vector<Group> groups = make_groups(omf_plan_access::sizes(plan), ratio, max_runs,
-                                                  topk_group_count(plan));
+                                                  topk_group_count(plan, kn));
     if (groups.size() > 1)
       if (int r = pipe_streams(hsync)) return r;
-    const int dbg = dbg_bits();
+    const int dbg = kn.dbg;
     for (size_t gi = 0; gi < groups.size(); ++gi) {
       const Group& G = groups[gi];
       // group 0 runs on the caller's stream; its sample launch (which clears the call's status
@@ -2165,10 +2196,10 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       OMF_HIP(hipEventRecord(hsync->join, hsync->side));
       OMF_HIP(hipStreamWaitEvent(st, hsync->join, 0));
     }
-    if (int rc = wait_status(hsync, seq, st)) return rc;
+    if (int rc = wait_status(hsync, seq, st, t_call)) return rc;
     uint32_t host_status[4];
     std::memcpy(host_status, hsync->pinned, 16);
-    if (dbg_bits() & 4) fprintf(stderr, "omf_topk: redo %u overflow %u\n", host_status[1], host_status[2]);
+    if (kn.dbg & 4) fprintf(stderr, "omf_topk: redo %u overflow %u\n", host_status[1], host_status[2]);
     if (!host_status[1] && !host_status[2] && !forced) return OMF_OK;
     // fallback (a redo, a fine bin over kBucketHalf keys, or forced): device-wide radix sort
     if (rz) hipLaunchKernelGGL(topk_restore, grid, blk, 0, st, cand, items, sub_cnt, d_begins, rz);
@@ -2224,10 +2255,12 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   return OMF_OK;
 }
 
-// Tiled zero-fill decode.  Plan-owned constant tables per ratio (omf_plan_access::topk_table):
-// koff[nt + 1] (int64: each tensor's first selected value) and cap_base[nsuper + 1] (uint32:
-// the buckets' prefix of capacities).  Caller workspace: fill[nsuper] + the overflow count
-// (zeroed by the call), the buckets (cap_base[nsuper] entries) and the overflow list (ktot).
+// Whole-arena decode.  Plan-owned constant tables per selection layout (omf_plan_access::
+// topk_table, keyed by the ratio; topk_table_counts, keyed by a received message's per-tensor
+// counts): koff[nt + 1] (int64: each tensor's first value), cap_base[nsuper + 1] (uint32: the
+// tiled decode's bucket-capacity prefix) and blk_t (per place block: its first and last tensor).
+// Caller workspace of the tiled zero-fill decode: fill[nsuper] + the overflow count (left zero by
+// every call), the buckets (cap_base[nsuper] entries) and the overflow list (ktot).
 struct DecTables {
   int64_t* koff = nullptr;
   uint32_t* cap_base = nullptr;
@@ -2236,22 +2269,38 @@ struct DecTables {
   uint64_t cap_total = 0;
 };
 
-static int64_t decode_ktot(const omf_plan* plan, double ratio) {
-  int64_t ktot = 0;
-  for (int64_t n : omf_plan_access::sizes(plan)) {
-    const int64_t k = omf_topk_k(n, ratio);
-    if (k > n) return -1;
-    ktot += k;
+// k_t of every tensor at `ratio` (omf_topk_k); false when some k_t > n_t.
+static bool ratio_counts(const omf_plan* plan, double ratio, std::vector<int64_t>& ks) {
+  const std::vector<int64_t>& sizes = omf_plan_access::sizes(plan);
+  ks.resize(sizes.size());
+  for (size_t t = 0; t < sizes.size(); ++t) {
+    ks[t] = omf_topk_k(sizes[t], ratio);
+    if (ks[t] > sizes[t]) return false;
   }
-  return ktot;
+  return true;
+}
+
+// Explicit counts: 0 <= counts[t] <= n_t (a received selection of more values than its tensor
+// has elements would need duplicates; the caller decodes such a layer on its own).
+static int check_counts(const omf_plan* plan, const int64_t* counts, int64_t* ktot) {
+  if (!counts) return fail(OMF_EINVAL, "counts is NULL");
+  const std::vector<int64_t>& sizes = omf_plan_access::sizes(plan);
+  int64_t s = 0;
+  for (size_t t = 0; t < sizes.size(); ++t) {
+    if (counts[t] < 0 || counts[t] > sizes[t])
+      return fail(OMF_EINVAL, "counts[t] must be in [0, sizes[t]] (tensor " + std::to_string(t) + ")");
+    s += counts[t];
+  }
+  *ktot = s;
+  return OMF_OK;
 }
 
 // Host computation of the tables (also sizes the workspace): bucket capacity = 2 x the
 // expected count of the super-tile (each tensor's k spread over its elements) + 256.
 static int64_t dec_place_blocks(int64_t ktot) { return std::max<int64_t>(1, (ktot + kDecChunk - 1) / kDecChunk); }
 
-static void dec_tables_host(const omf_plan* p, double ratio, std::vector<int64_t>& koff, std::vector<uint32_t>& cap_base,
-                            int32_t& nsuper, std::vector<uint32_t>* blk_t = nullptr) {
+static void dec_tables_host(const omf_plan* p, const int64_t* ks, std::vector<int64_t>& koff,
+                            std::vector<uint32_t>& cap_base, int32_t& nsuper, std::vector<uint32_t>* blk_t = nullptr) {
   const std::vector<int64_t>& sizes = omf_plan_access::sizes(p);
   const int32_t nt = (int32_t)sizes.size();
   const int64_t ae = omf_plan_access::arena_end(p);
@@ -2260,8 +2309,9 @@ static void dec_tables_host(const omf_plan* p, double ratio, std::vector<int64_t
   std::vector<double> expect((size_t)nsuper, 0.0);
   const std::vector<int64_t>& begins = omf_plan_access::offsets(p);
   for (int32_t t = 0; t < nt; ++t) {
-    const int64_t n = sizes[t], k = omf_topk_k(n, ratio);
+    const int64_t n = sizes[t], k = ks[t];
     koff[(size_t)t + 1] = koff[(size_t)t] + k;
+    if (n <= 0 || k <= 0) continue;
     const int64_t begin = begins[t];
     const double dens = (double)k / (double)n;
     for (int64_t s0 = begin >> kDecSuperBits; s0 <= (begin + n - 1) >> kDecSuperBits; ++s0) {
@@ -2308,19 +2358,20 @@ static uint64_t ratio_key(double ratio) {
   return k;
 }
 
-// The plan's tables for `ratio` (computed and uploaded on first use; the bucket total is
-// kept in the table's host word).
-static int dec_tables(omf_plan* p, double ratio, DecTables* out) {
+// The plan's tables for the layout ks (computed and uploaded on first use; the bucket total is
+// kept in the table's host word).  ratio != NULL: keyed by the ratio, else by the counts.
+static int dec_tables(omf_plan* p, const int64_t* ks, int64_t ktot, const double* ratio, DecTables* out) {
   const int32_t nt = omf_plan_access::ntensors(p);
   const int64_t ae = omf_plan_access::arena_end(p);
   const int32_t nsuper = (int32_t)((ae + (1 << kDecSuperBits) - 1) >> kDecSuperBits);
-  const int64_t nb = dec_place_blocks(decode_ktot(p, ratio));
+  const int64_t nb = dec_place_blocks(ktot);
   const size_t o_cap = align256(8 * ((size_t)nt + 1)), o_blk = o_cap + align256(4 * ((size_t)nsuper + 1));
   const size_t bytes = o_blk + 8 * (size_t)nb;
   bool fresh = false;
   uint64_t* host = nullptr;
-  void* d = omf_plan_access::topk_table(p, ratio_key(ratio), bytes, &fresh, &host);
-  if (!d) return fail(OMF_ENOMEM, "omf_topk_decode_arena: table allocation failed");
+  void* d = ratio ? omf_plan_access::topk_table(p, ratio_key(*ratio), bytes, &fresh, &host)
+                  : omf_plan_access::topk_table_counts(p, ks, bytes, &fresh, &host);
+  if (!d) return fail(OMF_ENOMEM, "Top-K decode: table allocation failed");
   out->koff = static_cast<int64_t*>(d);
   out->cap_base = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d) + o_cap);
   out->blk_t = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d) + o_blk);
@@ -2329,7 +2380,7 @@ static int dec_tables(omf_plan* p, double ratio, DecTables* out) {
     std::vector<int64_t> koff;
     std::vector<uint32_t> cap_base, blk_t;
     int32_t ns = 0;
-    dec_tables_host(p, ratio, koff, cap_base, ns, &blk_t);
+    dec_tables_host(p, ks, koff, cap_base, ns, &blk_t);
     OMF_HIP(hipMemcpy(out->koff, koff.data(), 8 * koff.size(), hipMemcpyHostToDevice));
     OMF_HIP(hipMemcpy(out->cap_base, cap_base.data(), 4 * cap_base.size(), hipMemcpyHostToDevice));
     OMF_HIP(hipMemcpy(out->blk_t, blk_t.data(), 4 * blk_t.size(), hipMemcpyHostToDevice));
@@ -2339,15 +2390,69 @@ static int dec_tables(omf_plan* p, double ratio, DecTables* out) {
   return OMF_OK;
 }
 
-size_t omf_topk_decode_workspace_bytes(const omf_plan* plan, double ratio) {
-  if (!plan || !(ratio == ratio)) return 0;
-  const int64_t ktot = decode_ktot(plan, ratio);
-  if (ktot < 0) return 0;
+static size_t dec_ws_bytes(const omf_plan* plan, const int64_t* ks, int64_t ktot) {
   std::vector<int64_t> koff;
   std::vector<uint32_t> cap_base;
   int32_t nsuper = 0;
-  dec_tables_host(plan, ratio, koff, cap_base, nsuper);
+  dec_tables_host(plan, ks, koff, cap_base, nsuper);
   return dec_ws_layout(nsuper, cap_base.back(), ktot).total;
+}
+
+// One client's whole selection in the layout ks into the arena y (modes 0 / 1 / 2).
+static int decode_layout(omf_plan* plan, const int64_t* ks, int64_t ktot, const double* ratio, const float* values,
+                         const int64_t* indices, float* y, int32_t mode, void* ws, size_t ws_bytes, void* stream) {
+  if (mode < 0 || mode > 2) return fail(OMF_EINVAL, "Top-K arena decode: mode must be 0, 1 or 2");
+  if ((ktot && (!values || !indices)) || !y) return fail(OMF_EINVAL, "Top-K arena decode: NULL buffer");
+  const int32_t nt = omf_plan_access::ntensors(plan);
+  if (nt > kArenaMaxTensors) return fail(OMF_EINVAL, "Top-K arena decode: too many tensors (decode per tensor)");
+  DeviceGuard g(omf_plan_access::device(plan));
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t ae = omf_plan_access::arena_end(plan);
+  DecTables tb;
+  if (int r = dec_tables(plan, ks, ktot, ratio, &tb)) return r;
+  if (mode == 0 && ws && ((ae + (1 << kDecSuperBits) - 1) >> kDecSuperBits) <= kDecMaxSuper) {
+    // one streaming write of the arena (larger arenas: fill + scatter below)
+    const DecWs d = dec_ws_layout(tb.nsuper, tb.cap_total, ktot);
+    if (ws_bytes < d.total) return fail(OMF_EINVAL, "Top-K arena decode: workspace too small");
+    if (((uintptr_t)ws & 255) || ((uintptr_t)y & 15)) return fail(OMF_EINVAL, "Top-K arena decode: misaligned buffer");
+    uint8_t* w = static_cast<uint8_t*>(ws);
+    uint32_t* fill = reinterpret_cast<uint32_t*>(w + d.fill);
+    uint32_t* ovf_cnt = fill + tb.nsuper;
+    uint64_t* pairs = reinterpret_cast<uint64_t*>(w + d.pairs);
+    uint64_t* ovf = reinterpret_cast<uint64_t*>(w + d.ovf);
+    // fill[] and the overflow count start at zero (a zero-filled workspace) and every call leaves
+    // them so: topk_dec_tiles clears its bucket's count, topk_dec_overflow the overflow count (a
+    // memset here was two fill kernels, ~10 us per decode)
+    if (ktot > 0) {
+      const dim3 gb((unsigned)dec_place_blocks(ktot));
+      hipLaunchKernelGGL(topk_dec_place, gb, dim3(kThreads), 4 * (size_t)tb.nsuper, st, values, indices,
+                         omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (const int64_t*)tb.koff,
+                         (const uint32_t*)tb.blk_t, ktot, (const uint32_t*)tb.cap_base, fill, pairs, ovf_cnt, ovf);
+    }
+    hipLaunchKernelGGL(topk_dec_tiles, dim3((unsigned)tb.nsuper), dim3(kDecTileThreads), 0, st, (const uint64_t*)pairs,
+                       (const uint32_t*)tb.cap_base, fill, y, ae);
+    if (ktot > 0) hipLaunchKernelGGL(topk_dec_overflow, dim3(1), dim3(kThreads), 0, st, ovf_cnt, (const uint64_t*)ovf, y);
+    OMF_HIP(hipGetLastError());
+    return OMF_OK;
+  }
+  if (mode == 0) OMF_HIP(hipMemsetAsync(y, 0, 4 * (size_t)ae, st));
+  if (ktot == 0) return OMF_OK;
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ktot + kThreads - 1) / kThreads, 4096));
+  hipLaunchKernelGGL(topk_scatter_arena, dim3(gx), dim3(kThreads), 0, st, values, indices,
+                     omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (const int64_t*)tb.koff, (int)nt,
+                     ktot, y, mode == 2 ? 1 : 0);
+  OMF_HIP(hipGetLastError());
+  return OMF_OK;
+}
+
+size_t omf_topk_decode_workspace_bytes(const omf_plan* plan, double ratio) {
+  if (!plan || !(ratio == ratio)) return 0;
+  std::vector<int64_t> ks;
+  if (!ratio_counts(plan, ratio, ks)) return 0;
+  int64_t ktot = 0;
+  for (int64_t k : ks) ktot += k;
+  return dec_ws_bytes(plan, ks.data(), ktot);
 }
 
 int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
@@ -2358,47 +2463,48 @@ int omf_topk_decode_arena(omf_plan* plan, double ratio, const float* values, con
 int omf_topk_decode_arena_ws(omf_plan* plan, double ratio, const float* values, const int64_t* indices, float* y,
                              int32_t mode, void* ws, size_t ws_bytes, void* stream) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
-  if (mode < 0 || mode > 2) return fail(OMF_EINVAL, "omf_topk_decode_arena: mode must be 0, 1 or 2");
   if (!(ratio == ratio)) return fail(OMF_EINVAL, "ratio is NaN");
-  if (!values || !indices || !y) return fail(OMF_EINVAL, "omf_topk_decode_arena: NULL buffer");
+  std::vector<int64_t> ks;
+  if (!ratio_counts(plan, ratio, ks))
+    return fail(OMF_EINVAL, "selected index k out of range (k > numel): compress_ratio too large");
+  int64_t ktot = 0;
+  for (int64_t k : ks) ktot += k;
+  return decode_layout(plan, ks.data(), ktot, &ratio, values, indices, y, mode, ws, ws_bytes, stream);
+}
+
+size_t omf_topk_decode_counts_workspace_bytes(const omf_plan* plan, const int64_t* counts) {
+  if (!plan || !counts) return 0;
+  int64_t ktot = 0;
+  if (check_counts(plan, counts, &ktot)) return 0;
+  return dec_ws_bytes(plan, counts, ktot);
+}
+
+int omf_topk_decode_counts(omf_plan* plan, const int64_t* counts, const float* values, const int64_t* indices, float* y,
+                           int32_t mode, void* ws, size_t ws_bytes, void* stream) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  int64_t ktot = 0;
+  if (int r = check_counts(plan, counts, &ktot)) return r;
+  return decode_layout(plan, counts, ktot, nullptr, values, indices, y, mode, ws, ws_bytes, stream);
+}
+
+int omf_topk_check_indices(omf_plan* plan, const int64_t* counts, int64_t* indices, int32_t* bad, void* stream) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (!bad) return fail(OMF_EINVAL, "omf_topk_check_indices: bad is NULL");
+  int64_t ktot = 0;
+  if (int r = check_counts(plan, counts, &ktot)) return r;
+  if (ktot && !indices) return fail(OMF_EINVAL, "omf_topk_check_indices: indices is NULL");
   const int32_t nt = omf_plan_access::ntensors(plan);
-  if (nt > kArenaMaxTensors) return fail(OMF_EINVAL, "omf_topk_decode_arena: too many tensors (decode per tensor)");
-  const int64_t ktot = decode_ktot(plan, ratio);
-  if (ktot < 0) return fail(OMF_EINVAL, "selected index k out of range (k > numel): compress_ratio too large");
+  if (nt > kArenaMaxTensors) return fail(OMF_EINVAL, "omf_topk_check_indices: too many tensors");
   DeviceGuard g(omf_plan_access::device(plan));
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   hipStream_t st = (hipStream_t)stream;
-  const int64_t ae = omf_plan_access::arena_end(plan);
-  if (mode == 0 && ws && ((ae + (1 << kDecSuperBits) - 1) >> kDecSuperBits) <= kDecMaxSuper) {
-    // one streaming write of the arena (larger arenas: fill + scatter below)
-    DecTables tb;
-    if (int r = dec_tables(plan, ratio, &tb)) return r;
-    const DecWs d = dec_ws_layout(tb.nsuper, tb.cap_total, ktot);
-    if (ws_bytes < d.total) return fail(OMF_EINVAL, "omf_topk_decode_arena: workspace too small");
-    if (((uintptr_t)ws & 255) || ((uintptr_t)y & 15)) return fail(OMF_EINVAL, "omf_topk_decode_arena: misaligned buffer");
-    uint8_t* w = static_cast<uint8_t*>(ws);
-    uint32_t* fill = reinterpret_cast<uint32_t*>(w + d.fill);
-    uint32_t* ovf_cnt = fill + tb.nsuper;
-    uint64_t* pairs = reinterpret_cast<uint64_t*>(w + d.pairs);
-    uint64_t* ovf = reinterpret_cast<uint64_t*>(w + d.ovf);
-    // fill[] and the overflow count start at zero (a zero-filled workspace) and every call leaves
-    // them so: topk_dec_tiles clears its bucket's count, topk_dec_overflow the overflow count (a
-    // memset here was two fill kernels, ~10 us per decode)
-    const dim3 gb((unsigned)dec_place_blocks(ktot));
-    hipLaunchKernelGGL(topk_dec_place, gb, dim3(kThreads), 4 * (size_t)tb.nsuper, st, values, indices,
-                       omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (const int64_t*)tb.koff,
-                       (const uint32_t*)tb.blk_t, ktot, (const uint32_t*)tb.cap_base, fill, pairs, ovf_cnt, ovf);
-    hipLaunchKernelGGL(topk_dec_tiles, dim3((unsigned)tb.nsuper), dim3(kDecTileThreads), 0, st, (const uint64_t*)pairs,
-                       (const uint32_t*)tb.cap_base, fill, y, ae);
-    hipLaunchKernelGGL(topk_dec_overflow, dim3(1), dim3(kThreads), 0, st, ovf_cnt, (const uint64_t*)ovf, y);
-    OMF_HIP(hipGetLastError());
-    return OMF_OK;
-  }
-  if (mode == 0) OMF_HIP(hipMemsetAsync(y, 0, 4 * (size_t)ae, st));
-  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ktot + kThreads - 1) / kThreads, 4096));
-  hipLaunchKernelGGL(topk_scatter_arena, dim3(gx), dim3(kThreads), 0, st, values, indices,
-                     omf_plan_access::d_sizes(plan), omf_plan_access::d_begins(plan), (int)nt, ratio, ktot, y,
-                     mode == 2 ? 1 : 0);
+  DecTables tb;
+  if (int r = dec_tables(plan, counts, ktot, nullptr, &tb)) return r;
+  OMF_HIP(hipMemsetAsync(bad, 0x7f, 4, st));  // 0x7f7f7f7f: no tensor
+  if (ktot == 0) return OMF_OK;
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ktot + 4 * kThreads - 1) / (4 * kThreads), 2048));
+  hipLaunchKernelGGL(topk_check_idx, dim3(gx), dim3(kThreads), 0, st, indices, omf_plan_access::d_sizes(plan),
+                     (const int64_t*)tb.koff, (int)nt, ktot, bad);
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }

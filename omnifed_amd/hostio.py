@@ -26,11 +26,13 @@ import ctypes
 import os
 import threading
 from concurrent.futures import ThreadPoolExecutor
+from contextlib import contextmanager
 from typing import Callable, Dict, Iterator, List, Optional, Sequence, Tuple
 
 import torch
 
 CHUNK_BYTES = 32 << 20
+INLINE_BYTES = 1 << 20  # a copy this small is done on the calling thread (a pool hand-off costs more)
 
 _new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
 _new_bytes.restype = ctypes.py_object
@@ -112,20 +114,57 @@ def retain_host_memory(mmap_threshold: int = 32 << 20, trim_threshold: int = 1 <
 
 
 class PinnedStaging:
-    """Reusable page-locked host buffers (one per purpose), grown on demand.  A caller finishes
-    with a buffer (its copies have landed) before the next call reuses it."""
+    """Reusable page-locked host buffers, per purpose (``key``), grown on demand.
+
+    ``lease(key, nbytes)`` hands out a buffer no other caller holds until the lease ends: the
+    reference PS runs the codec on gRPC worker threads (``ThreadPoolExecutor(max_workers=10)``,
+    global_grpc.py:44-45), and a client and the PS may share one process, so two calls may stage
+    at once — each gets its own buffer (a key's pool grows to the number of concurrent users:
+    one under the servicer's lock).  A caller finishes with a buffer (its copies have landed)
+    before its lease ends."""
 
     def __init__(self):
-        self._bufs: Dict[str, torch.Tensor] = {}
+        self._free: Dict[str, List[tuple]] = {}  # key -> [(buffer, event its last copies completed by)]
         self._lock = threading.Lock()
 
-    def get(self, key: str, nbytes: int) -> torch.Tensor:
+    @contextmanager
+    def lease(self, key: str, nbytes: int) -> Iterator["Lease"]:
+        nbytes = max(int(nbytes), 1)
         with self._lock:
-            b = self._bufs.get(key)
-            if b is None or b.numel() < nbytes:
-                b = torch.empty(max(int(nbytes), 4096), dtype=torch.uint8, pin_memory=True)
-                self._bufs[key] = b
-            return b[:nbytes]
+            pool = self._free.setdefault(key, [])
+            pick = None
+            for i, (c, _) in enumerate(pool):  # the smallest free buffer that fits, else the largest (regrown)
+                if c.numel() >= nbytes and (pick is None or c.numel() < pool[pick][0].numel()):
+                    pick = i
+            buf, ev = pool.pop(pick) if pick is not None else (pool.pop() if pool else (None, None))
+        if ev is not None:
+            ev.synchronize()  # the previous holder's copies out of the buffer have landed
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 4096), dtype=torch.uint8, pin_memory=True)
+        h = Lease(buf[:nbytes])
+        try:
+            yield h
+        finally:
+            with self._lock:
+                self._free.setdefault(key, []).append((buf, h.event))
+                self._free[key].sort(key=lambda e: e[0].numel())
+
+    def get(self, key: str, nbytes: int) -> torch.Tensor:
+        """A buffer for single-threaded callers that finish with it before their next call (tests,
+        tools); product paths take a ``lease``."""
+        with self.lease(key, nbytes) as h:
+            return h.buf
+
+
+class Lease:
+    """A leased staging buffer; ``event``: set by a holder whose copies out of the buffer are
+    still queued when the lease ends (the next holder waits for it)."""
+
+    __slots__ = ("buf", "event")
+
+    def __init__(self, buf: torch.Tensor):
+        self.buf = buf
+        self.event = None
 
 
 STAGING = PinnedStaging()
@@ -167,7 +206,11 @@ def fill_bytes(base: int, spans: Sequence[Tuple[int, int]], landed: Callable[[in
             if n <= 0:
                 continue
             obj = _new_bytes(None, n)
-            filled.append((i, obj, ex.submit(ctypes.memmove, _bytes_addr(obj), base + off, n)))
+            if n < INLINE_BYTES:
+                ctypes.memmove(_bytes_addr(obj), base + off, n)
+                filled.append((i, obj, _Inline._Done(None)))
+            else:
+                filled.append((i, obj, ex.submit(ctypes.memmove, _bytes_addr(obj), base + off, n)))
         for item in pending:  # the previous chunk, while this one is copied
             item[2].result()
             yield item[0], item[1]
@@ -187,16 +230,20 @@ def device_to_bytes(src: torch.Tensor, spans: Sequence[Tuple[int, int]], stream=
         stream = torch.cuda.current_stream(src.device)
     raw = src.reshape(-1).view(torch.uint8)
     total = max((off + n for off, n in spans), default=0)
-    staged = STAGING.get(key, max(total, 1))
-    events = []
-    with torch.cuda.stream(stream):
-        for a, b, _ in _groups(spans, limit):
-            if b > a:
-                staged[a:b].copy_(raw[a:b], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            events.append(ev)
-    yield from fill_bytes(staged.data_ptr(), spans, lambda g: events[g].synchronize(), limit)
+    with STAGING.lease(key, max(total, 1)) as h:
+        staged = h.buf
+        events = []
+        with torch.cuda.stream(stream):
+            for a, b, _ in _groups(spans, limit):
+                if b > a:
+                    staged[a:b].copy_(raw[a:b], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(stream)
+                events.append(ev)
+        try:
+            yield from fill_bytes(staged.data_ptr(), spans, lambda g: events[g].synchronize(), limit)
+        finally:
+            events[-1].synchronize() if events else None  # an abandoned generator: the copies land first
 
 
 def stage_payloads(items: Sequence[Tuple[int, Callable[[], bytes]]], base: int, total_bytes: int,
@@ -235,7 +282,9 @@ def stage_payloads(items: Sequence[Tuple[int, Callable[[], bytes]]], base: int, 
                 if prev is not None:
                     close(prev)
                 prev, ga, gb, futs, held = (ga, gb, futs, held), off, off, [], []
-            if n:
+            if 0 < n < INLINE_BYTES:
+                ctypes.memmove(base + off, _bytes_addr(p), n)
+            elif n:
                 f = ex.submit(ctypes.memmove, base + off, _bytes_addr(p), n)
                 futs.append(f)
                 started.append(f)
@@ -254,16 +303,21 @@ def stage_payloads(items: Sequence[Tuple[int, Callable[[], bytes]]], base: int, 
 def bytes_to_device(items: Sequence[Tuple[int, Callable[[], bytes]]], dst: torch.Tensor, total_bytes: int,
                     stream=None, key: str = "decode", limit: int = CHUNK_BYTES,
                     check: Optional[Callable[[int, bytes], None]] = None) -> None:
-    """``stage_payloads`` into pinned staging, each chunk's host-to-device copy into the device
-    buffer ``dst`` queued on ``stream`` as soon as the chunk is complete.  Returns once the last
-    copy is queued; the caller synchronises the stream before the staging is reused."""
+    """``stage_payloads`` into pinned staging (a lease), each chunk's host-to-device copy into the
+    device buffer ``dst`` queued on ``stream`` as soon as the chunk is complete.  Returns once the
+    last copy is queued (the staging goes back to its pool with an event the next holder waits for)."""
     if stream is None:
         stream = torch.cuda.current_stream(dst.device)
     raw = dst.reshape(-1).view(torch.uint8)
-    staged = STAGING.get(key, max(int(total_bytes), 1))
+    with STAGING.lease(key, max(int(total_bytes), 1)) as h:
+        staged = h.buf
 
-    def flush(a: int, b: int) -> None:
-        with torch.cuda.stream(stream):
-            raw[a:b].copy_(staged[a:b], non_blocking=True)
+        def flush(a: int, b: int) -> None:
+            with torch.cuda.stream(stream):
+                raw[a:b].copy_(staged[a:b], non_blocking=True)
 
-    stage_payloads(items, staged.data_ptr(), total_bytes, flush, limit, check)
+        try:
+            stage_payloads(items, staged.data_ptr(), total_bytes, flush, limit, check)
+        finally:
+            h.event = torch.cuda.Event()  # the next holder waits for these copies
+            h.event.record(stream)

@@ -40,7 +40,7 @@ from ..compression.qsgd import (
     choose_qsgd_storage_width,
     should_compress_tensor,
 )
-from ..compression.topk import TOPK_COMPRESSION_NAME, TopKCompression
+from ..compression.topk import TOPK_COMPRESSION_NAME, TopKCompression, topk_index_offset
 from ..compression.core import compute_device
 from ... import codec, hostio
 
@@ -173,6 +173,18 @@ def topk_layer_from_payload(name: str, shape, values: np.ndarray, indices: np.nd
     layer.compression_type = TOPK_COMPRESSION_NAME
     layer.values_data = np.ascontiguousarray(values, dtype=np.float32).tobytes()
     layer.indices_data = np.ascontiguousarray(indices, dtype=np.int64).tobytes()
+    layer.values_dtype = "torch.float32"
+    layer.indices_dtype = "torch.int64"
+    layer.original_shape.extend(list(shape))
+    return layer
+
+
+def topk_layer_from_bytes(name: str, shape, values: bytes, indices: bytes):
+    """``topk_layer_from_payload`` from the payload bytes themselves (fp32 values, int64 indices)."""
+    layer = global_grpc_pb2.layer_state(layer_name=name)
+    layer.compression_type = TOPK_COMPRESSION_NAME
+    layer.values_data = values
+    layer.indices_data = indices
     layer.values_dtype = "torch.float32"
     layer.indices_dtype = "torch.int64"
     layer.original_shape.extend(list(shape))
@@ -400,7 +412,81 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
     return layers
 
 
+def _topk_batchable(tensors) -> bool:
+    """The batched Top-K path takes non-empty fp32 tensors (others: the per-layer path)."""
+    return bool(tensors) and all(isinstance(t, torch.Tensor) and t.dtype == torch.float32 and t.numel() > 0
+                                 for t in tensors)
+
+
+def _encode_topk_updates(updates, compressor: TopKCompression, weight) -> list:
+    """Every tensor of the dict in ONE Top-K encode (``TopKCompression.encode_arena``: error
+    feedback for each name, the client weighting fused), then one chunked device-to-host copy of
+    the (values, indices) buffer through pinned staging, each layer's ``bytes`` filled by worker
+    threads (hostio.device_to_bytes).  Same LayerStates as the per-layer loop of
+    global_grpc_compression.py:84-98 / 207-211 (the selection does not depend on the batching)."""
+    names = list(updates.keys())
+    flats = [updates[n].detach().reshape(-1) for n in names]
+    plan, values, indices, ks = compressor.encode_arena(names, flats, _alpha(weight))
+    nt = len(names)
+    koff = [0]
+    for k in ks:
+        koff.append(koff[-1] + k)
+    io = topk_index_offset(koff[-1])
+    spans = [(4 * koff[t], 4 * ks[t]) for t in range(nt)] + [(io + 8 * koff[t], 8 * ks[t]) for t in range(nt)]
+    buf = values.untyped_storage()
+    src = torch.empty(0, dtype=torch.uint8, device=values.device).set_(buf, values.storage_offset() * 4,
+                                                                         (io + 8 * koff[-1],))
+    layers: List = [None] * nt
+    vals: List[Optional[bytes]] = [None] * nt
+    for i, payload in hostio.device_to_bytes(src, spans, key="topk_encode"):
+        if i < nt:
+            vals[i] = payload
+        else:
+            t = i - nt
+            layers[t] = topk_layer_from_bytes(names[t], tuple(updates[names[t]].shape), vals[t], payload)
+            vals[t] = None
+    return layers
+
+
+def qsgd_layers_from_arena(plan, q: torch.Tensor, norms: torch.Tensor, names, shapes, levels: int,
+                           packed: bool = False, stream=None) -> list:
+    """The QSGD ``LayerState``s of an encoded payload arena (plan order): the norms copied first,
+    then the payload arena device-to-host in chunks through pinned staging, each chunk's ``bytes``
+    filled by worker threads while the previous chunk's LayerStates are built
+    (hostio.device_to_bytes; protobuf copies the bytes into its message).  ``packed``: the opt-in
+    bit-packed wire, packed on the GPU first.  A zero-norm tensor gets ``None`` (the caller emits
+    the reference's dense passthrough); an in-kernel encoder timeout raises."""
+    stream = torch.cuda.current_stream(plan.device) if stream is None else stream
+    width, _ = choose_qsgd_storage_width(levels)
+    with _STAGING.lease("encode_norms", 4 * plan.nt) as h:
+        nh = h.buf.view(torch.float32)
+        with torch.cuda.stream(stream):
+            nh.copy_(norms[:plan.nt], non_blocking=True)  # queued before the payload chunks: it lands first
+        ev = torch.cuda.Event()
+        ev.record(stream)
+        if packed:  # pack on the GPU; (b/8) bytes per element cross PCIe
+            src = plan.qsgd_pack(q, width, levels, stream=stream.cuda_stream)
+            b = codec.packed_bits(levels)
+            spans = [(o * b // 8, (n * b + 7) // 8) for o, n in zip(plan.offsets, plan.sizes)]
+        else:  # the payload arena: w bytes per element
+            src, isz = q, q.element_size()
+            spans = [(o * isz, n * isz) for o, n in zip(plan.offsets, plan.sizes)]
+        ev.synchronize()
+        host_norms = nh.tolist()
+    spans = [(off, ln if nv != 0 else 0) for (off, ln), nv in zip(spans, host_norms)]  # zero norm: dense
+    layers: List = [None] * plan.nt
+    for k, payload in hostio.device_to_bytes(src, spans, stream=stream):
+        if packed:
+            layers[k] = qsgd_packed_layer_from_payload(names[k], shapes[k], payload, host_norms[k], levels)
+        else:
+            layers[k] = qsgd_layer_from_payload(names[k], shapes[k], payload, host_norms[k], width, levels)
+    plan.check(stream.cuda_stream)  # an in-kernel timeout raises: the payload would be invalid
+    return layers
+
+
 def _encode_updates(updates, compressor, weight) -> list:
+    if isinstance(compressor, TopKCompression) and _topk_batchable(list(updates.values())):
+        return _encode_topk_updates(updates, compressor, weight)
     if not isinstance(compressor, QSGDQuantCompression):
         return [encode_layer_state(name, tensor, compressor, weight=weight) for name, tensor in updates.items()]
     names = list(updates.keys())
@@ -416,34 +502,12 @@ def _encode_updates(updates, compressor, weight) -> list:
         groups = encode_groups(flats, compressor.s, dev, compressor.rng, compressor._next_call(),
                                alpha=_alpha(weight), key=compressor.philox_key())
         levels = 2**compressor.s
-        width, _ = choose_qsgd_storage_width(levels)
         for plan, q, norms, members in groups:  # one group per dtype (normally one)
             idx = [comp_idx[m] for m in members]
-            stream = torch.cuda.current_stream(dev)
-            nh = _STAGING.get("encode_norms", 4 * plan.nt).view(torch.float32)
-            nh.copy_(norms, non_blocking=True)  # queued before the payload chunks: it lands first
-            ev = torch.cuda.Event()
-            ev.record(stream)
-            if compressor.packed_wire:  # pack on the GPU; (b/8) bytes per element cross PCIe
-                src = plan.qsgd_pack(q, width, levels)
-                b = codec.packed_bits(levels)
-                spans = [(o * b // 8, (n * b + 7) // 8) for o, n in zip(plan.offsets, plan.sizes)]
-            else:  # the payload arena: w bytes per element
-                src, isz = q, q.element_size()
-                spans = [(o * isz, n * isz) for o, n in zip(plan.offsets, plan.sizes)]
-            ev.synchronize()
-            host_norms = nh.tolist()
-            spans = [(off, ln if nv != 0 else 0) for (off, ln), nv in zip(spans, host_norms)]  # zero norm: dense
-            # chunked D2H; each chunk's bytes filled by worker threads while the previous chunk's
-            # LayerStates are built (protobuf copies the bytes into its message)
-            for k, payload in hostio.device_to_bytes(src, spans, stream=stream):
-                i = idx[k]
-                t = updates[names[i]]
-                if compressor.packed_wire:
-                    layers[i] = qsgd_packed_layer_from_payload(names[i], tuple(t.shape), payload, host_norms[k], levels)
-                else:
-                    layers[i] = qsgd_layer_from_payload(names[i], tuple(t.shape), payload, host_norms[k], width, levels)
-            plan.check()  # an in-kernel timeout raises: the payload would be invalid
+            got = qsgd_layers_from_arena(plan, q, norms, [names[i] for i in idx],
+                                         [tuple(updates[names[i]].shape) for i in idx], levels, compressor.packed_wire)
+            for i, L in zip(idx, got):
+                layers[i] = L
     for i, name in enumerate(names):
         if layers[i] is None:
             layers[i] = _encode_dense_layer(name, _weighted(updates[name], weight))
@@ -477,37 +541,112 @@ def _decode_qsgd_batch(layers, dev: torch.device):
         items = [(o * isz, (lambda L=L: L.values_data)) for L, o in zip(layers, plan.offsets)]
         hostio.bytes_to_device(items, qd, isz * plan.arena_end, check=lambda i, p: _check_qsgd_payload(layers[i], p))
         y = plan.qsgd_decode(qd, width, level, nd)
-    # the staging buffer is reused by the next call: make sure this copy has been consumed
-    torch.cuda.current_stream(dev).synchronize()
-    return y, plan
+    return y, plan  # stream-ordered (the staging's lease carries the event its copies complete by)
+
+
+def read_topk_layer(layer):
+    """The Top-K layer's payloads, checked as the reference's decoder checks them before any
+    work (global_grpc_compression.py:145-146; np.frombuffer raises ValueError on a size that is
+    not a whole number of elements, the fancy assignment on a length mismatch): ``(values bytes,
+    indices bytes, k)``.  Each payload is read once (protobuf copies a bytes field on every read)."""
+    v = layer.values_data
+    i = layer.indices_data
+    if not v or not i:
+        raise ValueError(f"Compressed layer {layer.layer_name!r} missing values/indices")
+    if len(v) % 4 or len(i) % 8:
+        raise ValueError(f"Compressed layer {layer.layer_name!r}: buffer size must be a multiple of element size")
+    if len(v) // 4 != len(i) // 8:
+        raise ValueError(f"Compressed layer {layer.layer_name!r}: {len(v) // 4} values, {len(i) // 8} indices")
+    return v, i, len(v) // 4
 
 
 def _validate_layer(layer):
     """The checks decode_layer_tensor makes before any work (global_grpc_compression.py:
-    145-146, 164-171, 193-194, 204), so a batched decode raises for the same first layer."""
+    145-146, 164-171, 193-194, 204), so a batched decode raises for the same first layer.
+    Returns the Top-K payloads (read_topk_layer) for a Top-K layer, else None."""
     ct = layer.compression_type or ""
     if ct == "":
         if not layer.param_shape:
             raise ValueError(f"Dense layer {layer.layer_name!r} missing param_shape")
     elif ct == TOPK_COMPRESSION_NAME:
-        if not layer.values_data or not layer.indices_data:
-            raise ValueError(f"Compressed layer {layer.layer_name!r} missing values/indices")
+        return read_topk_layer(layer)
     elif ct == QSGD_COMPRESSION_NAME:
         _check_qsgd_fields(layer)  # the payload's size: checked as it is staged (_decode_qsgd_batch)
     elif ct == QSGD_PACKED_COMPRESSION_NAME:
         _check_packed_fields(layer)
     else:
         raise ValueError(f"Unsupported compression_type={ct!r}")
+    return None
 
 
-def _qsgd_groups(proto_layers):
-    """Validate every layer in message order; QSGD layers grouped by (type, width, level)."""
+def _scan_layers(proto_layers):
+    """Validate every layer in message order.  Returns the QSGD layers grouped by (type, width,
+    level) and the Top-K layers with their payloads ``[(layer, values, indices, k)]``."""
     groups: Dict[tuple, list] = {}
+    topk: List[tuple] = []
     for L in proto_layers:
-        _validate_layer(L)
-        if L.compression_type in _QSGD_TYPES:
+        got = _validate_layer(L)
+        if got is not None:
+            topk.append((L, *got))
+        elif L.compression_type in _QSGD_TYPES:
             groups.setdefault((L.compression_type, L.width, L.level), []).append(L)
-    return groups
+    return groups, topk
+
+
+def _layer_numel(layer) -> int:
+    return int(np.prod(tuple(layer.original_shape)))
+
+
+def _topk_batch_ok(topk) -> bool:
+    """A message's Top-K layers decode in one call when their names are distinct (a repeated
+    name: the reference's dict keeps the last decode) and every k fits its tensor."""
+    names = set()
+    for L, _v, _i, k in topk:
+        n = _layer_numel(L)
+        if n < 1 or k > n or L.layer_name in names:
+            return False
+        names.add(L.layer_name)
+    return True
+
+
+def stage_topk(pairs, dev: torch.device, key: str):
+    """One device buffer holding a message's Top-K selections in plan order — values (fp32) at
+    its start, indices (int64) from ``topk_index_offset(K)`` — through pinned staging in chunks
+    (hostio.bytes_to_device).  ``pairs``: ``[(values bytes, indices bytes)]`` per plan tensor
+    (``(b"", b"")`` for a tensor absent from the message).  Returns ``(counts, values, indices)``
+    (stream-ordered)."""
+    counts = [len(v) // 4 for v, _ in pairs]
+    koff = [0]
+    for k in counts:
+        koff.append(koff[-1] + k)
+    K = koff[-1]
+    io = topk_index_offset(K)
+    buf = torch.empty(max(io + 8 * K, 256), dtype=torch.uint8, device=dev)
+    items = [(4 * koff[t], (lambda v=v: v)) for t, (v, _) in enumerate(pairs)]
+    items += [(io + 8 * koff[t], (lambda i=i: i)) for t, (_, i) in enumerate(pairs)]
+    hostio.bytes_to_device(items, buf, io + 8 * K, key=key)
+    return counts, buf[:4 * K].view(torch.float32), buf[io:io + 8 * K].view(torch.int64)
+
+
+def check_topk_indices(plan, counts, indices, names) -> None:
+    """Wrap negative indices and raise the reference's IndexError for one out of range
+    (omf_topk_check_indices); synchronises the stream."""
+    bad = int(plan.topk_check_indices(counts, indices).item())
+    if bad < plan.nt:
+        raise IndexError(f"Compressed layer {names[bad]!r}: index out of bounds for size {plan.sizes[bad]}")
+
+
+def _decode_topk_batch(topk, dev: torch.device):
+    """Decode a message's Top-K layers (zero-filled, no base) in one call: returns the decoded
+    fp32 arena and the plan (layer t at ``[plan.offsets[t], + plan.sizes[t])``)."""
+    plan = codec.Plan.get([_layer_numel(L) for L, *_ in topk], device=dev)
+    counts, values, indices = stage_topk([(v, i) for _L, v, i, _k in topk], dev, "topk_decode")
+    bad = plan.topk_check_indices(counts, indices)
+    y = plan.topk_decode_counts(counts, values, indices, mode=0)  # out-of-range indices are skipped
+    b = int(bad.item())  # synchronises: the staging is free again
+    if b < plan.nt:
+        raise IndexError(f"Compressed layer {topk[b][0].layer_name!r}: index out of bounds for size {plan.sizes[b]}")
+    return y, plan
 
 
 def decode_updates_dict(proto_layers, *, base_updates: Optional[Dict[str, torch.Tensor]] = None,
@@ -521,7 +660,8 @@ def decode_updates_dict(proto_layers, *, base_updates: Optional[Dict[str, torch.
     proto_layers = list(proto_layers)
     out_dev = _out_device(None, device)
     decoded: Dict[str, torch.Tensor] = {}
-    groups = _qsgd_groups(proto_layers)
+    topk_done = set()
+    groups, topk = _scan_layers(proto_layers)
     if groups:
         dev = _gpu_for(out_dev)
         for layers in groups.values():
@@ -530,9 +670,19 @@ def decode_updates_dict(proto_layers, *, base_updates: Optional[Dict[str, torch.
                 y = y.cpu()  # one D2H for the whole group; returned tensors are views of it
             for L, o, n in zip(layers, plan.offsets, plan.sizes):
                 decoded[L.layer_name] = y[o:o + n].view(tuple(L.original_shape))
+    if base_updates is not None:  # overlays decode layer by layer, on their bases' devices
+        topk = [e for e in topk if e[0].layer_name not in base_updates]
+    if topk and _topk_batch_ok(topk):
+        y, plan = _decode_topk_batch(topk, _gpu_for(out_dev))
+        if out_dev.type == "cpu":
+            y = y.cpu()
+        for (L, *_), o, n in zip(topk, plan.offsets, plan.sizes):
+            decoded[L.layer_name] = y[o:o + n].view(tuple(L.original_shape))
+            topk_done.add(id(L))
     out: Dict[str, torch.Tensor] = {}
     for layer in proto_layers:
-        if layer.layer_name in decoded and layer.compression_type in _QSGD_TYPES:
+        ct = layer.compression_type
+        if layer.layer_name in decoded and (ct in _QSGD_TYPES or (ct == TOPK_COMPRESSION_NAME and id(layer) in topk_done)):
             out[layer.layer_name] = decoded[layer.layer_name]
             continue
         base = None if base_updates is None else base_updates.get(layer.layer_name)
@@ -549,7 +699,10 @@ def decode_updates_into(proto_layers, targets: Dict[str, torch.Tensor]) -> None:
     in place (the reference's overlay-on-a-copy); dense layers are copied.
     """
     proto_layers = [L for L in proto_layers if L.layer_name in targets]
-    groups = _qsgd_groups(proto_layers)
+    groups, topk = _scan_layers(proto_layers)
+    done = set()
+    if topk and _topk_batch_ok(topk):
+        done = _overlay_topk_into(topk, targets)
     for layers in groups.values():
         dev = _gpu_for(targets[layers[0].layer_name].device)
         y, plan = _decode_qsgd_batch(layers, dev)
@@ -557,11 +710,44 @@ def decode_updates_into(proto_layers, targets: Dict[str, torch.Tensor]) -> None:
             t = targets[L.layer_name]
             t.copy_(y[o:o + n].view(tuple(L.original_shape)).to(t.dtype))
     for L in proto_layers:
-        if L.compression_type in _QSGD_TYPES:
+        if L.compression_type in _QSGD_TYPES or id(L) in done:
             continue
         t = targets[L.layer_name]
         dec = decode_layer_tensor(L, base_tensor=t, device=t.device)
         t.copy_(dec.to(t.dtype))
+
+
+def _overlay_topk_into(topk, targets) -> set:
+    """The Top-K part of decode_updates_into: the values set at their indices in each target
+    (the reference's overlay on ``param.data``, global_grpc_client.py:98-111), in place.  Layers
+    whose target is a contiguous fp32 GPU tensor of the layer's size are staged together (one
+    chunked H2D), checked (one index check; an out-of-range index raises before any target is
+    written) and scattered — as one launch when the targets are views of one arena, else one
+    launch per target.  Returns the ids of the layers handled; the caller decodes the rest."""
+    first = targets[topk[0][0].layer_name]
+    if not first.is_cuda:
+        return set()
+    dev = first.device
+    mine = [e for e in topk if (lambda t: t.is_cuda and t.device == dev and t.dtype == torch.float32
+                                and t.is_contiguous() and t.numel() == _layer_numel(e[0]))(targets[e[0].layer_name])]
+    if not mine:
+        return set()
+    names = [L.layer_name for L, *_ in mine]
+    plan = codec.Plan.get([_layer_numel(L) for L, *_ in mine], device=dev)
+    counts, values, indices = stage_topk([(v, i) for _L, v, i, _k in mine], dev, "topk_overlay")
+    check_topk_indices(plan, counts, indices, names)
+    flats = [targets[n].detach().reshape(-1) for n in names]
+    from ..compression.core import shared_arena
+
+    arena = shared_arena(flats, dev, plan)
+    if arena is not None:
+        plan.topk_decode_counts(counts, values, indices, y=arena, mode=1)
+    else:
+        K = 0
+        for f, k in zip(flats, counts):
+            codec.topk_decode(values[K:K + k], indices[K:K + k], f.numel(), y=f, mode=1)
+            K += k
+    return {id(L) for L, *_ in mine}
 
 
 __all__: List[str] = [
@@ -575,7 +761,9 @@ __all__: List[str] = [
     "encode_updates_dict",
     "hybrid_global_compressor_from_cfg",
     "qsgd_layer_from_payload",
+    "qsgd_layers_from_arena",
     "qsgd_packed_layer_from_payload",
+    "topk_layer_from_bytes",
     "topk_layer_from_payload",
     "wire_size",
 ]

@@ -90,6 +90,40 @@ def to_arena(t: torch.Tensor, dev: torch.device, plan: "codec.Plan") -> torch.Te
     return buf
 
 
+def shared_arena(flats, dev: torch.device, plan: "codec.Plan"):
+    """The arena ``flats`` already form, if they do: every flat is a contiguous fp32 view of ONE
+    storage on ``dev`` at ``base + plan.offsets[t]`` (a model's flat gradient buffer, the PS's
+    average arena), 16-byte aligned and long enough for the plan — then that storage is the
+    arena (no copy).  None otherwise."""
+    f0 = flats[0]
+    if f0.dtype != torch.float32 or f0.device != dev:
+        return None
+    st = f0.untyped_storage()
+    sptr = st.data_ptr()
+    base = f0.storage_offset() - plan.offsets[0]
+    if base < 0 or (sptr + 4 * base) % 16 or st.nbytes() < 4 * (base + plan.arena_end):
+        return None
+    for f, o in zip(flats, plan.offsets):
+        if (f.dtype != torch.float32 or not f.is_contiguous() or f.storage_offset() != base + o
+                or f.untyped_storage().data_ptr() != sptr):
+            return None
+    return torch.empty(0, dtype=torch.float32, device=dev).set_(st, base, (plan.arena_end,))
+
+
+def gather_arena(flats, dev: torch.device, plan: "codec.Plan") -> torch.Tensor:
+    """The fp32 update arena of ``flats`` (flat tensors in plan order): the storage they already
+    share (``shared_arena``), else a fresh arena they are copied into (bf16/fp16 -> fp32 exact)."""
+    if len(flats) == 1:
+        return to_arena(flats[0], dev, plan)
+    x = shared_arena(flats, dev, plan)
+    if x is not None:
+        return x
+    x = torch.empty(plan.arena_end, dtype=torch.float32, device=dev)
+    for f, o, n in zip(flats, plan.offsets, plan.sizes):
+        x[o:o + n].copy_(f.detach().reshape(-1))
+    return x
+
+
 def layerwise_decompress(collected_vals, collected_ix, tensor_shape, client_count, device):
     """core.py:62-71 on the GPU: scatter-add every client's (values, indices), then ``/ client_count``."""
     dev = compute_device(collected_vals[0] if collected_vals else torch.empty(0), torch.device(device))

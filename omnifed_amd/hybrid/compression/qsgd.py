@@ -36,7 +36,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import torch
 
 from ... import codec
-from .core import Compression, compute_device, to_arena
+from .core import Compression, compute_device, gather_arena
 
 QSGD_COMPRESSION_NAME = "QSGDQuantCompression"
 # Opt-in bit-packed wire (not reference-compatible): codes q + L in
@@ -68,12 +68,7 @@ def value_format(dtype: torch.dtype) -> int:
 
 
 def _arena(flats: Sequence[torch.Tensor], dev: torch.device, plan) -> torch.Tensor:
-    if len(flats) == 1:
-        return to_arena(flats[0], dev, plan)
-    x = torch.empty(plan.arena_end, dtype=torch.float32, device=dev)
-    for f, o, n in zip(flats, plan.offsets, plan.sizes):
-        x[o:o + n].copy_(f.detach().reshape(-1))  # bf16/fp16 -> fp32 is exact
-    return x
+    return gather_arena(flats, dev, plan)  # bf16/fp16 -> fp32 is exact
 
 
 def encode_groups(flats: Sequence[torch.Tensor], bit_width: int, dev: torch.device, rng: str = "philox",

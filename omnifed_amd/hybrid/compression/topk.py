@@ -3,7 +3,10 @@
 ``TopKCompression.compress`` = compensate (t' = residual + x) → select the
 k = max(1, int(n·ratio)) largest |t'| → residual := t' − desparse(selection)
 (topk.py:33-42, core.py:26-37), all in ``omf_topk_encode``; the per-name
-residual lives on the GPU in ``self.residual.residuals[name]`` (flat fp32).
+residual lives on the GPU in ``self.residual.residuals[name]`` (flat fp32).  ``encode_arena``
+(the batched wire path, ``encode_updates_dict``) encodes a whole update dict in one call; its
+residuals live in one compressor-owned arena per dict layout and ``residuals[name]`` are views
+of it, so the per-tensor and the batched paths share the same error-feedback state.
 Selection order: descending |t'|, ties by ascending index — torch.topk's order
 for k·64 <= n on the reference CPU path (its ties are unspecified).
 """
@@ -13,7 +16,7 @@ from __future__ import annotations
 import torch
 
 from ... import codec
-from .core import Compression, ResidualUpdates, compute_device, to_arena
+from .core import Compression, ResidualUpdates, compute_device, gather_arena, to_arena
 
 TOPK_COMPRESSION_NAME = "TopKCompression"
 
@@ -38,6 +41,11 @@ def topk_desparse(values: torch.Tensor, indices: torch.Tensor, numel: int, devic
     return y[: int(numel)].to(out_dev)
 
 
+def topk_index_offset(K: int) -> int:
+    """Byte offset of the indices in a combined (values, indices) buffer of K selected values."""
+    return (4 * int(K) + 255) // 256 * 256
+
+
 class TopKCompression(Compression):
     """Top-k sparsification with error feedback (largest-magnitude elements)."""
 
@@ -46,6 +54,7 @@ class TopKCompression(Compression):
         self.residual = ResidualUpdates()
         self.device = torch.device(device)
         self.compress_ratio = float(compress_ratio)
+        self._arenas = {}  # residual arenas of the batched path, per dict layout
 
     def compress(self, tensor: torch.Tensor, name: str):
         """topk.py:33-42: ``((values, indices), (numel, shape))``; mutates the residual of ``name``."""
@@ -78,6 +87,65 @@ class TopKCompression(Compression):
         self.residual.residuals[name] = res
         ctx = (numel, shape)
         return (values.to(self.device), indices.to(self.device)), ctx
+
+    def _residual_arena(self, names, plan):
+        """The residual arena of the dict layout (``names``, ``plan``) and the encoder's residual
+        mode: each name's current residual copied in unless ``residuals[name]`` already is its
+        view of the arena; a name with no residual yet gets -0.0, the additive identity (-0 + a
+        = a for every a, signed zeros and NaN payloads included), so one compensating launch
+        (mode 1) computes exactly the reference's ``compensate`` for every name (core.py:26-31).
+        Mode 2 (no read) when no name has a residual."""
+        key = (tuple(names), tuple(plan.sizes), str(plan.device))
+        arena = self._arenas.get(key)
+        if arena is None:
+            if len(self._arenas) >= 4:
+                self._arenas.pop(next(iter(self._arenas)))
+            arena = torch.empty(max(plan.arena_end, 4), dtype=torch.float32, device=plan.device)
+            self._arenas[key] = arena
+        base = arena.data_ptr()
+        fresh = []
+        for t, name in enumerate(names):
+            o, n = plan.offsets[t], plan.sizes[t]
+            r = self.residual.residuals.get(name)
+            if r is None:
+                fresh.append(t)
+            elif not (r.data_ptr() == base + 4 * o and r.numel() == n and r.dtype == torch.float32
+                      and r.device == plan.device):
+                if r.numel() != n:
+                    raise ValueError(f"residual for {name!r} has {r.numel()} elements, tensor has {n}")
+                arena[o:o + n].copy_(r.reshape(-1))
+        if len(fresh) == len(names):
+            return arena, 2
+        for t in fresh:
+            arena[plan.offsets[t]:plan.offsets[t] + plan.sizes[t]].fill_(-0.0)
+        return arena, 1
+
+    def encode_arena(self, names, flats, alpha: float = 1.0, out: "torch.Tensor" = None):
+        """``compress_weighted(flat, name, alpha)`` for every (name, flat) in ONE encode call
+        (flats: non-empty fp32 tensors; the residuals become views of one arena).  Returns
+        ``(plan, values, indices, ks)``: tensor t's selection at ``[sum(ks[:t]), + ks[t])``.
+        ``out`` (optional uint8 device buffer): values are written at its start and indices at
+        byte ``topk_index_offset(K)``, so one device-to-host copy fetches both."""
+        dev = compute_device(flats[0], self.device)
+        plan = codec.Plan.get([int(f.numel()) for f in flats], device=dev)
+        ks = plan.topk_ks(self.compress_ratio)
+        K = sum(ks)
+        x = gather_arena(flats, dev, plan)
+        res, mode = self._residual_arena(names, plan)
+        if out is None:
+            out = torch.empty(topk_index_offset(K) + 8 * K, dtype=torch.uint8, device=dev)
+        io = topk_index_offset(K)
+        values = out[:4 * K].view(torch.float32)
+        indices = out[io:io + 8 * K].view(torch.int64)
+        plan.topk_encode(x, self.compress_ratio, residual=res, residual_mode=mode, values=values, indices=indices,
+                         alpha=float(alpha))
+        base = res.data_ptr()
+        for t, name in enumerate(names):
+            o, n = plan.offsets[t], plan.sizes[t]
+            r = self.residual.residuals.get(name)
+            if r is None or r.data_ptr() != base + 4 * o or r.numel() != n:
+                self.residual.residuals[name] = res[o:o + n]
+        return plan, values, indices, ks
 
     def decompress(self, tensors, ctx):
         numel, shape = ctx

@@ -125,53 +125,85 @@ class DeviceAggregator:
         return self.avg[o:o + n]
 
     def accumulate_layers(self, layers, number_samples: int = 0):
-        """Decode one client's update into the accumulator (global_grpc_server.py:108-111, 147-153)."""
-        qsgd = [L for L in layers if L.compression_type == "QSGDQuantCompression" and L.layer_name in self.index]
+        """Decode one client's update into the accumulator (global_grpc_server.py:108-111, 147-153).
+
+        Every layer is checked and staged before the accumulator is touched (the reference decodes
+        the whole update, then accumulates: a bad layer leaves acc as it was).  All QSGD layers go
+        through ONE decode-accumulate launch, all Top-K layers through ONE index check and ONE
+        scatter-add (omf_topk_decode_counts), both fed by chunked pinned staging.  A repeated name:
+        the last layer, as the reference's decoded dict."""
+        from .hybrid.communicator.global_grpc_compression import _validate_layer, check_topk_indices, stage_topk
+
+        last: Dict[str, object] = {}
+        topk_payload: Dict[str, tuple] = {}
+        for L in layers:
+            got = _validate_layer(L)  # the reference decoder's checks, in message order
+            if L.layer_name not in self.index:
+                continue
+            last[L.layer_name] = L
+            if got is not None:
+                topk_payload[L.layer_name] = got
+        kept = sorted(last.values(), key=lambda L: self.index[L.layer_name])  # ascending arena offsets
+        qsgd = [L for L in kept if L.compression_type == "QSGDQuantCompression"]
+        topk = [L for L in kept if L.compression_type == "TopKCompression"]
+        dense = [L for L in kept if L.compression_type == ""]
+        if any(L.compression_type not in ("QSGDQuantCompression", "TopKCompression", "") for L in kept):
+            bad = next(L for L in kept if L.compression_type not in ("QSGDQuantCompression", "TopKCompression", ""))
+            raise ValueError(f"Unsupported compression_type={bad.compression_type!r}")
+        # --- stage and check everything
+        q_args = None
         if qsgd:
             width, level = qsgd[0].width, qsgd[0].level
             if any(L.width != width or L.level != level for L in qsgd):
                 raise ValueError("mixed QSGD width/level within one update")
-            if width not in (8, 32) or level <= 0:
-                raise ValueError(f"unsupported QSGD width={width} / level={level}")
             isz = width // 8
             norms = np.zeros(self.plan.nt, dtype=np.float32)  # absent tensors: norm 0 adds +0
-            # one payload per name (a repeated name: the last one, as the reference's decoded dict),
-            # in ascending arena offsets
-            order = sorted({L.layer_name: L for L in qsgd}.values(), key=lambda L: self.index[L.layer_name])
             items = []
-            for L in order:
+            for L in qsgd:
                 i = self.index[L.layer_name]
                 norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
                 items.append((self.plan.offsets[i] * isz, (lambda L=L: L.values_data)))
 
             def check(k, payload):
-                n = self.plan.sizes[self.index[order[k].layer_name]]
+                n = self.plan.sizes[self.index[qsgd[k].layer_name]]
                 if len(payload) != n * isz:
-                    raise ValueError(f"QSGD layer {order[k].layer_name!r}: {len(payload) // isz} values, expected {n}")
+                    raise ValueError(f"QSGD layer {qsgd[k].layer_name!r}: {len(payload) // isz} values, expected {n}")
 
             qd = torch.empty(self.plan.payload_elems(width), dtype=torch.int8 if width == 8 else torch.int32,
                              device=self.device)
             nd = torch.from_numpy(norms).to(self.device)
-            # the payloads through pinned staging, chunk by chunk (omnifed_amd.hostio); validated
-            # before anything reaches the accumulator
             hostio.bytes_to_device(items, qd, isz * self.plan.payload_elems(width), key="ps_decode", check=check)
+            q_args = (qd, width, level, nd)
+        t_args = None
+        if topk:
+            pairs = [(b"", b"")] * self.plan.nt
+            for L in topk:
+                i = self.index[L.layer_name]
+                v, ix, k = topk_payload[L.layer_name]
+                if k > self.plan.sizes[i]:
+                    raise IndexError(f"Compressed layer {L.layer_name!r}: {k} values for a tensor of "
+                                     f"{self.plan.sizes[i]} elements")
+                pairs[i] = (v, ix)
+            counts, values, indices = stage_topk(pairs, self.device, "ps_topk")
+            check_topk_indices(self.plan, counts, indices, self.names)  # synchronises
+            t_args = (counts, values, indices)
+        dense_args = []
+        for L in dense:
+            arr = torch.tensor(list(L.param_update), dtype=torch.float32)
+            n = self.plan.sizes[self.index[L.layer_name]]
+            if arr.numel() != n:
+                raise ValueError(f"Dense layer {L.layer_name!r}: {arr.numel()} values, expected {n}")
+            dense_args.append((L.layer_name, arr.to(self.device, non_blocking=False)))
+        # --- accumulate (client terms in the reference's per-name order: one term per name)
+        if q_args is not None:
             # Tensors absent from this update keep acc += (0 * q)/L = +0 (whatever q holds there:
             # any int8 / int32 level times a zero norm is a zero).
+            qd, width, level, nd = q_args
             self.plan.qsgd_decode(qd, width, level, nd, y_out=self.acc, accumulate=True)
-            torch.cuda.current_stream(self.device).synchronize()  # the staging is reused by the next update
-        for L in layers:
-            if L.layer_name not in self.index or L.compression_type == "QSGDQuantCompression":
-                continue
-            dst = self._slice(L.layer_name)
-            if L.compression_type == "TopKCompression":
-                v = torch.from_numpy(np.frombuffer(L.values_data, dtype=np.float32).copy()).to(self.device)
-                ix = torch.from_numpy(np.frombuffer(L.indices_data, dtype=np.int64).copy()).to(self.device)
-                codec.topk_decode(v, ix, dst.numel(), y=dst, mode=2)
-            elif L.compression_type == "":
-                arr = torch.tensor(list(L.param_update), dtype=torch.float32).to(self.device)
-                dst.add_(arr.reshape(-1))
-            else:
-                raise ValueError(f"Unsupported compression_type={L.compression_type!r}")
+        if t_args is not None:
+            self.plan.topk_decode_counts(*t_args, y=self.acc, mode=2)
+        for name, arr in dense_args:
+            self._slice(name).add_(arr.reshape(-1))
         self.update_count += 1
         self.total_samples += int(number_samples)
 
@@ -229,8 +261,8 @@ class DeviceAggregator:
         independently, as the reference does per request.  An in-kernel encoder timeout raises
         ``RuntimeError``.
         """
-        from .hybrid.compression.qsgd import QSGDQuantCompression, choose_qsgd_storage_width
-        from .hybrid.communicator.global_grpc_compression import qsgd_layer_from_payload, _encode_dense_layer
+        from .hybrid.compression.qsgd import QSGDQuantCompression
+        from .hybrid.communicator.global_grpc_compression import _encode_dense_layer, qsgd_layers_from_arena
 
         total = self.total_samples if total_samples is None else int(total_samples)
         if self.avg is None:
@@ -247,19 +279,14 @@ class DeviceAggregator:
         # avg_out disjoint from acc: the one-launch path (omf_ps_apply_encode)
         _, q, norms = self.plan.ps_apply_encode(self.acc, float(total), s, avg_out=self.avg,
                                                 seed=compressor.philox_key(), offset=compressor._next_call())
-        levels = 2**s
-        width, _ = choose_qsgd_storage_width(levels)
-        qh = q.cpu().numpy()
-        nh = norms.cpu().tolist()
-        self.plan.check()  # an in-kernel timeout raises: the payload would be invalid
         avg = {n: self._avg_slice(n).view(self.shapes[n]) for n in self.names}
+        # the payload arena through the wire pipeline (chunked pinned D2H, worker-filled bytes);
+        # raises on an in-kernel encoder timeout
+        got = qsgd_layers_from_arena(self.plan, q, norms, self.names, [self.shapes[n] for n in self.names], 2**s,
+                                     compressor.packed_wire)
         layers = []
-        for i, n in enumerate(self.names):
-            o, k = self.plan.offsets[i], self.plan.sizes[i]
-            if nh[i] != 0 and int(np.prod(self.shapes[n])) > 0:
-                layers.append(qsgd_layer_from_payload(n, self.shapes[n], qh[o:o + k].tobytes(), nh[i], width, levels))
-            else:
-                layers.append(_encode_dense_layer(n, avg[n]))
+        for n, L in zip(self.names, got):
+            layers.append(L if L is not None and int(np.prod(self.shapes[n])) > 0 else _encode_dense_layer(n, avg[n]))
         return avg, layers
 
     def apply(self, total_samples: Optional[int] = None) -> Dict[str, torch.Tensor]:

@@ -56,27 +56,36 @@ def philox4x32_10(c0, c1, c2, c3, k0, k1):
 
 
 def philox_uniforms(seed: int, offset: int, tensor_index: int, n: int) -> np.ndarray:
-    """The perf-mode uniforms ``u_0..u_{n-1}`` for one tensor (layout above)."""
-    i = np.arange(n, dtype=np.int64)
-    j = i >> 2
-    m = j >> 8
-    G = ((m >> 2) << 8) | (j & 255)
-    f = 4 * (m & 3) + (i & 3)
-    groups = np.unique(G)
-    gpos = np.searchsorted(groups, G)
-    words = np.empty((groups.size, 12), dtype=np.uint32)
-    for c in range(3):
-        ctr = (3 * groups.astype(np.uint64) + np.uint64(c))
-        o = philox4x32_10((ctr & _MASK).astype(np.uint32), (ctr >> np.uint64(32)).astype(np.uint32),
-                          np.full(groups.size, tensor_index & 0xFFFFFFFF, dtype=np.uint32),
-                          np.full(groups.size, offset & 0xFFFFFFFF, dtype=np.uint32),
-                          seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
-        for w in range(4):
-            words[:, 4 * c + w] = o[w]
-    bit = 24 * f
-    wi = bit >> 5
-    sh = (bit & 31).astype(np.uint64)
-    lo = words[gpos, wi].astype(np.uint64)
-    hi = words[gpos, np.minimum(wi + 1, 11)].astype(np.uint64)
-    val = ((lo | (hi << np.uint64(32))) >> sh) & np.uint64(0xFFFFFF)
-    return (val.astype(np.float64) * 2.0**-24).astype(np.float32)
+    """The perf-mode uniforms ``u_0..u_{n-1}`` for one tensor (layout above).
+
+    The groups of a tensor are (nearly) the dense range 0..max(G), so every group below max(G) + 1
+    is generated and indexed by G directly (a few unused groups at a partial tail cost nothing);
+    the whole tensor is processed in slices of 2^22 elements to bound the temporaries."""
+    out = np.empty(n, dtype=np.float32)
+    step = 1 << 22  # a multiple of 1024 * 4: a slice starts on a group-row boundary
+    k0, k1 = seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF
+    for a in range(0, n, step):
+        i = np.arange(a, min(n, a + step), dtype=np.int64)
+        j = i >> 2
+        m = j >> 8
+        G = ((m >> 2) << 8) | (j & 255)
+        f = 4 * (m & 3) + (i & 3)
+        g0 = int(G.min())
+        groups = np.arange(g0, int(G.max()) + 1, dtype=np.uint64)
+        gpos = G - g0
+        words = np.empty((groups.size, 12), dtype=np.uint32)
+        for c in range(3):
+            ctr = 3 * groups + np.uint64(c)
+            o = philox4x32_10((ctr & _MASK).astype(np.uint32), (ctr >> np.uint64(32)).astype(np.uint32),
+                              np.full(groups.size, tensor_index & 0xFFFFFFFF, dtype=np.uint32),
+                              np.full(groups.size, offset & 0xFFFFFFFF, dtype=np.uint32), k0, k1)
+            for w in range(4):
+                words[:, 4 * c + w] = o[w]
+        bit = 24 * f
+        wi = bit >> 5
+        sh = (bit & 31).astype(np.uint64)
+        lo = words[gpos, wi].astype(np.uint64)
+        hi = words[gpos, np.minimum(wi + 1, 11)].astype(np.uint64)
+        val = ((lo | (hi << np.uint64(32))) >> sh) & np.uint64(0xFFFFFF)
+        out[a:a + len(i)] = (val.astype(np.float64) * 2.0**-24).astype(np.float32)
+    return out

@@ -1,0 +1,70 @@
+#!/bin/bash
+# One driver for the GPU-box runs (gpurun -- bash scripts/gpu.sh <task> [args]).  Every GPU step
+# runs under its own time limit and the first failure ends the script (no retries).
+#   tests [pytest -k expr]  the -m gpu suite (or a subset), one process
+#   wire [tag]              host-inclusive wire timings -> gpurun_out/<tag>_wire.json
+#   bench [tag] [args...]   bench.py line -> gpurun_out/<tag>_bench.json
+#   prof [tag] [args...]    rocprofv3 --kernel-trace --stats of bench.py (args: e.g. --codec topk)
+#   pmc [tag] [args...]     FETCH_SIZE / WRITE_SIZE passes of bench.py + pmc_traffic.json
+#   py <script> [args...]   any experiment script (its stdout -> gpurun_out/py.out)
+set -o pipefail
+cd "$(dirname "$0")/.." && export TMPDIR=/tmp
+R=$(pwd)
+mkdir -p gpurun_out
+task=${1:-tests}
+shift || true
+case "$task" in
+  tests)
+    K=()
+    [ -n "$1" ] && K=(-k "$1")
+    timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${K[@]}" \
+      > gpurun_out/tests.log 2>&1
+    rc=$?
+    tail -n 40 gpurun_out/tests.log
+    exit $rc
+    ;;
+  wire)
+    T=${1:-r04}
+    timeout -k 10 600 python3 -u scripts/wire_bench.py llama400m gpurun_out/${T}_wire.json \
+      > gpurun_out/${T}_wire.out 2> gpurun_out/${T}_wire.err || { tail -20 gpurun_out/${T}_wire.err; exit 2; }
+    cat gpurun_out/${T}_wire.json
+    ;;
+  bench)
+    T=${1:-r04}
+    shift || true
+    timeout -k 10 600 python3 -u bench.py "$@" > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err \
+      || { tail -20 gpurun_out/${T}_bench.err; exit 2; }
+    cat gpurun_out/${T}_bench.json
+    ;;
+  prof)
+    T=${1:-r04}
+    shift || true
+    rm -rf gpurun_out/${T}_prof
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/${T}_prof" -o run \
+      -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-extras "$@" \
+      > gpurun_out/${T}_prof.log 2>&1 || { tail -20 gpurun_out/${T}_prof.log; exit 2; }
+    s=$(find gpurun_out/${T}_prof -name '*kernel_stats.csv' | head -n 1)
+    [ -n "$s" ] && cp "$s" gpurun_out/${T}_kernel_stats.csv && cat gpurun_out/${T}_kernel_stats.csv
+    ;;
+  pmc)
+    T=${1:-r04}
+    shift || true
+    for c in FETCH_SIZE WRITE_SIZE; do
+      rm -rf gpurun_out/${T}_pmc_$c
+      timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d "$R/gpurun_out/${T}_pmc_$c" -o run \
+        -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-extras "$@" \
+        > gpurun_out/${T}_pmc_$c.log 2>&1 || { tail -20 gpurun_out/${T}_pmc_$c.log; exit 2; }
+    done
+    python3 scripts/pmc_traffic.py gpurun_out/${T}_pmc_FETCH_SIZE gpurun_out/${T}_pmc_WRITE_SIZE \
+      gpurun_out/${T}_pmc_traffic.json llama400m 4 || exit 3
+    cat gpurun_out/${T}_pmc_traffic.json
+    ;;
+  py)
+    S=$1
+    shift || true
+    timeout -k 10 900 python3 -u "$S" "$@" > gpurun_out/py.out 2> gpurun_out/py.err || { tail -30 gpurun_out/py.err; exit 2; }
+    tail -c 20000 gpurun_out/py.out
+    ;;
+  *)
+    echo "unknown task $task"; exit 64 ;;
+esac

@@ -1,11 +1,17 @@
 """Host-inclusive wire path timing: the drop-in's user-visible API on Llama-400M.
 
-encode_updates_dict : device gradients -> one encode launch -> chunked pinned D2H of the
-                      int8 payload arena -> bytes filled by worker threads -> 183 LayerState
-                      messages (omnifed_amd.hostio)
+QSGD (s = 4) and Top-K (k = 1 %, the reference's default scheme, conf/base.yaml:197):
+encode_updates_dict : device gradients -> one encode call -> chunked pinned D2H of the payload
+                      buffer -> bytes filled by worker threads -> 183 LayerState messages
 decode_updates_dict : LayerStates -> pinned staging (worker threads) -> chunked H2D -> one
-                      decode launch (device="cuda": stays on the GPU; default: CPU tensors)
+                      decode call (device="cuda": stays on the GPU; default: CPU tensors)
 decode_updates_into : client downlink straight into the model's device tensors
+accumulate_layers   : the PS's SendUpdate decode-accumulate of one client (DeviceAggregator)
+apply_and_encode    : the PS's GetUpdatedModel: average + re-encode + LayerStates
+host round trip     : host fp32 tensors in -> LayerStates -> host fp32 tensors out (the rate
+                      including the H<->D copies, north_star)
+
+usage: python scripts/wire_bench.py [config] [out.json]
 """
 import json
 import sys
@@ -14,17 +20,18 @@ import time
 import torch
 
 sys.path.insert(0, ".")
-from omnifed_amd import shapes  # noqa: E402
+from omnifed_amd import codec, hostio, shapes  # noqa: E402
 from omnifed_amd.hybrid.communicator.global_grpc_compression import (  # noqa: E402
-    build_global_compressor, decode_updates_dict, decode_updates_into, encode_updates_dict)
+    build_global_compressor, decode_updates_dict, decode_updates_into, encode_layer_state, encode_updates_dict)
+from omnifed_amd.ps import DeviceAggregator  # noqa: E402
 
 dev = torch.device("cuda", 0)
 cfg = sys.argv[1] if len(sys.argv) > 1 else "llama400m"
+out_path = sys.argv[2] if len(sys.argv) > 2 else None
 named = shapes.model_shapes(cfg)
 g = torch.Generator(device=dev).manual_seed(0)
 upd = {n: torch.randn(s, device=dev, generator=g) * 1e-3 for n, s in named}
 N = sum(t.numel() for t in upd.values())
-comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev)
 targets = {n: torch.empty_like(t) for n, t in upd.items()}
 
 
@@ -38,34 +45,60 @@ def tm(fn, reps=7, warm=3):
         fn()
         torch.cuda.synchronize()
         ts.append(time.perf_counter() - t0)
-    return sorted(ts)[len(ts) // 2]
+    return round(sorted(ts)[len(ts) // 2] * 1e3, 2)
 
 
-stats = {}
-layers = encode_updates_dict(upd, comp, stats=stats)
-from omnifed_amd import hostio  # noqa: E402
-res = {"config": cfg, "elements": N, "tensors": len(named), "wire": stats, "copy_threads": hostio.workers(),
-       "agg_accumulate_layers_ms": None, "by_copy_threads": {},
-       "encode_updates_dict_ms": tm(lambda: encode_updates_dict(upd, comp)) * 1e3,
-       "decode_updates_dict_gpu_ms": tm(lambda: decode_updates_dict(layers, device=dev)) * 1e3,
-       "decode_updates_into_ms": tm(lambda: decode_updates_into(layers, targets)) * 1e3,
-       "decode_updates_dict_cpu_ms": tm(lambda: decode_updates_dict(layers)) * 1e3}
+def leg(comp, tag):
+    """The wire legs of one compressor; returns a dict of medians (ms) and rates."""
+    r = {}
+    st = {}
+    layers = encode_updates_dict(upd, comp, stats=st)
+    r["wire"] = st
+    r["encode_updates_dict_ms"] = tm(lambda: encode_updates_dict(upd, comp))
+    r["decode_updates_dict_gpu_ms"] = tm(lambda: decode_updates_dict(layers, device=dev))
+    r["decode_updates_into_ms"] = tm(lambda: decode_updates_into(layers, targets))
+    r["decode_updates_dict_cpu_ms"] = tm(lambda: decode_updates_dict(layers), reps=3, warm=1)
+    agg = DeviceAggregator(named, device=dev)
+    r["agg_accumulate_layers_ms"] = tm(lambda: agg.accumulate_layers(layers, number_samples=1))
+    # GetUpdatedModel: the server's compressor re-encodes the average (apply_and_encode) of a
+    # dense accumulator (the model parameters / the average of many clients' updates; one sparse
+    # Top-K update alone leaves 99 % zeros, whose ties at 0 send a Top-K re-encode to the exact path)
+    srv = build_global_compressor(enabled=True, scheme=tag, bit_width=4, compress_ratio=0.01, device=dev)
+    agg.acc.copy_(torch.randn(agg.acc.numel(), device=dev, generator=g) * 4e-2)
+    agg.total_samples = 40
+    r["ps_apply_and_encode_ms"] = tm(lambda: agg.apply_and_encode(srv, total_samples=40))
+    del agg
+    # host round trip: host fp32 tensors in, LayerStates, host fp32 tensors out
+    host = {n: t.cpu().pin_memory() for n, t in upd.items()}
+    r["host_roundtrip_ms"] = tm(lambda: decode_updates_dict(encode_updates_dict(host, comp)), reps=3, warm=1)
+    for k in ("encode_updates_dict_ms", "decode_updates_dict_gpu_ms", "decode_updates_into_ms",
+              "decode_updates_dict_cpu_ms", "host_roundtrip_ms"):
+        r[k.replace("_ms", "_fp32_GBs")] = round(4 * N / (r[k] * 1e-3) / 1e9, 2)
+    r["device_roundtrip_ms"] = round(r["encode_updates_dict_ms"] + r["decode_updates_dict_gpu_ms"], 2)
+    return r, layers
+
+
+res = {"config": cfg, "elements": N, "tensors": len(named), "copy_threads": hostio.workers()}
+qcomp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev)
+res["qsgd_s4"], layers = leg(qcomp, "qsgd")
+tcomp = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+res["topk_1pct"], tlayers = leg(tcomp, "topk")
+# the round-3 per-layer Top-K loop (one encode + host wait + small D2H per tensor), for comparison
+tper = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+res["topk_1pct"]["per_layer_encode_ms"] = tm(lambda: [encode_layer_state(n, t, tper) for n, t in upd.items()],
+                                             reps=3, warm=1)
 # the host copies on the calling thread vs worker threads (hostio.set_workers), same process
+res["by_copy_threads"] = {}
 for nthr in (0, 2, 4, 8):
     hostio.set_workers(nthr)
     res["by_copy_threads"][str(nthr)] = {
-        "encode_updates_dict_ms": round(tm(lambda: encode_updates_dict(upd, comp)) * 1e3, 2),
-        "decode_updates_dict_gpu_ms": round(tm(lambda: decode_updates_dict(layers, device=dev)) * 1e3, 2)}
+        "qsgd_encode_updates_dict_ms": tm(lambda: encode_updates_dict(upd, qcomp)),
+        "qsgd_decode_updates_dict_gpu_ms": tm(lambda: decode_updates_dict(layers, device=dev)),
+        "topk_encode_updates_dict_ms": tm(lambda: encode_updates_dict(upd, tcomp)),
+        "topk_decode_updates_dict_gpu_ms": tm(lambda: decode_updates_dict(tlayers, device=dev))}
 hostio.set_workers(None)
-# the PS uplink: one client's LayerStates decode-accumulated into the aggregator arena
-from omnifed_amd import codec  # noqa: E402
-from omnifed_amd.ps import DeviceAggregator  # noqa: E402
 
-agg = DeviceAggregator(named, device=dev)
-res["agg_accumulate_layers_ms"] = round(tm(lambda: agg.accumulate_layers(layers, number_samples=1)) * 1e3, 2)
-del agg
 # fused PS step (omf_ps_apply_encode) vs divide + encode, device-resident
-
 plan = codec.Plan.get([t.numel() for t in upd.values()], device=dev)
 acc = torch.randn(plan.arena_end, device=dev, generator=g)
 avg = torch.empty_like(acc)
@@ -79,25 +112,23 @@ def separate():
     plan.qsgd_encode(avg, 4, q_out=q, norm_out=nr, seed=1)
 
 
-res["ps_fused_apply_encode_ms"] = tm(lambda: plan.ps_apply_encode(acc, 40.0, 4, avg_out=avg, q_out=q, norm_out=nr,
-                                                                   seed=1), reps=10) * 1e3
-res["ps_divide_then_encode_ms"] = tm(separate, reps=10) * 1e3
-res["ps_fused_apply_encode_ms"] = round(res["ps_fused_apply_encode_ms"], 4)
-res["ps_divide_then_encode_ms"] = round(res["ps_divide_then_encode_ms"], 4)
+res["ps_fused_apply_encode_ms"] = round(tm(lambda: plan.ps_apply_encode(acc, 40.0, 4, avg_out=avg, q_out=q,
+                                                                         norm_out=nr, seed=1), reps=10), 4)
+res["ps_divide_then_encode_ms"] = round(tm(separate, reps=10), 4)
 # opt-in bit-packed wire (s = 4: 6 bits per element instead of 8)
 pcomp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev, packed_wire=True)
 players = encode_updates_dict(upd, pcomp)
-res["packed_encode_updates_dict_ms"] = round(tm(lambda: encode_updates_dict(upd, pcomp)) * 1e3, 2)
-res["packed_decode_updates_dict_gpu_ms"] = round(tm(lambda: decode_updates_dict(players, device=dev)) * 1e3, 2)
+res["packed_encode_updates_dict_ms"] = tm(lambda: encode_updates_dict(upd, pcomp))
+res["packed_decode_updates_dict_gpu_ms"] = tm(lambda: decode_updates_dict(players, device=dev))
 res["packed_wire_bytes"] = sum(len(L.values_data) for L in players)
 res["int8_wire_bytes"] = sum(len(L.values_data) for L in layers)
 qq, nn = plan.qsgd_encode(acc, 4, seed=1)
 pk = plan.qsgd_pack(qq, 8, 16)
-res["device_pack_ms"] = round(tm(lambda: plan.qsgd_pack(qq, 8, 16, packed_out=pk), reps=10) * 1e3, 4)
-res["device_decode_packed_ms"] = round(tm(lambda: plan.qsgd_decode_packed(pk, 16, nn, y_out=avg), reps=10) * 1e3, 4)
-res["device_decode_int8_ms"] = round(tm(lambda: plan.qsgd_decode(qq, 8, 16, nn, y_out=avg), reps=10) * 1e3, 4)
-for k in ("encode_updates_dict_ms", "decode_updates_dict_gpu_ms", "decode_updates_into_ms",
-          "decode_updates_dict_cpu_ms"):
-    res[k.replace("_ms", "_fp32_GBs")] = round(4 * N / (res[k] * 1e-3) / 1e9, 2)
-    res[k] = round(res[k], 2)
-print(json.dumps(res), flush=True)
+res["device_pack_ms"] = round(tm(lambda: plan.qsgd_pack(qq, 8, 16, packed_out=pk), reps=10), 4)
+res["device_decode_packed_ms"] = round(tm(lambda: plan.qsgd_decode_packed(pk, 16, nn, y_out=avg), reps=10), 4)
+res["device_decode_int8_ms"] = round(tm(lambda: plan.qsgd_decode(qq, 8, 16, nn, y_out=avg), reps=10), 4)
+line = json.dumps(res)
+print(line, flush=True)
+if out_path:
+    with open(out_path, "w") as f:
+        f.write(json.dumps(res, indent=1) + "\n")

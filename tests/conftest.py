@@ -38,3 +38,27 @@ def gpu():
 
     build()
     return torch.device("cuda", 0)
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.fixture(scope="module")
+def nccl1(gpu):
+    """A one-rank RCCL group in this process (loopback rendezvous, device bound), per test module."""
+    import torch.distributed as dist
+
+    if dist.is_initialized():
+        pytest.skip("a process group already exists")
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
+    yield gpu
+    dist.destroy_process_group()

@@ -1,0 +1,73 @@
+"""The bench's headline arenas pinned to the oracle directly, tensor by tensor (round 4).
+
+bench.py encodes one client's Llama-400M update (N(0,1)·1e-3, generator seed 1000 + rank) at
+s = 4 with on-device Philox draws and the client weighting fused as alpha, through the
+bracketed single-read encoder.  Here EVERY tensor of that arena — and of Llama-400M at s = 3
+with alpha = 3, and of Llama-150M at s = 4 — is compared with ``oracle.qsgd_quantize``
+(qsgd.py:36-64 restated) given the GPU's norm and ``oracle.philox_uniforms``: payload bytes
+equal, and the decode equal to ``oracle.qsgd_dequantize``.  The bracketed encoder's finish
+pass (the undecided quads it lists and fixes) must have run: spec_stats()["listed"] > 0.
+"""
+
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from omnifed_amd import codec, shapes
+
+pytestmark = pytest.mark.gpu
+
+
+def _threads() -> int:
+    import os
+
+    try:
+        return max(1, min(16, len(os.sched_getaffinity(0))))
+    except AttributeError:  # pragma: no cover
+        return 8
+
+
+@pytest.mark.parametrize("cfg,s,alpha", [("llama400m", 4, 1.0), ("llama400m", 3, 3.0), ("llama150m", 4, 1.0)])
+def test_headline_arena_every_tensor_equals_oracle(gpu, cfg, s, alpha):
+    named = shapes.model_shapes(cfg)
+    sizes = [shapes.numel(sh) for _, sh in named]
+    plan = codec.Plan.get(sizes, device=gpu)
+    assert plan.strategy == "bracket"  # the default encoder of these arenas (bench.py's)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(1000)  # bench.py's rank-0 client
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    seed, off = 0x5EED, 7
+    q, norms = plan.qsgd_encode(x, s, alpha=alpha, seed=seed, offset=off)
+    stats = plan.spec_stats()
+    plan.check()
+    assert stats["listed"] > 0, stats  # the finish pass fixed undecided quads
+    L = 2**s
+    y = plan.qsgd_decode(q, 8, L, norms)
+    xh = x.cpu().numpy()
+    qh = q.cpu().numpy()
+    yh = y.cpu().numpy()
+    nh = norms.cpu().numpy()
+    xs_all = xh if alpha == 1.0 else (xh * np.float32(alpha)).astype(np.float32)  # torch.mul(param, batch_samples)
+
+    def check(t):
+        o, n = plan.offsets[t], sizes[t]
+        xs = xs_all[o:o + n]
+        ref = float(np.sqrt(np.sum(xs.astype(np.float64) ** 2)))
+        if abs(float(nh[t]) - ref) > 2e-6 * ref:
+            return f"tensor {t}: norm {nh[t]} vs fp64 {ref}"
+        u = torch.from_numpy(oracle.philox_uniforms(seed, off, t, n))
+        want, _, _, _ = oracle.qsgd_quantize(torch.from_numpy(xs), s, norm=float(nh[t]), u=u)
+        if qh[o:o + n].tobytes() != want.numpy().tobytes():
+            bad = np.flatnonzero(qh[o:o + n] != want.numpy())
+            return f"tensor {t}: {bad.size} levels differ, first at {bad[:4].tolist()}"
+        want_y = oracle.qsgd_dequantize(want, float(nh[t]), L, (n,)).numpy()
+        if yh[o:o + n].tobytes() != want_y.tobytes():
+            return f"tensor {t}: decode differs"
+        return None
+
+    with ThreadPoolExecutor(_threads()) as ex:
+        errors = [e for e in ex.map(check, range(len(sizes))) if e]
+    assert not errors, errors[:5]

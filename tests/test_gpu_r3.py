@@ -11,13 +11,10 @@
   bracketed single-read encoder.
 """
 
-import os
-import socket
 
 import numpy as np
 import pytest
 import torch
-import torch.distributed as dist
 
 import oracle
 from omnifed_amd import codec, shapes
@@ -109,26 +106,6 @@ def test_timeout_raises_on_the_drop_in(gpu, strategy):
 
 
 # ---------------------------------------------------------------- RCCL, world size 1
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-@pytest.fixture(scope="module")
-def nccl1(gpu):
-    """A one-rank RCCL group in this process (loopback rendezvous, device bound)."""
-    if dist.is_initialized():
-        pytest.skip("a process group already exists")
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(_free_port())
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=gpu)
-    yield gpu
-    dist.destroy_process_group()
-
 
 def _r18_arena(gpu, seed):
     named = shapes.model_shapes("resnet18")
@@ -387,11 +364,7 @@ def test_topk_group_pipeline_matches_one_group(gpu, monkeypatch, groups):
     xs = [torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3 for _ in range(3)]
 
     def run(n_groups, fallback=False):
-        monkeypatch.setenv("OMF_TOPK_GROUPS", str(n_groups))
-        if fallback:
-            monkeypatch.setenv("OMF_TOPK_FALLBACK", "1")
-        else:
-            monkeypatch.delenv("OMF_TOPK_FALLBACK", raising=False)
+        plan.set_topk(groups=n_groups, fallback=1 if fallback else 0)
         res = torch.zeros(plan.arena_end, device=gpu)
         outs = []
         for i, x in enumerate(xs):
@@ -408,10 +381,9 @@ def test_topk_group_pipeline_matches_one_group(gpu, monkeypatch, groups):
         assert torch.equal(ref_res, res)
 
 
-@pytest.mark.parametrize("knob,value", [("OMF_TOPK_SURE", "0,0"), ("OMF_TOPK_SURE", "0.5,0"),
-                                        ("OMF_TOPK_SURE", "6,32"), ("OMF_TOPK_SURE", "40,0"),
-                                        ("OMF_TOPK_SAMPLE_RUNS", "4096"), ("OMF_TOPK_SAMPLE_RUNS", "512")])
-def test_topk_sure_margin_does_not_change_the_selection(gpu, monkeypatch, knob, value):
+@pytest.mark.parametrize("knob,value", [("sure", (0, 0)), ("sure", (0.5, 0)), ("sure", (6, 32)), ("sure", (40, 0)),
+                                        ("sample_runs", 4096), ("sample_runs", 512)])
+def test_topk_sure_margin_does_not_change_the_selection(gpu, knob, value):
     """The "sure" bin (keys whose residual the fused pass zeroes at once) is a performance knob:
     with no margin about half the tensors take more sure keys than k (the bucket kernels give
     those their t' back), with a huge one none is sure — values, indices and the residual over
@@ -432,9 +404,9 @@ def test_topk_sure_margin_does_not_change_the_selection(gpu, monkeypatch, knob, 
         torch.cuda.synchronize()
         return outs, res
 
-    monkeypatch.delenv(knob, raising=False)
+    plan.set_topk(sample_runs=0, sure=(1.5, 2.0))  # the defaults
     ref_outs, ref_res = run()
-    monkeypatch.setenv(knob, value)
+    plan.set_topk(**{knob: value})
     outs, res = run()
     for (v0, i0), (v1, i1) in zip(ref_outs, outs):
         assert torch.equal(v0, v1) and torch.equal(i0, i1)

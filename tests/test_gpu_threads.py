@@ -1,0 +1,177 @@
+"""The codec on gRPC worker threads (round 4).
+
+The reference PS serves SendUpdate / GetUpdatedModel from ``grpc.server(ThreadPoolExecutor(
+max_workers=10))`` (global_grpc.py:44-45): each request runs on whichever worker is free, under
+the servicer's ``self.lock`` (global_grpc_server.py:78, 181, 198); a client and the PS may also
+share a process.  Per-thread state the codec meets there: torch's current stream and device,
+the Top-K encoder's per-thread verdict word (omf_topk.hip), and the pinned staging buffers
+(omnifed_amd.hostio: leased per call).  Both tests compare bytes with a single-thread run.
+"""
+
+import threading
+from concurrent.futures import ThreadPoolExecutor
+
+import pytest
+import torch
+
+from omnifed_amd.hybrid.communicator.global_grpc_compression import (
+    build_global_compressor,
+    decode_updates_into,
+    encode_updates_dict,
+)
+from omnifed_amd.ps import DeviceAggregator
+
+pytestmark = pytest.mark.gpu
+
+# ~37.6 M elements: the int8 payload spans two 32 MiB staging chunks
+SHAPES = [("emb", (16384, 1024)), ("w1", (2048, 1024)), ("b1", (2048,)), ("w2", (1024, 2048)), ("n", (7,)),
+          ("head", (16000, 1024))]
+SAMPLES = [5, 11, 3, 8]
+
+
+def _updates(gpu, c):
+    g = torch.Generator(device=gpu).manual_seed(100 + c)
+    return {n: torch.randn(*s, device=gpu, generator=g) * 1e-3 for n, s in SHAPES}
+
+
+def _compressor(scheme, gpu, instance):
+    comp = build_global_compressor(enabled=True, scheme=scheme, bit_width=4, compress_ratio=0.01, device=gpu)
+    if scheme == "qsgd":
+        comp._instance = instance  # a fixed Philox key across the runs (key = f(seed, instance, client))
+        comp.client_id = instance
+    return comp
+
+
+def _round(gpu, scheme, run):
+    """One PS round: 4 clients encode (``run(fn)`` decides the thread of each call), the PS
+    accumulates each SendUpdate under its lock in a fixed order, applies and re-encodes
+    (GetUpdatedModel), and every client decodes the downlink into its model."""
+    clients = [_compressor(scheme, gpu, c) for c in range(len(SAMPLES))]
+    msgs = [None] * len(SAMPLES)
+
+    def client_encode(c):
+        msgs[c] = encode_updates_dict(_updates(gpu, c), clients[c], weight=float(SAMPLES[c]))
+
+    run([lambda c=c: client_encode(c) for c in range(len(SAMPLES))], ordered=False)
+    agg = DeviceAggregator(SHAPES, device=gpu)
+    lock = threading.Lock()
+
+    def send_update(c):
+        with lock:
+            agg.accumulate_layers(msgs[c], SAMPLES[c])
+
+    run([lambda c=c: send_update(c) for c in range(len(SAMPLES))], ordered=True)
+    server = _compressor(scheme, gpu, 99)
+    down = {}
+
+    def get_updated_model():
+        with lock:
+            down["avg"], down["layers"] = agg.apply_and_encode(server)
+
+    run([get_updated_model], ordered=True)
+    models = [{n: torch.zeros(*s, device=gpu) for n, s in SHAPES} for _ in SAMPLES]
+    run([lambda c=c: decode_updates_into(down["layers"], models[c]) for c in range(len(SAMPLES))], ordered=False)
+    torch.cuda.synchronize()
+    return ([[L.SerializeToString() for L in m] for m in msgs], agg.acc.cpu(),
+            [L.SerializeToString() for L in down["layers"]], [{n: t.cpu() for n, t in m.items()} for m in models])
+
+
+def _inline(fns, ordered):
+    for f in fns:
+        f()
+
+
+def _workers(pool, seen):
+    """Unordered calls all at once on the pool's workers; ordered calls one after another, each on a
+    thread of its own."""
+
+    def run(fns, ordered):
+        if not ordered:
+            for f in [pool.submit(lambda f=f: (seen.add(threading.get_ident()), f())) for f in fns]:
+                f.result()
+            return
+        # each call on a new thread that stays alive until the round's calls are done, so every
+        # call runs on a thread no earlier call ran on
+        alive, errors = [], []
+        for f in fns:
+            finished, release = threading.Event(), threading.Event()
+
+            def body(f=f, finished=finished, release=release):
+                seen.add(threading.get_ident())
+                try:
+                    f()
+                except BaseException as e:  # re-raised on the calling thread
+                    errors.append(e)
+                finally:
+                    finished.set()
+                    release.wait()
+
+            t = threading.Thread(target=body)
+            t.start()
+            finished.wait()
+            alive.append((t, release))
+        for t, release in alive:
+            release.set()
+            t.join()
+        if errors:
+            raise errors[0]
+
+    return run
+
+
+@pytest.mark.parametrize("scheme", ["qsgd", "topk"])
+def test_servicer_calls_from_worker_threads_equal_single_thread(gpu, scheme):
+    want = _round(gpu, scheme, _inline)
+    seen = set()
+    with ThreadPoolExecutor(max_workers=10) as pool:
+        got = _round(gpu, scheme, _workers(pool, seen))
+    assert len(seen) >= 3
+    assert got[0] == want[0]  # every client's LayerStates
+    assert torch.equal(got[1], want[1])  # the PS accumulator
+    assert got[2] == want[2]  # the downlink
+    for a, b in zip(got[3], want[3]):
+        for n in a:
+            assert torch.equal(a[n], b[n]), n
+
+
+def test_client_and_ps_threads_unlocked_on_different_plans(gpu):
+    """A client thread (QSGD and Top-K encodes of its own model, its own plans) and a PS thread
+    (accumulate + apply_and_encode of another model) run at once, without a shared lock, three
+    rounds each: every result equals the same work done on one thread."""
+    ps_shapes = [("a", (3000, 2000)), ("b", (4099,)), ("c", (1 << 22,))]
+
+    def ps_work():
+        out = []
+        agg = DeviceAggregator(ps_shapes, device=gpu)
+        for r in range(3):
+            comp = _compressor("topk" if r % 2 else "qsgd", gpu, 50 + r)
+            g = torch.Generator(device=gpu).manual_seed(7 + r)
+            upd = {n: torch.randn(*s, device=gpu, generator=g) for n, s in ps_shapes}
+            layers = encode_updates_dict(upd, comp, weight=2.0)
+            agg.reset()
+            agg.accumulate_layers(layers, 2)
+            _, down = agg.apply_and_encode(_compressor("qsgd", gpu, 60 + r))
+            out.append(([L.SerializeToString() for L in layers], [L.SerializeToString() for L in down]))
+        torch.cuda.synchronize()
+        return out
+
+    def client_work():
+        out = []
+        q, t = _compressor("qsgd", gpu, 70), _compressor("topk", gpu, 71)
+        for r in range(3):
+            upd = _updates(gpu, 20 + r)
+            out.append([L.SerializeToString() for L in encode_updates_dict(upd, q)]
+                       + [L.SerializeToString() for L in encode_updates_dict(upd, t)])
+        torch.cuda.synchronize()
+        return out
+
+    want = (ps_work(), client_work())
+    res = {}
+    threads = [threading.Thread(target=lambda: res.__setitem__("ps", ps_work())),
+               threading.Thread(target=lambda: res.__setitem__("client", client_work()))]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert res["ps"] == want[0]
+    assert res["client"] == want[1]

@@ -161,18 +161,18 @@ def test_topk_sampled_threshold_error_feedback(gpu, alpha):
             K += k
 
 
-def test_topk_sampled_threshold_redo(gpu, monkeypatch):
+def test_topk_sampled_threshold_redo(gpu):
     """A tensor whose sampled elements are exactly its largest: the sample puts the threshold
     above the k-th magnitude, the pass finds fewer than k candidates, and the tensor is redone
     exactly — the k largest, ties by ascending index."""
-    runs = 16384
-    monkeypatch.setenv("OMF_TOPK_SAMPLE_RUNS", str(runs))  # the sample size the positions assume
+    runs = 16384  # the sample size the positions assume
     n = 1 << 25  # 16 Ki runs of 16 = 256 Ki samples < k = 335544
     x = np.ones(n, np.float32)
     sp = _sample_positions(n, 1, runs)
     x[sp] = 10.0
     sizes = [40000, n]
     plan = codec.Plan(sizes, device=gpu)
+    plan.set_topk(sample_runs=runs)
     xa = torch.zeros(plan.arena_end)
     xa[plan.offsets[1]:plan.offsets[1] + n] = torch.from_numpy(x)
     xa[:40000] = torch.arange(40000, dtype=torch.float32)
@@ -267,17 +267,16 @@ def test_encode_updates_dict_mt_matches_reference_when_norm_agrees(gpu, golden, 
 
 def _encode_both_paths(plan, x, ratio, residual0=None, mode=0, alpha=1.0):
     """Top-K encode through the bucket-sort fast path and through the device-wide radix-sort
-    fallback (OMF_TOPK_FALLBACK=1, read per call by the library) on the same input."""
-    import os
+    fallback (omf_plan_set_topk force_fallback) on the same input."""
     outs = []
-    for fb in ("0", "1"):
+    for fb in (0, 1):
         res = residual0.clone() if residual0 is not None else None
-        os.environ["OMF_TOPK_FALLBACK"] = fb
+        plan.set_topk(fallback=fb)
         try:
             v, i, ks = plan.topk_encode(x, ratio, residual=res, residual_mode=mode, alpha=alpha)
             torch.cuda.synchronize()
         finally:
-            os.environ.pop("OMF_TOPK_FALLBACK", None)
+            plan.set_topk(fallback=0)
         outs.append((v, i, res))
     return outs, ks
 
