@@ -236,7 +236,8 @@ int omf_div_f32(float* y, int64_t n, float divisor, void* stream);
  * packed as code 0; groups of arena padding are neither written nor decoded).  Both calls
  * need every tensor offset to be a multiple of 32 elements (OMF_EINVAL otherwise; the
  * Python arena_layout's are multiples of 64).
- * omf_qsgd_pack: payload (width 8 or 32, as omf_qsgd_encode wrote it) -> packed arena.
+ * omf_qsgd_pack: payload (width 8 or 32, as omf_qsgd_encode wrote it) -> packed arena (8-byte
+ * aligned: even widths are stored as 8-byte word pairs; omf_qsgd_decode_packed needs 4).
  * omf_qsgd_decode_packed: y = fl32(fl32(norm * (code - L)) / L), bit-identical to
  * omf_qsgd_decode of the unpacked payload (accumulate: y += that).
  */

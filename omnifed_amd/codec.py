@@ -357,7 +357,7 @@ class Plan:
         words = self.packed_words(levels)
         if packed_out is None:
             packed_out = torch.empty(max(words, 1), dtype=torch.int32, device=dev)
-        _need(packed_out, "packed_out", torch.int32, dev, words, 4)
+        _need(packed_out, "packed_out", torch.int32, dev, words, 8)  # 8-byte word-pair stores
         st = stream if stream is not None else _stream(dev)
         check(lib().omf_qsgd_pack(self._h, _ptr(q), width, levels, _ptr(packed_out), ctypes.c_void_p(st)),
               "omf_qsgd_pack")

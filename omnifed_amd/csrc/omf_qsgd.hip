@@ -2091,8 +2091,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     ga.e = a;
     ga.partials = p->d_spec_part;
     ga.bar = p->d_grid_bar;
-    ++p->grid_launches;
-    ga.target = (unsigned long long)p->grid_launches * (unsigned long long)p->grid_wgs;
+    ga.target = (unsigned long long)(p->grid_launches + 1) * (unsigned long long)p->grid_wgs;
     ga.nblocks = p->n_spec_blocks;
     ga.dbg = p->spec_skip;
     const dim3 gg((unsigned)p->grid_wgs), gblk(1024);
@@ -2103,6 +2102,9 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
       hipLaunchKernelGGL(qsgd_encode_grid<4>, gg, gblk, 0, st, ga, (const Item*)p->d_flat, (const int64_t*)p->d_begins,
                          (const uint32_t*)p->d_grid_pbeg, (const uint32_t*)p->d_grid_pcnt);
     OMF_HIP(hipGetLastError());
+    // counted only once the launch is in: the device's monotonic arrival counter advances by
+    // grid_wgs per launch that ran, so a failed launch must not move the host's target
+    ++p->grid_launches;
     return OMF_OK;
   }
   // Bracketed single-read encoder: fp32 values with on-device draws (other formats and

@@ -125,7 +125,8 @@ __global__ __launch_bounds__(kThreads) void qsgd_pack(const void* __restrict__ q
 // pass: 0.38 ms on Llama-400M).  Each thread unpacks its 32 elements into LDS; the workgroup
 // transposes them (33-word rows: conflict-free both ways) so the fp32 stores are lane-contiguous
 // 16-byte non-temporal stores.  A block not inside one tensor finds each 32-element group's
-// tensor (offsets are multiples of 64: a group never spans two) and writes only its elements;
+// tensor (packed_arena requires offsets that are multiples of 32: a group never spans two) and
+// writes only its elements;
 // padding keeps what y held.
 template <int B, bool ACC, bool POW2>
 __global__ __launch_bounds__(kThreads) void qsgd_decode_packed(const uint32_t* __restrict__ packed,
@@ -295,7 +296,8 @@ int omf_qsgd_pack(omf_plan* plan, const void* q, int32_t width, int32_t levels, 
   if (b < 0 || b > 32) return fail(OMF_EINVAL, "levels must be in [1, 2^31 - 1)");
   if (width == 8 && levels > 127) return fail(OMF_EINVAL, "an int8 payload holds levels <= 127");
   if (!q || !packed) return fail(OMF_EINVAL, "q and packed must be non-NULL");
-  if (((uintptr_t)q & 15) || ((uintptr_t)packed & 3)) return fail(OMF_EINVAL, "q must be 16-byte, packed 4-byte aligned");
+  // even widths store 8-byte word pairs: the packed arena must be 8-byte aligned
+  if (((uintptr_t)q & 15) || ((uintptr_t)packed & 7)) return fail(OMF_EINVAL, "q must be 16-byte, packed 8-byte aligned");
   ArenaArgs a;
   dim3 grid;
   if (const int rc = packed_arena(plan, &a, &grid)) return rc;

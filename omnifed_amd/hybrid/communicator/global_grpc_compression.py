@@ -26,6 +26,7 @@ work happens, not what is produced:
 
 from __future__ import annotations
 
+import logging
 import os
 from typing import Dict, List, Optional, Union
 
@@ -63,6 +64,11 @@ def _host_memory_policy() -> bool:
     global _HOST_POLICY
     if _HOST_POLICY is None:
         _HOST_POLICY = os.environ.get("OMF_RETAIN_HOST_MEMORY", "1") != "0" and hostio.retain_host_memory()
+        if _HOST_POLICY:
+            logging.getLogger("omnifed_amd").info(
+                "omnifed_amd: glibc malloc now keeps freed wire-message memory for reuse (mmap threshold 32 MiB, "
+                "trim threshold 1 GiB per arena; resident size may stay ~one round's payload higher). "
+                "OMF_RETAIN_HOST_MEMORY=0 leaves glibc's defaults alone (INTEGRATION.md §3c).")
     return _HOST_POLICY
 
 
