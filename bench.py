@@ -141,9 +141,22 @@ def _median_time(fn, reps=5):
     return float(np.median(ts))
 
 
+def thread_sweep(torch, fn):
+    """Median time of ``fn`` at 1 thread, torch's default (the box sets OMP_NUM_THREADS) and every
+    core this process may run on."""
+    default = torch.get_num_threads()
+    times = {}
+    for th in sorted({1, default, visible_cores()}):
+        torch.set_num_threads(th)
+        times[th] = _median_time(fn)
+    torch.set_num_threads(default)
+    return times
+
+
 def cpu_baseline(torch, named, bits, budget=40_000_000):
-    """The reference's op sequence (oracle, kind 'port') on a stratified sample of the arena, at 1 thread
-    and at all threads, median of 5 after 1 warm-up; extrapolated per element to the whole arena."""
+    """The reference's op sequence (oracle, kind 'port') on a stratified sample of the arena, at 1 thread,
+    torch's default thread count and every visible core, median of 5 after 1 warm-up; the fastest is the
+    value (``cores`` = its thread count); extrapolated per element to the whole arena."""
     import oracle
 
     picked, sizes = stratified_sample(named, budget)
@@ -161,20 +174,15 @@ def cpu_baseline(torch, named, bits, budget=40_000_000):
             q = torch.from_numpy(np.frombuffer(b, dtype=np.int8 if wd == 8 else np.int32).copy())
             oracle.qsgd_dequantize(q, norm, lv, (n,))
 
-    all_threads = torch.get_num_threads()
-    times = {}
-    for th in (1, all_threads):
-        torch.set_num_threads(th)
-        times[th] = _median_time(one)
-    torch.set_num_threads(all_threads)
+    times = thread_sweep(torch, one)
     N = sum(sizes)
     per = (8 + 2 * w)
     best = min(times, key=lambda k: times[k])
     return {
         "value": round(per * tot / times[best] / 1e9, 4),
         "unit": "GB/s",
-        "cores": visible_cores(),
-        "threads": best,
+        "cores": best,
+        "visible_cores": visible_cores(),
         "kind": "port",
         "cpu": cpu_model(),
         "sample": f"{len(picked)} of {len(sizes)} tensors (every {max(1, int(np.ceil(N / budget)))}th; {tot} of {N} "
@@ -187,7 +195,7 @@ def cpu_baseline(torch, named, bits, budget=40_000_000):
 
 def cpu_baseline_topk(torch, named, ratio, budget=12_000_000):
     """The reference Top-K with error feedback (oracle TopKOracle: compensate -> topk -> residual) plus its
-    zero-fill decode, on a stratified sample, all threads and 1 thread, median of 5; extrapolated."""
+    zero-fill decode, on a stratified sample, at the thread counts of thread_sweep, median of 5."""
     import oracle
 
     picked, sizes = stratified_sample(named, budget)
@@ -202,15 +210,10 @@ def cpu_baseline_topk(torch, named, ratio, budget=12_000_000):
             (vals, idx), _ = comp.compress(x, f"t{j}")
             oracle.topk_desparse(vals, idx, x.numel())
 
-    all_threads = torch.get_num_threads()
-    times = {}
-    for th in (1, all_threads):
-        torch.set_num_threads(th)
-        times[th] = _median_time(one)
-    torch.set_num_threads(all_threads)
+    times = thread_sweep(torch, one)
     alg = 16 * tot + 24 * sum(ks)
     best = min(times, key=lambda k: times[k])
-    return {"value": round(alg / times[best] / 1e9, 4), "unit": "GB/s", "cores": visible_cores(), "threads": best,
+    return {"value": round(alg / times[best] / 1e9, 4), "unit": "GB/s", "cores": best, "visible_cores": visible_cores(),
             "kind": "port",
             "cpu": cpu_model(),
             "sample": f"{len(picked)} of {len(sizes)} tensors ({tot} fp32 elements), Top-K k={ratio:g} with error "

@@ -7,6 +7,10 @@
 #   prof [tag] [args...]    rocprofv3 --kernel-trace --stats of bench.py (args: e.g. --codec topk)
 #   pmc [tag] [args...]     FETCH_SIZE / WRITE_SIZE passes of bench.py + pmc_traffic.json
 #   py <script> [args...]   any experiment script (its stdout -> gpurun_out/py.out)
+#   measure [tag]           the round's profile set: rocprofv3 kernel stats of the QSGD and the Top-K
+#                           bench lines, the two PMC passes (-> profiles/pmc_traffic.json, stamped with
+#                           the source digest; OMF_COMMIT names the commit), the bench line (reads the
+#                           fresh PMC file), the wire timings; copied into profiles/<tag>_*
 set -o pipefail
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp
 R=$(pwd)
@@ -64,6 +68,21 @@ case "$task" in
     shift || true
     timeout -k 10 900 python3 -u "$S" "$@" > gpurun_out/py.out 2> gpurun_out/py.err || { tail -30 gpurun_out/py.err; exit 2; }
     tail -c 20000 gpurun_out/py.out
+    ;;
+  measure)
+    T=${1:-r04}
+    bash scripts/gpu.sh prof ${T} > /dev/null || exit 2
+    bash scripts/gpu.sh prof ${T}_topk --codec topk > /dev/null || exit 3
+    bash scripts/gpu.sh pmc ${T} || exit 4
+    cp gpurun_out/${T}_pmc_traffic.json profiles/pmc_traffic.json
+    bash scripts/gpu.sh bench ${T} || exit 5
+    bash scripts/gpu.sh wire ${T} > /dev/null || exit 6
+    cp gpurun_out/${T}_kernel_stats.csv profiles/${T}_kernel_stats.csv
+    cp gpurun_out/${T}_topk_kernel_stats.csv profiles/${T}_topk_kernel_stats.csv
+    cp gpurun_out/${T}_bench.json profiles/${T}_bench.json
+    cp gpurun_out/${T}_wire.json profiles/${T}_wire.json
+    mkdir -p gpurun_out/profiles_copy && cp profiles/pmc_traffic.json profiles/${T}_* gpurun_out/profiles_copy/
+    echo "measure ok"
     ;;
   *)
     echo "unknown task $task"; exit 64 ;;
