@@ -2024,6 +2024,7 @@ static int upload_plan(omf_plan* p) {
                     hipMemcpyHostToDevice));
   OMF_HIP(hipMemset(p->d_spec_cnt, 0, 4 * (size_t)p->nt + 4));
   OMF_HIP(hipMemset(p->d_spec_flags, 0, 4 * (size_t)p->nt));
+  OMF_HIP(hipMemset(p->d_spec_status, 0, 4 * (size_t)p->nt));  // read by the repair launch
   OMF_HIP(hipMemset(p->d_spec_ngran, 0, 8 * (size_t)p->nt));  // epoch 0 is never a launch's tag
   OMF_HIP(hipMemset(p->d_ring_prof, 0, 8 * 16));
   OMF_HIP(hipMemcpy(p->d_enc[0], seq[0].data(), sizeof(Item) * seq[0].size(), hipMemcpyHostToDevice));
