@@ -243,7 +243,8 @@ def test_int32_payload_width(gpu):
     q, norms = plan.qsgd_encode(x, 8, seed=3)
     assert q.dtype == torch.int32
     y = plan.qsgd_decode(q, 32, 256, norms)
-    assert torch.isfinite(y).all()
+    for o, n in zip(plan.offsets, plan.sizes):  # tensor ranges (the arena padding is never written)
+        assert torch.isfinite(y[o:o + n]).all()
 
 
 def test_div(gpu):

@@ -206,7 +206,8 @@ def test_weighted_round_timeout_raises_on_every_rank(nccl1):
             with pytest.raises(RuntimeError, match="in-kernel timeout"):
                 qsgd_weighted_round(x, 2.0, 2.0, ops, 4, 0, mode="gather")
         out = qsgd_weighted_round(x, 2.0, 2.0, ops, 4, 1, mode="reduce")
-        assert bool(torch.isfinite(out).all())
+        for o, n in zip(plan.offsets, plan.sizes):  # tensor ranges (the arena padding is never written)
+            assert bool(torch.isfinite(out[o:o + n]).all())
 
 
 # ---------------------------------------------------------------- oracle pins (f2, bracketed L400)
@@ -449,7 +450,8 @@ def test_grid_encoder_against_the_oracle(gpu, cfg, s, alpha):
     # decode round trip stays the decoder's
     L = 2**s
     y = plan.qsgd_decode(q, 8 if L <= 127 else 32, L, norms)
-    assert bool(torch.isfinite(y[:plan.arena_end]).all())
+    for o, n in zip(plan.offsets, plan.sizes):  # tensor ranges: the decoder never writes the arena padding
+        assert bool(torch.isfinite(y[o:o + n]).all())
 
 
 def test_grid_encoder_barrier_timeout_recovers_exactly(gpu):
