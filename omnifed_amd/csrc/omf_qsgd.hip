@@ -459,20 +459,7 @@ struct SpecArgs {
   float* xout;
   uint32_t epoch;          // per-launch tag (never 0)
   int64_t nblocks;
-  // fused finish (the default): per-tensor arrival counters (zero between launches), each tensor's
-  // first spec block and block count, and the dispatch rotation (block b runs at b - shift)
-  uint32_t* tcnt;
-  const uint32_t* tblk0;
-  const uint32_t* tnblk;
-  int64_t shift;
 };
-
-__device__ __forceinline__ void st_agent32(uint32_t* p, uint32_t v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_agent32(const uint32_t* p) {
-  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 __device__ __forceinline__ uint32_t spec_hash(uint32_t a, uint32_t b) {
   uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
@@ -655,13 +642,9 @@ __device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t 
 // One block's pass: loads issued first, the Philox draws (independent of x) computed while
 // they are in flight, then the partial, the levels and the undecided list.  FULL: a whole
 // 4 Ki block (straight-line code, no bounds checks).
-// FUSED (the in-pass finish): an undecided quad's level is left to the fixer (each payload byte is
-// written once, by one workgroup), and the hand-off words — the wave's partial, its head, the listed
-// quads' indices and records — are agent-scope (sc1, write-through) stores, read by the tensor's
-// last-arriving workgroup inside this launch (cdna_hip_programming.md §6 Guideline 16, R1).
-template <int WIDTH, bool FULL, bool DIV, bool FUSED>
-__device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t sb, int64_t b, int64_t end, int32_t t,
-                                           int64_t tb, const SpecBracket& br, uint32_t* slot, uint64_t* part) {
+template <int WIDTH, bool FULL, bool DIV>
+__device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t end, int32_t t, int64_t tb,
+                                           const SpecBracket& br, uint32_t* slot, uint64_t* part) {
   const EncArgs& e = a.e;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float4 v[kSpecV];
@@ -703,24 +686,15 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t sb, int64_
       int32_t qq[4];
       bool und = false;
       spec_quad(v[k], uu[k], br.c_lo, br.c_hi, qq, und);
-      if (live && !(FUSED && und)) store_quad<WIDTH>(e, el, FULL ? el + 4 : end, qq);
+      if (live) store_quad<WIDTH>(e, el, FULL ? el + 4 : end, qq);
       const uint64_t m = __ballot(live && und);
       if (m) {  // rare: list this wave's undecided quads
         const uint32_t pos = cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         if (live && und && pos < (uint32_t)kSpecPerWave) {  // the quad, its x and its draws: no re-read
-          float4* rec = a.recs + 2 * ((sb * kWaves + wave) * kSpecPerWave + pos);
-          if (FUSED) {
-            st_agent32(&list[pos], (uint32_t)(el >> 2));
-            uint64_t* r64 = reinterpret_cast<uint64_t*>(rec);
-            st_agent(r64 + 0, ((uint64_t)__float_as_uint(v[k].y) << 32) | __float_as_uint(v[k].x));
-            st_agent(r64 + 1, ((uint64_t)__float_as_uint(v[k].w) << 32) | __float_as_uint(v[k].z));
-            st_agent(r64 + 2, ((uint64_t)__float_as_uint(uu[k].y) << 32) | __float_as_uint(uu[k].x));
-            st_agent(r64 + 3, ((uint64_t)__float_as_uint(uu[k].w) << 32) | __float_as_uint(uu[k].z));
-          } else {
-            list[pos] = (uint32_t)(el >> 2);
-            rec[0] = v[k];
-            rec[1] = uu[k];
-          }
+          list[pos] = (uint32_t)(el >> 2);
+          float4* rec = a.recs + 2 * ((blockIdx.x * kWaves + wave) * kSpecPerWave + pos);
+          rec[0] = v[k];
+          rec[1] = uu[k];
         }
         cnt += (uint32_t)__popcll(m);
       }
@@ -728,51 +702,19 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t sb, int64_
   }
   const double s = wave_sum_f64((double)acc);
   if (lane == 0) {
-    const uint32_t head = ((uint32_t)t << 8) | min(cnt, (uint32_t)kSpecPerWave);
-    if (FUSED) {
-      st_agent(part, (uint64_t)__double_as_longlong(s));
-      st_agent32(&a.heads[sb * kWaves + wave], head);
-    } else {
-      *part = (uint64_t)__double_as_longlong(s);
-      a.heads[sb * kWaves + wave] = head;
-    }
+    *part = (uint64_t)__double_as_longlong(s);
+    a.heads[blockIdx.x * kWaves + wave] = ((uint32_t)t << 8) | min(cnt, (uint32_t)kSpecPerWave);
     if (cnt > (uint32_t)kSpecPerWave)
       __hip_atomic_fetch_or(&a.flags[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
-template <int WIDTH>
-__device__ void spec_tensor_finish(const SpecArgs& a, int32_t t);
-
-// FUSED: every workgroup of tensor t arrives once its hand-off words are written (each wave's
-// vmcnt(0), a workgroup barrier, one agent-scope add); the last to arrive finishes the tensor.
-template <int WIDTH>
-__device__ __forceinline__ void spec_arrive(const SpecArgs& a, int32_t t) {
-  __shared__ uint32_t s_last;
-  drain_vmem();
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t last = add_agent(&a.tcnt[t], 1u) == a.tnblk[t] - 1u ? 1u : 0u;
-    if (last) st_agent32(&a.tcnt[t], 0u);  // ready for the next launch
-    s_last = last;
-  }
-  __syncthreads();
-  if (s_last) spec_tensor_finish<WIDTH>(a, t);
-}
-
 // The per-tensor tables are __restrict__ const kernel arguments so that they are read with
 // scalar loads (a vector load there is waited for before the x loads are issued).
-// FUSED: blocks run in a rotated order (block b at position b - shift, so that the last tensors to
-// complete are small ones: plan_spec_rotation) and each tensor's last-arriving workgroup folds its
-// norm and fixes its listed quads (spec_tensor_finish) while later tensors stream.
-template <int WIDTH, bool DIV, bool FUSED>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
+template <int WIDTH, bool DIV>
+__global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
                                                             const int64_t* __restrict__ begins) {
-  int64_t blk = blockIdx.x;
-  if (FUSED) {
-    blk += a.shift;
-    if (blk >= a.nblocks) blk -= a.nblocks;
-  }
+  const int64_t blk = blockIdx.x;
   const Item it = a.e.items[blk >> 2];
   const SpecBracket br = brs[it.tensor];
   const int64_t tb = begins[it.tensor];
@@ -782,20 +724,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(8))) v
   uint64_t* part = a.partials + blk * kWaves + wave;
   if (b >= it.end) {  // past the tensor's end: an empty block still reports (stale values otherwise)
     if ((threadIdx.x & 63) == 0) {
-      if (FUSED) {
-        st_agent(part, 0ull);
-        st_agent32(&a.heads[blk * kWaves + wave], (uint32_t)it.tensor << 8);
-      } else {
-        *part = 0ull;
-        a.heads[blk * kWaves + wave] = (uint32_t)it.tensor << 8;
-      }
+      *part = 0ull;
+      a.heads[blk * kWaves + wave] = (uint32_t)it.tensor << 8;
     }
-  } else {
-    const int64_t end = min(b + kSpecBlk, it.end);
-    if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, FUSED>(a, blk, b, end, it.tensor, tb, br, slot, part);
-    else spec_block<WIDTH, false, DIV, FUSED>(a, blk, b, end, it.tensor, tb, br, slot, part);
+    return;
   }
-  if (FUSED) spec_arrive<WIDTH>(a, it.tensor);
+  const int64_t end = min(b + kSpecBlk, it.end);
+  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV>(a, b, end, it.tensor, tb, br, slot, part);
+  else spec_block<WIDTH, false, DIV>(a, b, end, it.tensor, tb, br, slot, part);
 }
 
 // One fold segment (a workgroup of the finish launch); the last arriver of the tensor folds the
@@ -872,142 +808,6 @@ __device__ __forceinline__ bool spec_norm_wait(const SpecArgs& a, int32_t t, flo
   norm = __uint_as_float((uint32_t)g);
   bad = ((g >> 32) & 1u) != 0u;
   return true;
-}
-
-// The fused finish of tensor t, run by its last-arriving workgroup: the fold of spec_fold (the same
-// segments, the same arithmetic: the same norm bits), the bracket check, and — when the norm lies in
-// the bracket and no slot overflowed — every listed quad's exact level stored (the pass left those
-// bytes unwritten).  A bad tensor (norm outside its bracket, a slot overflow, a deferred sample) is
-// marked in status[t] and requantised whole by qsgd_spec_repair after the launch.  Every hand-off
-// word is read with agent-scope (sc1) loads.  Nothing here waits on another workgroup.
-constexpr int kFusedMaxSegs = 1024;  // fold segments of one tensor (plans beyond it take the finish launch)
-template <int WIDTH>
-__device__ void spec_tensor_finish(const SpecArgs& a, int32_t t) {
-  __shared__ double red[kWaves];
-  __shared__ double s_seg[kFusedMaxSegs];
-  __shared__ float s_norm;
-  __shared__ uint32_t s_ok;
-  const int64_t sb0 = a.tblk0[t], nsb = a.tnblk[t];
-  const int64_t p_begin = (int64_t)kWaves * sb0, p_end = p_begin + (int64_t)kWaves * nsb;
-  const int nsegs = (int)((p_end - p_begin + kSpecSeg - 1) / kSpecSeg);
-  if (a.dbg & 16u) {  // test hook (no fold): the launch reports an on-chip timeout, as the finish launch's waits do
-    if (threadIdx.x == 0) __hip_atomic_fetch_or(a.e.err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return;
-  }
-  double tot = 0.0;
-  constexpr int U = kSpecSeg / kThreads, UH = U / 2;  // two halves of 8 loads: the pass's VGPR budget
-  for (int sg = 0; sg < nsegs; ++sg) {
-    const int64_t pb = p_begin + (int64_t)sg * kSpecSeg, pe = min(p_end, pb + kSpecSeg);
-    double p = 0.0;  // spec_fold's order: partial i of the thread added for i = 0 .. U-1
-#pragma unroll
-    for (int hf = 0; hf < 2; ++hf) {
-      double v[UH];
-#pragma unroll
-      for (int i = 0; i < UH; ++i) {
-        const int64_t j = pb + threadIdx.x + (int64_t)(hf * UH + i) * kThreads;
-        const double d = __longlong_as_double((long long)ld_agent(&a.partials[j < pe ? j : pb]));  // unconditional
-        v[i] = j < pe ? d : 0.0;
-      }
-#pragma unroll
-      for (int i = 0; i < UH; ++i) p += v[i];
-    }
-    tot = block_sum_f64(p, red);
-    if (threadIdx.x == 0) s_seg[sg] = tot;
-  }
-  if (nsegs > 1) {
-    __syncthreads();
-    double q = 0.0;
-    for (int j = threadIdx.x; j < nsegs; j += kThreads) q += s_seg[j];
-    tot = block_sum_f64(q, red);
-  }
-  if (threadIdx.x == 0) {
-    const float norm = finish_norm(tot, kFmtF32);
-    a.e.norm_out[t] = norm;
-    const SpecBracket br = a.br[t];
-    const uint32_t fl = ld_agent32(&a.flags[t]);
-    const bool ok = br.mode == 0u && fl == 0u && norm >= br.n_lo && norm <= br.n_hi;
-    a.status[t] = ok ? 0u : 1u;
-    if (fl) st_agent32(&a.flags[t], 0u);
-    s_norm = norm;
-    s_ok = ok ? 1u : 0u;
-  }
-  __syncthreads();
-  if (!s_ok || (a.dbg & 8u)) return;
-  // the listed quads: wave slots [p_begin, p_end), 8 heads per thread in flight, then each slot's
-  // quads (their indices and records loaded together), the exact level, its store
-  const EncArgs& e = a.e;
-  const Divisor dv(s_norm);
-  const int64_t tend = a.begins[t] + a.sizes[t];
-  constexpr int H = 8;
-  for (int64_t w0 = p_begin; w0 < p_end; w0 += (int64_t)H * kThreads) {
-    uint32_t h[H];
-#pragma unroll
-    for (int i = 0; i < H; ++i) {
-      const int64_t ws = w0 + threadIdx.x + (int64_t)i * kThreads;
-      h[i] = ld_agent32(&a.heads[ws < p_end ? ws : p_begin]);
-      if (ws >= p_end) h[i] = 0u;
-    }
-#pragma unroll 1
-    for (int i = 0; i < H; ++i) {
-      const uint32_t cnt = h[i] & 0xffu;
-      if (!cnt) continue;
-      const int64_t ws = w0 + threadIdx.x + (int64_t)i * kThreads;
-      const uint32_t* sl = a.slots + (ws / kWaves) * kSpecSlot + kSpecPerWave * (int)(ws % kWaves);
-      const uint64_t* r64 = reinterpret_cast<const uint64_t*>(a.recs + 2 * (ws * kSpecPerWave));
-#pragma unroll 1
-      for (uint32_t j = 0; j < cnt; ++j) {  // one listed quad at a time (few VGPRs: the pass's occupancy)
-        const uint32_t qi = ld_agent32(sl + j);
-        uint64_t r[4];
-#pragma unroll
-        for (int c = 0; c < 4; ++c) r[c] = ld_agent(r64 + 4 * j + c);
-        const float4 xv = make_float4(__uint_as_float((uint32_t)r[0]), __uint_as_float((uint32_t)(r[0] >> 32)),
-                                      __uint_as_float((uint32_t)r[1]), __uint_as_float((uint32_t)(r[1] >> 32)));
-        const float4 uv = make_float4(__uint_as_float((uint32_t)r[2]), __uint_as_float((uint32_t)(r[2] >> 32)),
-                                      __uint_as_float((uint32_t)r[3]), __uint_as_float((uint32_t)(r[3] >> 32)));
-        int32_t qq[4];
-        qsgd_quad<false>(xv, uv, dv, e.levels, false, qq);
-        if (!(a.dbg & 4u)) store_quad<WIDTH>(e, 4 * (int64_t)qi, tend, qq);
-      }
-    }
-  }
-}
-
-// After a fused pass: the blocks of every tensor its finish marked bad are requantised whole from x
-// (the fused PS step: from the average the pass wrote), their norms as published.  One small launch;
-// with no bad tensor (the normal case) every workgroup reads the status words and exits.
-template <int WIDTH>
-__global__ __launch_bounds__(kThreads) void qsgd_spec_repair(SpecArgs a, const Item* __restrict__ items, int32_t nt) {
-  __shared__ int32_t s_bad[64];
-  __shared__ uint32_t s_nbad;
-  if (threadIdx.x == 0) s_nbad = 0u;
-  __syncthreads();
-  for (int32_t t = threadIdx.x; t < nt; t += kThreads)
-    if (a.status[t]) {
-      const uint32_t i = atomicAdd(&s_nbad, 1u);
-      if (i < 64u) s_bad[i] = t;
-    }
-  __syncthreads();
-  const uint32_t nbad = s_nbad;
-  if (!nbad) return;
-  EncArgs er = a.e;
-  if (a.divisor != 0.0f) {
-    er.x = a.xout;
-    er.alpha = 1.0f;
-  }
-  const bool listed = nbad <= 64u;  // else: scan every tensor's status
-  const int32_t nloop = listed ? (int32_t)nbad : nt;
-  for (int32_t i = 0; i < nloop; ++i) {
-    const int32_t t = listed ? s_bad[i] : i;
-    if (!listed && !a.status[t]) continue;
-    const int64_t sb0 = a.tblk0[t], nsb = a.tnblk[t];
-    const float norm = a.e.norm_out[t];
-    for (int64_t sb = sb0 + blockIdx.x; sb < sb0 + nsb; sb += gridDim.x) {
-      const Item it = items[sb >> 2];
-      const int64_t b = it.begin + (sb & 3) * kSpecBlk;
-      if (b < it.end)
-        quant_sub<WIDTH, false, kSpecV>(er, b, min(b + kSpecBlk, it.end), a.begins[t], t, norm);
-    }
-  }
 }
 
 // The finish launch: its first nfold workgroups fold the partials (spec_fold); the rest fix the
@@ -1551,13 +1351,6 @@ struct omf_plan {
   int32_t grid_wgs = 0;             // workgroups of a launch (CUs; 0 = unavailable)
   uint32_t* d_grid_pbeg = nullptr;  // per tensor: first flat item (one partial per item)
   uint32_t* d_grid_pcnt = nullptr;  // per tensor: flat items
-  // fused finish of the bracketed encoder: per-tensor arrival counters, first spec block and block
-  // count, the dispatch rotation, and whether every tensor's fold fits one workgroup's LDS
-  uint32_t* d_spec_tcnt = nullptr;
-  uint32_t* d_spec_tblk0 = nullptr;
-  uint32_t* d_spec_tnblk = nullptr;
-  int64_t spec_shift = 0;
-  bool spec_fused_ok = false;
   unsigned long long* d_grid_bar = nullptr;  // arrival counter (zeroed at upload)
   uint64_t grid_launches = 0;
   // Top-K tiled decode: per-ratio constant tables (omf_topk.hip), allocated on first use, with
@@ -1576,33 +1369,6 @@ struct omf_plan {
   hipStream_t last_stream = nullptr;
   bool last_valid = false;
 };
-
-// The fused bracketed pass runs its blocks rotated (block b at position b - shift, mod nblocks):
-// each tensor's finish (fold + fixes, by its last-arriving workgroup) runs while later blocks stream,
-// so the launch ends when the last tensor's finish does.  A finish is modelled as ~900 block
-// dispatches of fold latency plus ~5 per block of the tensor (its wave slots scanned by one
-// workgroup, one listed quad per round trip: ~120 us for a 32 Mi-element vocabulary matrix at ~300
-// blocks per us); the
-// shift is the tensor start that minimises the latest modelled end, so small tensors come last and
-// the largest ones early (Llama-400M: a layer's gate_proj, the attention projections last).
-static int64_t plan_spec_rotation(const std::vector<uint32_t>& tblk0, const std::vector<uint32_t>& tnblk,
-                                  int64_t nblocks) {
-  int64_t best = 0, best_end = INT64_MAX;
-  for (size_t c = 0; c < tblk0.size(); ++c) {
-    const int64_t shift = tblk0[c];
-    int64_t end = nblocks;
-    for (size_t t = 0; t < tblk0.size(); ++t) {
-      int64_t last = (int64_t)tblk0[t] + tnblk[t] - 1 - shift;  // position of the tensor's last block
-      if (last < 0) last += nblocks;
-      end = std::max(end, last + 1 + 900 + 5 * (int64_t)tnblk[t]);
-    }
-    if (end < best_end) {
-      best_end = end;
-      best = shift;
-    }
-  }
-  return best;
-}
 
 // Order this launch after the plan's previous stateful launch when the stream changes: the event is
 // recorded on the previous stream at the switch (it covers everything enqueued there so far, the
@@ -1959,17 +1725,6 @@ static int upload_plan(omf_plan* p) {
   const size_t o_g_pbeg = o; o = round16(o + 4 * (size_t)p->nt);
   const size_t o_g_pcnt = o; o = round16(o + 4 * (size_t)p->nt);
   const size_t o_g_bar = o; o = round16(o + 16);
-  const size_t o_sp_tcnt = o; o = round16(o + 4 * (size_t)p->nt);
-  const size_t o_sp_tblk0 = o; o = round16(o + 4 * (size_t)p->nt);
-  const size_t o_sp_tnblk = o; o = round16(o + 4 * (size_t)p->nt);
-  std::vector<uint32_t> tblk0((size_t)p->nt), tnblk((size_t)p->nt);
-  p->spec_fused_ok = true;
-  for (int32_t t = 0; t < p->nt; ++t) {
-    tblk0[(size_t)t] = 4u * gpbeg[(size_t)t];
-    tnblk[(size_t)t] = 4u * gpcnt[(size_t)t];
-    if ((int64_t)kWaves * tnblk[(size_t)t] > (int64_t)kFusedMaxSegs * kSpecSeg) p->spec_fused_ok = false;
-  }
-  p->spec_shift = plan_spec_rotation(tblk0, tnblk, p->n_spec_blocks);
   DeviceGuard g(p->device);
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   if (p->d_block) {
@@ -2009,12 +1764,6 @@ static int upload_plan(omf_plan* p) {
   p->d_grid_pbeg = reinterpret_cast<uint32_t*>(base + o_g_pbeg);
   p->d_grid_pcnt = reinterpret_cast<uint32_t*>(base + o_g_pcnt);
   p->d_grid_bar = reinterpret_cast<unsigned long long*>(base + o_g_bar);
-  p->d_spec_tcnt = reinterpret_cast<uint32_t*>(base + o_sp_tcnt);
-  p->d_spec_tblk0 = reinterpret_cast<uint32_t*>(base + o_sp_tblk0);
-  p->d_spec_tnblk = reinterpret_cast<uint32_t*>(base + o_sp_tnblk);
-  OMF_HIP(hipMemset(p->d_spec_tcnt, 0, 4 * (size_t)p->nt));
-  OMF_HIP(hipMemcpy(p->d_spec_tblk0, tblk0.data(), 4 * tblk0.size(), hipMemcpyHostToDevice));
-  OMF_HIP(hipMemcpy(p->d_spec_tnblk, tnblk.data(), 4 * tnblk.size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_grid_pbeg, gpbeg.data(), 4 * gpbeg.size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemcpy(p->d_grid_pcnt, gpcnt.data(), 4 * gpcnt.size(), hipMemcpyHostToDevice));
   OMF_HIP(hipMemset(p->d_grid_bar, 0, 16));
@@ -2024,7 +1773,7 @@ static int upload_plan(omf_plan* p) {
                     hipMemcpyHostToDevice));
   OMF_HIP(hipMemset(p->d_spec_cnt, 0, 4 * (size_t)p->nt + 4));
   OMF_HIP(hipMemset(p->d_spec_flags, 0, 4 * (size_t)p->nt));
-  OMF_HIP(hipMemset(p->d_spec_status, 0, 4 * (size_t)p->nt));  // read by the repair launch
+  OMF_HIP(hipMemset(p->d_spec_status, 0, 4 * (size_t)p->nt));  // spec_stats reads them before any encode
   OMF_HIP(hipMemset(p->d_spec_ngran, 0, 8 * (size_t)p->nt));  // epoch 0 is never a launch's tag
   OMF_HIP(hipMemset(p->d_ring_prof, 0, 8 * 16));
   OMF_HIP(hipMemcpy(p->d_enc[0], seq[0].data(), sizeof(Item) * seq[0].size(), hipMemcpyHostToDevice));
@@ -2215,7 +1964,7 @@ int omf_plan_set_resident_capacity(omf_plan* plan, int64_t cap, int64_t wait_us)
 int omf_plan_set_debug(omf_plan* plan, uint32_t ring_dbg, uint32_t spec_dbg, int64_t lds_wait_us) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
   if (lds_wait_us < 0) return fail(OMF_EINVAL, "lds_wait_us must be >= 0");
-  if ((ring_dbg & ~15u) || (spec_dbg & ~1023u)) return fail(OMF_EINVAL, "omf_plan_set_debug: unknown switch bits");
+  if ((ring_dbg & ~15u) || (spec_dbg & ~511u)) return fail(OMF_EINVAL, "omf_plan_set_debug: unknown switch bits");
   plan->ring_dbg = ring_dbg;
   plan->spec_skip = spec_dbg;
   plan->lds_wait_ticks = lds_wait_us > 0 ? (uint64_t)lds_wait_us * 100ull : kWaitTicks;
@@ -2389,36 +2138,16 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.flags = p->d_spec_flags;
     sa.status = p->d_spec_status;
     sa.nblocks = p->n_spec_blocks;
-    sa.tcnt = p->d_spec_tcnt;
-    sa.tblk0 = p->d_spec_tblk0;
-    sa.tnblk = p->d_spec_tnblk;
-    sa.shift = p->spec_shift;
     const dim3 gbr((unsigned)p->n_spec_br), gb((unsigned)p->n_spec_blocks);
     // p->spec_skip: test / experiment switches (omf_plan_set_debug; 0 in production): bit 0
-    // skips the bracket launch (the previous brackets stay), bit 1 the finish launch (fused: the
-    // repair launch), bits 2/3 the fix stores / the fix, bit 4 the fold — the payload is then not
-    // the encoder's; bit 9 takes the separate finish launch instead of the fused finish.
+    // skips the bracket launch (the previous brackets stay), bit 1 the finish launch, bits 2/3
+    // the fix stores / the fix, bit 4 the fold — the payload is then not the encoder's.
     if (!(p->spec_skip & 1u)) hipLaunchKernelGGL(qsgd_spec_bracket, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
     const bool div = divisor != 0.0f;
-    if (p->spec_fused_ok && !(p->spec_skip & 512u)) {
-      // the default: ONE pass launch that folds and fixes each tensor as it completes, then the
-      // repair launch (normally every workgroup reads the status words and exits)
-      if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
-      else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
-      else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
-      else hipLaunchKernelGGL((qsgd_spec_quant<4, true, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
-      if (!(p->spec_skip & 2u)) {
-        const dim3 grep((unsigned)std::min<int64_t>(256, p->n_spec_blocks));
-        if (width == 1) hipLaunchKernelGGL(qsgd_spec_repair<1>, grep, blk, 0, st, sa, (const Item*)a.items, p->nt);
-        else hipLaunchKernelGGL(qsgd_spec_repair<4>, grep, blk, 0, st, sa, (const Item*)a.items, p->nt);
-      }
-      OMF_HIP(hipGetLastError());
-      return OMF_OK;
-    }
-    if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
-    else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
-    else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
-    else hipLaunchKernelGGL((qsgd_spec_quant<4, true, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    else hipLaunchKernelGGL((qsgd_spec_quant<4, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
     if (p->spec_skip & 2u) {  // experiment: no finish launch (timings only)
       OMF_HIP(hipGetLastError());
       return OMF_OK;

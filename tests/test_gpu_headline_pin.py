@@ -71,52 +71,3 @@ def test_headline_arena_every_tensor_equals_oracle(gpu, cfg, s, alpha):
     with ThreadPoolExecutor(_threads()) as ex:
         errors = [e for e in ex.map(check, range(len(sizes))) if e]
     assert not errors, errors[:5]
-
-
-SPEC_LEGACY_FINISH = 512  # omf_plan_set_debug spec bit: the separate finish launch instead of the fused finish
-
-
-@pytest.mark.parametrize("case", ["llama400m", "mixed", "degenerate", "ps_step"])
-def test_fused_finish_equals_finish_launch(gpu, case):
-    """The bracketed encoder's fused finish (each tensor folded and fixed by its last-arriving pass
-    workgroup, blocks in the rotated order, the repair launch for bad tensors) writes the same payload
-    and norms, bit for bit, as the separate finish launch — on the bench arena, on mixed sizes, on
-    tensors whose sampled bracket is degenerate or misses the norm (requantised whole by the repair
-    launch), and in the fused PS step (divide + encode)."""
-    if case == "llama400m":
-        sizes = [shapes.numel(sh) for _, sh in shapes.model_shapes("llama400m")]
-    else:
-        sizes = [5, 16384, 70001, 1 << 20, 3000, 2_000_000, 1 << 25, 777_777, 4096 * 3 + 1]
-    plan = codec.Plan(sizes, device=gpu)
-    if plan.strategy != "bracket":
-        plan.set_encode_strategy("bracket")
-    g = torch.Generator(device=gpu).manual_seed(77)
-    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
-    if case == "degenerate":  # a zero tensor, a single spike (degenerate samples), a spiky tensor (bracket misses)
-        o1, o3, o5 = plan.offsets[1], plan.offsets[3], plan.offsets[5]
-        x[o1:o1 + sizes[1]] = 0.0
-        x[o3:o3 + sizes[3]] = 0.0
-        x[o3 + 12345] = 5.0
-        x[o5:o5 + sizes[5]:997] *= 4000.0
-    outs = []
-    for legacy in (False, True):
-        plan.set_debug(spec=SPEC_LEGACY_FINISH if legacy else 0)
-        try:
-            if case == "ps_step":
-                avg, q, n = plan.ps_apply_encode(x, 7.0, 4, seed=5, offset=2)
-                outs.append((q.clone(), n.clone(), avg.clone()))
-            else:
-                q, n = plan.qsgd_encode(x, 4, alpha=3.0, seed=5, offset=2)
-                outs.append((q.clone(), n.clone(), None))
-            stats = plan.spec_stats()
-            plan.check()
-        finally:
-            plan.set_debug()
-        if case == "degenerate":
-            assert stats["whole"] >= 2, stats  # the repair path ran
-    (qa, na, aa), (qb, nb, ab) = outs
-    assert torch.equal(na, nb)
-    for t, (o, n) in enumerate(zip(plan.offsets, sizes)):  # tensor ranges (arena padding is never written)
-        assert torch.equal(qa[o:o + n], qb[o:o + n]), t
-        if aa is not None:
-            assert torch.equal(aa[o:o + n], ab[o:o + n]), t
