@@ -1,0 +1,42 @@
+"""Encode / step time of one library build (OMF_CODEC_LIB_EXPERIMENT selects a variant), Llama-400M
+s = 4 bracketed encoder: HIP events around 20 calls, median of 7 rounds.  One JSON line."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from omnifed_amd import codec, shapes  # noqa: E402
+
+dev = torch.device("cuda", 0)
+sizes = [shapes.numel(s) for _, s in shapes.model_shapes(sys.argv[1] if len(sys.argv) > 1 else "llama400m")]
+p = codec.Plan.get(sizes, device=dev)
+g = torch.Generator(device=dev).manual_seed(1000)
+x = torch.randn(p.arena_end, device=dev, generator=g) * 1e-3
+q = torch.empty(p.payload_elems(8), dtype=torch.int8, device=dev)
+nr = torch.empty(p.nt, device=dev)
+y = torch.empty(p.arena_end, device=dev)
+st = torch.cuda.current_stream(dev)
+
+
+def tm(fn, reps=20):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn(0)
+    a.record(st)
+    for i in range(reps):
+        fn(i)
+    b.record(st)
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / reps
+
+
+enc, step = [], []
+for _ in range(7):
+    enc.append(tm(lambda i: p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=7, offset=i)))
+    step.append(tm(lambda i: (p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=7, offset=i),
+                              p.qsgd_decode(q, 8, 16, nr, y_out=y))))
+p.check()
+print(json.dumps({"lib": os.path.basename(os.environ.get("OMF_CODEC_LIB_EXPERIMENT", "base")),
+                  "enc_ms": round(sorted(enc)[3], 4), "step_ms": round(sorted(step)[3], 4),
+                  "payload_sha": __import__("hashlib").sha256(q.cpu().numpy().tobytes()).hexdigest()[:16]}), flush=True)
