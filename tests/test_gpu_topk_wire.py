@@ -259,3 +259,31 @@ def test_topk_decode_counts_modes_and_absent_tensors(gpu):
             assert yh[o:o + n].numpy().tobytes() == want[o:o + n].numpy().tobytes(), mode
     with pytest.raises(ValueError):
         plan.topk_decode_counts([50, 0, 18, 2000], v, ix)  # 18 values for a 17-element tensor
+
+
+def test_topk_wire_full_llama400m_equals_per_layer(gpu):
+    """The bench's arena through the drop-in: the batched encode_updates_dict of the whole
+    Llama-400M update (k = 1 %, weighting fused, two error-feedback calls) equals the per-layer
+    encode_layer_state loop byte for byte, and the batched decode_updates_dict / PS accumulate of
+    that message equal the per-layer decodes, bit for bit."""
+    from omnifed_amd import shapes
+    from omnifed_amd.ps import DeviceAggregator
+
+    named = shapes.model_shapes("llama400m")
+    g = torch.Generator(device=gpu).manual_seed(1000)
+    a = TopKCompression(device=gpu, compress_ratio=0.01)
+    b = TopKCompression(device=gpu, compress_ratio=0.01)
+    for call in range(2):
+        upd = {n: torch.randn(s, device=gpu, generator=g) * 1e-3 for n, s in named}
+        got = encode_updates_dict(upd, a, weight=3.0)
+        want = [encode_layer_state(n, t, b, weight=3.0) for n, t in upd.items()]
+        for L, P in zip(got, want):
+            assert L.SerializeToString() == P.SerializeToString(), (call, L.layer_name)
+        del upd
+    out = decode_updates_dict(got, device="cuda")
+    agg = DeviceAggregator(named, device=gpu)
+    agg.accumulate_layers(got, 3)
+    for L in got:
+        ref = decode_layer_tensor(L, device="cuda")
+        assert torch.equal(out[L.layer_name], ref), L.layer_name
+        assert torch.equal(agg._slice(L.layer_name), ref.reshape(-1)), L.layer_name
