@@ -6,6 +6,7 @@
 #   bench [tag] [args...]   bench.py line -> gpurun_out/<tag>_bench.json
 #   prof [tag] [args...]    rocprofv3 --kernel-trace --stats of bench.py (args: e.g. --codec topk)
 #   pmc [tag] [args...]     FETCH_SIZE / WRITE_SIZE passes of bench.py + pmc_traffic.json
+#   sq [tag]                SQ counter passes of the ResNet-18 encoders -> gpurun_out/<tag>_sq.json
 #   py <script> [args...]   any experiment script (its stdout -> gpurun_out/py.out)
 #   measure [tag]           the round's profile set: rocprofv3 kernel stats of the QSGD and the Top-K
 #                           bench lines, the two PMC passes (-> profiles/pmc_traffic.json, stamped with
@@ -62,6 +63,21 @@ case "$task" in
     python3 scripts/pmc_traffic.py gpurun_out/${T}_pmc_FETCH_SIZE gpurun_out/${T}_pmc_WRITE_SIZE \
       gpurun_out/${T}_pmc_traffic.json llama400m 4 || exit 3
     cat gpurun_out/${T}_pmc_traffic.json
+    ;;
+  sq)
+    # SQ counter passes (VALU work, wave-cycle split) over the ResNet-18 encoder A/B
+    # (scripts/exp/r18_ab.py: ring, grid, two-launch encoders and the decoder), one pass per group
+    T=${1:-r04_r18}
+    i=0
+    for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" \
+               "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAVES SQ_INSTS_SMEM"; do
+      i=$((i+1))
+      rm -rf gpurun_out/${T}_sq$i
+      timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$R/gpurun_out/${T}_sq$i" -o run \
+        -- python3 "$R/scripts/exp/r18_ab.py" 3 1 > gpurun_out/${T}_sq$i.log 2>&1 || { tail -20 gpurun_out/${T}_sq$i.log; exit 2; }
+    done
+    E=$(python3 -c "from omnifed_amd import shapes; print(sum(shapes.numel(s) for _, s in shapes.model_shapes('resnet18')))")
+    python3 scripts/sq_summary.py gpurun_out/${T}_sq.json "$E" gpurun_out/${T}_sq1 gpurun_out/${T}_sq2 || exit 3
     ;;
   py)
     S=$1
