@@ -102,6 +102,11 @@ def init_dist(torch, dist, force: bool = False):
 
 # ---------------------------------------------------------------- CPU baseline
 
+def progress(msg: str) -> None:
+    """One line on stderr per leg (long runs stay visibly alive; stdout carries only the JSON line)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -113,12 +118,32 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def visible_cores() -> int:
-    """CPU cores this process may run on (its affinity mask), which the thread counts are drawn from."""
+def affinity_cores() -> int:
+    """CPUs in this process's affinity mask (on the GPU box: every CPU of the machine)."""
     try:
         return len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover - non-Linux
         return os.cpu_count() or 1
+
+
+def cgroup_cpu_quota():
+    """The cgroup v2 CPU quota in whole CPUs (``cpu.max``: quota period), None when unlimited or absent."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+    except (OSError, ValueError):
+        return None
+    if quota == "max":
+        return None
+    return max(1, int(int(quota) // int(period)))
+
+
+def visible_cores() -> int:
+    """CPUs this process can actually use: its affinity mask, capped by its cgroup CPU quota (the GPU
+    box's affinity mask shows the whole machine while the job's share is 16 CPUs; torch at 256 threads
+    on a 16-CPU quota only thrashes)."""
+    q = cgroup_cpu_quota()
+    return min(affinity_cores(), q) if q else affinity_cores()
 
 
 def stratified_sample(named, budget):
@@ -149,6 +174,7 @@ def thread_sweep(torch, fn):
     for th in sorted({1, default, visible_cores()}):
         torch.set_num_threads(th)
         times[th] = _median_time(fn)
+        progress(f"cpu baseline at {th} threads: {times[th]:.3f} s per sample")
     torch.set_num_threads(default)
     return times
 
@@ -183,6 +209,7 @@ def cpu_baseline(torch, named, bits, budget=40_000_000):
         "unit": "GB/s",
         "cores": best,
         "visible_cores": visible_cores(),
+        "affinity_cores": affinity_cores(),
         "kind": "port",
         "cpu": cpu_model(),
         "sample": f"{len(picked)} of {len(sizes)} tensors (every {max(1, int(np.ceil(N / budget)))}th; {tot} of {N} "
@@ -214,7 +241,7 @@ def cpu_baseline_topk(torch, named, ratio, budget=12_000_000):
     alg = 16 * tot + 24 * sum(ks)
     best = min(times, key=lambda k: times[k])
     return {"value": round(alg / times[best] / 1e9, 4), "unit": "GB/s", "cores": best, "visible_cores": visible_cores(),
-            "kind": "port",
+            "affinity_cores": affinity_cores(), "kind": "port",
             "cpu": cpu_model(),
             "sample": f"{len(picked)} of {len(sizes)} tensors ({tot} fp32 elements), Top-K k={ratio:g} with error "
                       f"feedback + zero-fill decode, median of 5 after 1 warm-up",
@@ -324,6 +351,7 @@ def main():
 
     qsgd = None
     if args.codec == "qsgd":
+        progress("qsgd steps")
         for i in range(args.warmup):
             q_step(i)
         plan.check()
@@ -356,6 +384,7 @@ def main():
     # ------------------------------------------------------------ Top-K
     topk = None
     if args.codec == "topk" or not args.no_topk:
+        progress("topk steps")
         ratio = args.ratio
         ks = plan.topk_ks(ratio)
         K = sum(ks)
@@ -401,6 +430,7 @@ def main():
     if not args.no_extras and world == 1 and qsgd is not None and args.config == "llama400m":
         # the other QSGD configs of BASELINE.json on one GPU: ResNet-18 at "8 levels" (s = 3, int8)
         # and the base default s = 8 (int32 wire), Llama-150M at the presets' s = 4
+        progress("other configs")
         others = {}
         for cname, bits in (("resnet18", 3), ("resnet18", 8), ("llama150m", 4)):
             sz = [shapes.numel(sh) for _, sh in shapes.model_shapes(cname)]
@@ -426,6 +456,7 @@ def main():
             del xo, qo, no, yo
         extras["other_configs"] = others
     if not args.no_extras and world == 1 and qsgd is not None:
+        progress("pcie-inclusive rate")
         # PCIe-inclusive rate: host fp32 in -> device encode -> host payload; host payload -> decode -> host fp32
         xh = torch.empty(plan.arena_end, dtype=torch.float32, pin_memory=True)
         xh.copy_(x, non_blocking=False)
@@ -453,6 +484,7 @@ def main():
                                     "fp32_gradient_GBs": round(4 * N / pt / 1e9, 2)}
         del xh, qh, yh, xd
     if not args.no_extras and dist.is_initialized():
+        progress("PS aggregates over the process group")
         from omnifed_amd.ps import GpuOps, qsgd_weighted_round, topk_sparse_aggregate, total_weight
 
         ops = GpuOps(plan, seed=seed)
