@@ -67,8 +67,10 @@ def _host_memory_policy() -> bool:
         if _HOST_POLICY:
             logging.getLogger("omnifed_amd").info(
                 "omnifed_amd: glibc malloc now keeps freed wire-message memory for reuse (mmap threshold 32 MiB, "
-                "trim threshold 1 GiB per arena; resident size may stay ~one round's payload higher). "
-                "OMF_RETAIN_HOST_MEMORY=0 leaves glibc's defaults alone (INTEGRATION.md §3c).")
+                "trim threshold 1 GiB per arena; resident size may stay ~one round's payload higher), and "
+                "decoded arenas returned on the CPU reuse pooled pages (hostio.HOST_ARENAS, up to 8 GiB kept). "
+                "OMF_RETAIN_HOST_MEMORY=0 leaves glibc's defaults alone and allocates every arena afresh "
+                "(INTEGRATION.md §3c).")
     return _HOST_POLICY
 
 
@@ -673,7 +675,7 @@ def decode_updates_dict(proto_layers, *, base_updates: Optional[Dict[str, torch.
         for layers in groups.values():
             y, plan = _decode_qsgd_batch(layers, dev)
             if out_dev.type == "cpu":
-                y = y.cpu()  # one D2H for the whole group; returned tensors are views of it
+                y = hostio.device_to_host(y, pool_memory=_HOST_POLICY)  # one chunked D2H; tensors are views
             for L, o, n in zip(layers, plan.offsets, plan.sizes):
                 decoded[L.layer_name] = y[o:o + n].view(tuple(L.original_shape))
     if base_updates is not None:  # overlays decode layer by layer, on their bases' devices
@@ -681,7 +683,7 @@ def decode_updates_dict(proto_layers, *, base_updates: Optional[Dict[str, torch.
     if topk and _topk_batch_ok(topk):
         y, plan = _decode_topk_batch(topk, _gpu_for(out_dev))
         if out_dev.type == "cpu":
-            y = y.cpu()
+            y = hostio.device_to_host(y, pool_memory=_HOST_POLICY)
         for (L, *_), o, n in zip(topk, plan.offsets, plan.sizes):
             decoded[L.layer_name] = y[o:o + n].view(tuple(L.original_shape))
             topk_done.add(id(L))

@@ -175,3 +175,26 @@ def test_client_and_ps_threads_unlocked_on_different_plans(gpu):
         th.join()
     assert res["ps"] == want[0]
     assert res["client"] == want[1]
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.int8])
+def test_device_to_host_ring_equals_cpu(gpu, dtype):
+    """hostio.device_to_host (the CPU placement's chunked D2H): same bytes as .cpu() for empty,
+    odd-sized and many-chunk tensors, the ring wrapping several times (small chunks, 3 slots), from
+    the main thread and from concurrent threads (each call leases its own ring)."""
+    from omnifed_amd import hostio
+
+    g = torch.Generator(device=gpu).manual_seed(5)
+    srcs = [torch.empty(0, device=gpu, dtype=dtype)]
+    for n in (1, 4099, 3 * (1 << 20) + 5):
+        t = torch.randn(n, device=gpu, generator=g) * 100
+        srcs.append(t.to(dtype))
+    for s in srcs:
+        out = hostio.device_to_host(s, limit=1 << 16, slots=3)
+        assert out.device.type == "cpu" and out.dtype == dtype and not out.is_pinned()
+        assert torch.equal(out, s.cpu())
+        assert torch.equal(hostio.device_to_host(s), s.cpu())
+    with ThreadPoolExecutor(4) as ex:
+        outs = list(ex.map(lambda s: hostio.device_to_host(s, limit=1 << 16, slots=3), srcs * 2))
+    for o, s in zip(outs, srcs * 2):
+        assert torch.equal(o, s.cpu())

@@ -165,3 +165,30 @@ def test_shared_arena_detection():
     assert shared_arena([buf[0:10].double(), buf[64:164], buf[192:195]], dev, P) is None  # not fp32
     assert shared_arena([buf[0:10], buf[64:164], buf[192:195]], dev, type("Q", (), {
         "offsets": [0, 64, 192], "sizes": [10, 100, 200], "arena_end": 392})) is None  # storage too short
+
+
+def test_host_arena_pool_reuses_pages_and_honours_its_budget():
+    """Pooled pageable arenas (hostio.HostArenaPool): ordinary writable CPU tensors; the memory of a
+    dropped arena (every view gone) serves the next one; free arenas above the budget are released."""
+    import gc
+
+    P = hostio.HostArenaPool(max_bytes=200 << 20)
+    t = P.empty(4000).view(torch.float32)
+    assert t.numel() == 1000 and not t.is_pinned()
+    t.fill_(2.0)
+    view = t[10:20]
+    p = t.data_ptr()
+    del t
+    gc.collect()
+    assert P.free_bytes() == 0  # a view still holds the arena
+    assert float(view.sum()) == 20.0
+    del view
+    gc.collect()
+    assert P.free_bytes() == P.GRAIN
+    u = P.empty(100)
+    assert u.data_ptr() == p and P.free_bytes() == 0
+    a, b = P.empty(100 << 20), P.empty(100 << 20)  # 128 MiB each (64 MiB grain)
+    del u, a, b
+    gc.collect()
+    assert P.free_bytes() == P.GRAIN + (128 << 20)  # 64 + 128 + 128 MiB freed, 200 MiB kept at most
+    assert P.empty(0).numel() == 0
