@@ -20,6 +20,7 @@ from collections import defaultdict
 
 
 def short(name):
+    name = re.sub(r"^void\s+", "", name.replace("(anonymous namespace)::", ""))
     m = re.search(r"([A-Za-z_][A-Za-z0-9_]*)\s*[<(]", name)
     return m.group(1) if m else name
 
