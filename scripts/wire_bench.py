@@ -35,6 +35,10 @@ N = sum(t.numel() for t in upd.values())
 targets = {n: torch.empty_like(t) for n, t in upd.items()}
 
 
+def progress(msg):
+    print(f"[wire {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def tm(fn, reps=7, warm=3):
     for _ in range(warm):  # steady state: the retained host memory and the copy threads warmed up
         fn()
@@ -52,6 +56,7 @@ def leg(comp, tag):
     """The wire legs of one compressor; returns a dict of medians (ms) and rates."""
     r = {}
     st = {}
+    progress(f"{tag} legs")
     layers = encode_updates_dict(upd, comp, stats=st)
     r["wire"] = st
     r["encode_updates_dict_ms"] = tm(lambda: encode_updates_dict(upd, comp))
@@ -83,6 +88,7 @@ qcomp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device
 res["qsgd_s4"], layers = leg(qcomp, "qsgd")
 tcomp = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
 res["topk_1pct"], tlayers = leg(tcomp, "topk")
+progress("per-layer Top-K loop, copy threads, device-side steps")
 # the round-3 per-layer Top-K loop (one encode + host wait + small D2H per tensor), for comparison
 tper = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
 res["topk_1pct"]["per_layer_encode_ms"] = tm(lambda: [encode_layer_state(n, t, tper) for n, t in upd.items()],
