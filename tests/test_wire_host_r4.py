@@ -192,3 +192,41 @@ def test_host_arena_pool_reuses_pages_and_honours_its_budget():
     gc.collect()
     assert P.free_bytes() == P.GRAIN + (128 << 20)  # 64 + 128 + 128 MiB freed, 200 MiB kept at most
     assert P.empty(0).numel() == 0
+
+
+def test_host_arena_pool_threads_never_share_live_memory():
+    """Concurrent callers (gRPC worker threads) take and drop arenas: two live arenas never overlap,
+    and every returned arena is reusable."""
+    import gc
+
+    P = hostio.HostArenaPool(max_bytes=1 << 30)
+    errors = []
+    live = {}
+    lock = threading.Lock()
+
+    def work(seed):
+        try:
+            for i in range(30):
+                n = 1000 + 997 * ((seed * 31 + i) % 50)
+                t = P.empty(n)
+                a, b = t.data_ptr(), t.data_ptr() + n
+                with lock:
+                    for (x, y) in live.values():
+                        assert b <= x or y <= a, "two live arenas overlap"
+                    live[id(t)] = (a, b)
+                t.fill_(seed)
+                assert int(t.min()) == seed and int(t.max()) == seed
+                with lock:
+                    del live[id(t)]
+                del t
+        except Exception as e:  # pragma: no cover - reported below
+            errors.append(e)
+
+    ts = [threading.Thread(target=work, args=(s,)) for s in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    gc.collect()
+    assert not errors, errors
+    assert P.free_bytes() > 0
