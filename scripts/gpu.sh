@@ -6,6 +6,7 @@
 #   bench [tag] [args...]   bench.py line -> gpurun_out/<tag>_bench.json
 #   prof [tag] [args...]    rocprofv3 --kernel-trace --stats of bench.py (args: e.g. --codec topk)
 #   pmc [tag] [args...]     FETCH_SIZE / WRITE_SIZE passes of bench.py + pmc_traffic.json
+#                           (PMC_CFG / PMC_BITS name the config when args change it)
 #   sq [tag]                SQ counter passes of the ResNet-18 encoders -> gpurun_out/<tag>_sq.json
 #   py <script> [args...]   any experiment script (its stdout -> gpurun_out/py.out)
 #   measure [tag]           the round's profile set: rocprofv3 kernel stats of the QSGD and the Top-K
@@ -61,7 +62,7 @@ case "$task" in
         > gpurun_out/${T}_pmc_$c.log 2>&1 || { tail -20 gpurun_out/${T}_pmc_$c.log; exit 2; }
     done
     python3 scripts/pmc_traffic.py gpurun_out/${T}_pmc_FETCH_SIZE gpurun_out/${T}_pmc_WRITE_SIZE \
-      gpurun_out/${T}_pmc_traffic.json llama400m 4 || exit 3
+      gpurun_out/${T}_pmc_traffic.json ${PMC_CFG:-llama400m} ${PMC_BITS:-4} || exit 3
     cat gpurun_out/${T}_pmc_traffic.json
     ;;
   sq)
