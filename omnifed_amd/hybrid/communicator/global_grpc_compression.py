@@ -276,12 +276,24 @@ def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, dev
     dev = _gpu_for(out_dev)
     v = torch.from_numpy(values.copy()).to(dev)
     ix = torch.from_numpy(np.array(indices, dtype=np.int64, copy=True)).to(dev)
-    y = torch.empty(max(numel, 4), dtype=torch.float32, device=dev)
     if base_tensor is not None:
+        # the reference overlays a numpy copy of the base, so the result has the base's dtype
+        # (fp32 values cast on assignment: round-to-nearest for fp16, truncation for integers) and
+        # a bf16 base fails in .numpy() as it does there
+        bdt = base_tensor.dtype
+        if bdt == torch.bfloat16:
+            raise TypeError("Got unsupported ScalarType BFloat16")
+        if bdt == torch.float64:  # the fp32 kernel cannot hold the base exactly
+            flat = base_tensor.detach().reshape(-1).to(dev, torch.float64, copy=True)
+            flat[ix] = v.double()
+            return flat.reshape(original_shape).to(out_dev)
+        y = torch.empty(max(numel, 4), dtype=torch.float32, device=dev)
         y[:numel].copy_(base_tensor.detach().reshape(-1).to(dev, torch.float32))
         codec.topk_decode(v, ix, numel, y=y, mode=1)
-    else:
-        codec.topk_decode(v, ix, numel, y=y, mode=0)
+        out = y[:numel].reshape(original_shape)
+        return (out if bdt == torch.float32 else out.to(bdt)).to(out_dev)
+    y = torch.empty(max(numel, 4), dtype=torch.float32, device=dev)
+    codec.topk_decode(v, ix, numel, y=y, mode=0)
     return y[:numel].reshape(original_shape).to(out_dev)
 
 

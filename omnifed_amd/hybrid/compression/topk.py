@@ -28,7 +28,8 @@ def topk_sparse(tensor: torch.Tensor, compress_ratio: float):
     plan = codec.Plan.get([n], device=dev)
     x = to_arena(tensor, dev, plan)
     values, indices, _ = plan.topk_encode(x, compress_ratio)
-    return values.to(tensor.device), indices.to(tensor.device)
+    vdt = tensor.dtype if tensor.dtype in (torch.float16, torch.bfloat16) else values.dtype
+    return values.to(tensor.device, vdt), indices.to(tensor.device)
 
 
 def topk_desparse(values: torch.Tensor, indices: torch.Tensor, numel: int, device):
@@ -38,7 +39,10 @@ def topk_desparse(values: torch.Tensor, indices: torch.Tensor, numel: int, devic
     y = torch.empty(max(int(numel), 4), dtype=values.dtype if values.dtype == torch.float32 else torch.float32,
                     device=dev)
     codec.topk_decode(values.to(dev, torch.float32), indices.to(dev, torch.int64), int(numel), y=y, mode=0)
-    return y[: int(numel)].to(out_dev)
+    out = y[: int(numel)]
+    if values.dtype in (torch.float16, torch.bfloat16):  # zeros of values.dtype (exact narrowing)
+        out = out.to(values.dtype)
+    return out.to(out_dev)
 
 
 def topk_index_offset(K: int) -> int:
@@ -63,12 +67,14 @@ class TopKCompression(Compression):
     def compress_weighted(self, tensor: torch.Tensor, name: str, alpha: float):
         """``compress(fl32(alpha * tensor), name)`` with the weighting fused into the encoder (the
         client weighting param * batch_samples, global_grpc.py:101-123)."""
+        if tensor.dtype in (torch.float16, torch.bfloat16):
+            return self._compress_half(tensor, name, alpha)
         if tensor.is_floating_point() and tensor.dtype != torch.float32:
-            # The reference selects and keeps its residual in the tensor's dtype; this codec's Top-K
-            # is fp32 (integer tensors are selected on their exact fp32 values, as the wire's
-            # astype(float32) sends them; a bf16 tensor fails in the reference's wire encode anyway:
-            # numpy has no bfloat16).
-            raise ValueError(f"Top-K on the MI355X codec encodes float32 (or integer) tensors, not {tensor.dtype}")
+            # fp64: the reference would select on fp64 magnitudes and round the values to fp32 on
+            # the wire; this codec's Top-K selects in fp32 / fp16 / bf16 (integer tensors on their
+            # exact fp32 values, as the wire's astype(float32) sends them).
+            raise ValueError(f"Top-K on the MI355X codec encodes float32/float16/bfloat16 (or integer) "
+                             f"tensors, not {tensor.dtype}")
         dev = compute_device(tensor, self.device)
         numel = tensor.numel()
         shape = tensor.size()
@@ -87,6 +93,31 @@ class TopKCompression(Compression):
         self.residual.residuals[name] = res
         ctx = (numel, shape)
         return (values.to(self.device), indices.to(self.device)), ctx
+
+    def _compress_half(self, tensor: torch.Tensor, name: str, alpha: float):
+        """fp16 / bf16 tensors, in the tensor's dtype as the reference computes them: the weighting
+        (``param * batch_samples``) and ``compensate`` (``beta * residual + gamma * tensor``,
+        core.py:26-30) are the reference's own torch expressions, evaluated on the GPU; t' is then
+        widened to fp32 (exact) and the selection and the residual update (t' with the selected
+        slots zeroed: core.py:32-37's ``t' - desparse``) are the fp32 kernel's, whose magnitude
+        order on the widened values is the half-precision order.  Values come back in the tensor's
+        dtype (exact), the residual is kept in it."""
+        dev = compute_device(tensor, self.device)
+        t = tensor.detach().to(dev).reshape(-1)
+        if float(alpha) != 1.0:
+            t = torch.mul(t, float(alpha))
+        res = self.residual.residuals.get(name)
+        if res is not None:
+            if res.numel() != t.numel():
+                raise ValueError(f"residual for {name!r} has {res.numel()} elements, tensor has {t.numel()}")
+            t = self.residual.beta * res.to(dev).reshape(-1) + self.residual.gamma * t
+        numel, shape = tensor.numel(), tensor.size()
+        plan = codec.Plan.get([numel], device=dev)
+        x = to_arena(t, dev, plan)  # exact widening (or t itself when the compensate promoted to fp32)
+        r = torch.empty(numel, dtype=torch.float32, device=dev)
+        values, indices, _ = plan.topk_encode(x, self.compress_ratio, residual=r, residual_mode=2)
+        self.residual.residuals[name] = r.to(t.dtype)
+        return (values.to(self.device, t.dtype), indices.to(self.device)), (numel, shape)
 
     def _residual_arena(self, names, plan):
         """The residual arena of the dict layout (``names``, ``plan``) and the encoder's residual

@@ -194,13 +194,14 @@ def test_half_drop_in_layers(gpu, g2, g2i):
     assert same >= len(g2i["half"]) - 3, same
 
 
-def test_float64_and_half_topk_are_refused(gpu):
+def test_float64_qsgd_and_topk_are_refused(gpu):
+    """fp64 is refused by both codecs (fp16 / bf16 Top-K: tests/test_gpu_topk_half.py)."""
     comp = QSGDQuantCompression(bit_width=4)
     with pytest.raises(ValueError, match="float64"):
         encode_layer_state("d", torch.randn(100, dtype=torch.float64, device=gpu), comp)
     tk = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.1)
-    with pytest.raises(ValueError, match="float32"):
-        encode_layer_state("h", torch.randn(100, device=gpu).half(), tk)
+    with pytest.raises(ValueError, match="float64"):
+        encode_layer_state("h", torch.randn(100, device=gpu).double(), tk)
 
 
 # ---------------------------------------------------------------- client weighting on the drop-in
