@@ -278,7 +278,8 @@ class HostArenaPool:
     handed out are ordinary, writable CPU tensors (numpy-backed storage); the pool keeps at most
     ``max_bytes`` of free buffers (the rest goes back to the OS)."""
 
-    GRAIN = 64 << 20
+    GRAIN = 64 << 20      # sizes rounded up to this above it (to 1 MiB below)
+    MIN_BYTES = 1 << 20   # smaller arenas are not pooled
 
     def __init__(self, max_bytes: int = 8 << 30):
         import numpy as np
@@ -303,12 +304,15 @@ class HostArenaPool:
     def empty(self, nbytes: int) -> torch.Tensor:
         """An uninitialised uint8 CPU tensor of ``nbytes`` backed by pooled memory."""
         nbytes = int(nbytes)
+        if nbytes < self.MIN_BYTES:  # small: malloc's own free lists serve it
+            return torch.empty(nbytes, dtype=torch.uint8)
         with self._lock:
             self._drain()
-            pick = next((i for i, m in enumerate(self._free) if m.nbytes >= nbytes), None)
+            pick = next((i for i, m in enumerate(self._free) if nbytes <= m.nbytes <= 2 * nbytes + self.GRAIN), None)
             mem = self._free.pop(pick) if pick is not None else None
         if mem is None:
-            mem = self._np.empty(max(self.GRAIN, -(-nbytes // self.GRAIN) * self.GRAIN), dtype=self._np.uint8)
+            grain = self.GRAIN if nbytes >= self.GRAIN else self.MIN_BYTES
+            mem = self._np.empty(-(-nbytes // grain) * grain, dtype=self._np.uint8)
         return torch.from_numpy(self._np.asarray(_HostLease(mem, nbytes, self)))
 
     def free_bytes(self) -> int:

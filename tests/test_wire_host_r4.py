@@ -169,12 +169,14 @@ def test_shared_arena_detection():
 
 def test_host_arena_pool_reuses_pages_and_honours_its_budget():
     """Pooled pageable arenas (hostio.HostArenaPool): ordinary writable CPU tensors; the memory of a
-    dropped arena (every view gone) serves the next one; free arenas above the budget are released."""
+    dropped arena (every view gone) serves the next one of a similar size; free arenas above the
+    budget are released; small ones are not pooled."""
     import gc
 
-    P = hostio.HostArenaPool(max_bytes=200 << 20)
-    t = P.empty(4000).view(torch.float32)
-    assert t.numel() == 1000 and not t.is_pinned()
+    MiB = 1 << 20
+    P = hostio.HostArenaPool(max_bytes=200 * MiB)
+    t = P.empty(3 * MiB + 8).view(torch.float32)
+    assert t.numel() == (3 * MiB + 8) // 4 and not t.is_pinned()
     t.fill_(2.0)
     view = t[10:20]
     p = t.data_ptr()
@@ -184,14 +186,19 @@ def test_host_arena_pool_reuses_pages_and_honours_its_budget():
     assert float(view.sum()) == 20.0
     del view
     gc.collect()
-    assert P.free_bytes() == P.GRAIN
-    u = P.empty(100)
+    assert P.free_bytes() == 4 * MiB  # rounded up to 1 MiB below the 64 MiB grain
+    u = P.empty(3 * MiB)
     assert u.data_ptr() == p and P.free_bytes() == 0
-    a, b = P.empty(100 << 20), P.empty(100 << 20)  # 128 MiB each (64 MiB grain)
+    a, b = P.empty(100 * MiB), P.empty(100 * MiB)  # 128 MiB each (64 MiB grain)
     del u, a, b
     gc.collect()
-    assert P.free_bytes() == P.GRAIN + (128 << 20)  # 64 + 128 + 128 MiB freed, 200 MiB kept at most
-    assert P.empty(0).numel() == 0
+    assert P.free_bytes() == 4 * MiB + 128 * MiB  # 4 + 128 + 128 MiB freed, 200 MiB kept at most
+    big = P.empty(120 * MiB)  # the free 128 MiB arena serves it
+    assert P.free_bytes() == 4 * MiB
+    del big
+    small = P.empty(1000)
+    assert small.numel() == 1000 and P.empty(0).numel() == 0
+    gc.collect()
 
 
 def test_host_arena_pool_threads_never_share_live_memory():
@@ -207,7 +214,7 @@ def test_host_arena_pool_threads_never_share_live_memory():
     def work(seed):
         try:
             for i in range(30):
-                n = 1000 + 997 * ((seed * 31 + i) % 50)
+                n = (1 << 20) + 99991 * ((seed * 31 + i) % 50)
                 t = P.empty(n)
                 a, b = t.data_ptr(), t.data_ptr() + n
                 with lock:
