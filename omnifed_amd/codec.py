@@ -196,7 +196,14 @@ class Plan:
     @property
     def encoder_kernel(self) -> str:
         """Name of the kernel one encode launch runs (profiling / roofline bookkeeping)."""
-        # the bracketed encoder is three launches (qsgd_spec_bracket, _quant, _finish): "qsgd_spec_all"
+        return self.encoder_kernel_for(4)
+
+    def encoder_kernel_for(self, bit_width: int) -> str:
+        """The kernel an fp32, on-device-draw encode at ``bit_width`` runs: the bracketed encoder
+        (three launches: "qsgd_spec_all") serves bit widths 1-4 and hands wider payloads to the
+        two-pass encoder (omf_plan_encode_strategy)."""
+        if self.strategy == "bracket" and not 1 <= int(bit_width) <= 4:
+            return "qsgd_encode_ordered"
         return {"ring": "qsgd_encode_pc", "bracket": "qsgd_spec_all", "grid": "qsgd_encode_grid"}.get(
             self.strategy, "qsgd_encode_ordered")
 

@@ -1,5 +1,6 @@
-"""Encode / step time of one library build (OMF_CODEC_LIB_EXPERIMENT selects a variant), Llama-400M
-s = 4 bracketed encoder: HIP events around 20 calls, median of 7 rounds.  One JSON line."""
+"""Encode / step time of one library build (OMF_CODEC_LIB_EXPERIMENT selects a variant): HIP events
+around 20 calls, median of 7 rounds.  One JSON line.
+usage: enc_time.py [config=llama400m] [bits=4] [strategy=the plan's default]"""
 import json
 import os
 import sys
@@ -11,10 +12,15 @@ from omnifed_amd import codec, shapes  # noqa: E402
 
 dev = torch.device("cuda", 0)
 sizes = [shapes.numel(s) for _, s in shapes.model_shapes(sys.argv[1] if len(sys.argv) > 1 else "llama400m")]
-p = codec.Plan.get(sizes, device=dev)
+p = codec.Plan(sizes, device=dev)
+bits = int(sys.argv[2]) if len(sys.argv) > 2 else 4
+if len(sys.argv) > 3:
+    p.set_encode_strategy(sys.argv[3])
+L = 2 ** bits
+w = 8 if L <= 127 else 32
 g = torch.Generator(device=dev).manual_seed(1000)
 x = torch.randn(p.arena_end, device=dev, generator=g) * 1e-3
-q = torch.empty(p.payload_elems(8), dtype=torch.int8, device=dev)
+q = torch.empty(p.payload_elems(w), dtype=torch.int8 if w == 8 else torch.int32, device=dev)
 nr = torch.empty(p.nt, device=dev)
 y = torch.empty(p.arena_end, device=dev)
 st = torch.cuda.current_stream(dev)
@@ -33,10 +39,11 @@ def tm(fn, reps=20):
 
 enc, step = [], []
 for _ in range(7):
-    enc.append(tm(lambda i: p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=7, offset=i)))
-    step.append(tm(lambda i: (p.qsgd_encode(x, 4, q_out=q, norm_out=nr, seed=7, offset=i),
-                              p.qsgd_decode(q, 8, 16, nr, y_out=y))))
+    enc.append(tm(lambda i: p.qsgd_encode(x, bits, q_out=q, norm_out=nr, seed=7, offset=i)))
+    step.append(tm(lambda i: (p.qsgd_encode(x, bits, q_out=q, norm_out=nr, seed=7, offset=i),
+                              p.qsgd_decode(q, w, L, nr, y_out=y))))
 p.check()
-print(json.dumps({"lib": os.path.basename(os.environ.get("OMF_CODEC_LIB_EXPERIMENT", "base")),
+print(json.dumps({"lib": os.path.basename(os.environ.get("OMF_CODEC_LIB_EXPERIMENT", "base")), "bits": bits,
+                  "strategy": p.strategy,
                   "enc_ms": round(sorted(enc)[3], 4), "step_ms": round(sorted(step)[3], 4),
                   "payload_sha": __import__("hashlib").sha256(q.cpu().numpy().tobytes()).hexdigest()[:16]}), flush=True)
