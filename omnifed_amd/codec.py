@@ -200,10 +200,10 @@ class Plan:
 
     def encoder_kernel_for(self, bit_width: int) -> str:
         """The kernel an fp32, on-device-draw encode at ``bit_width`` runs: the bracketed encoder
-        (three launches: "qsgd_spec_all") serves bit widths 1-4 and hands wider payloads to the
-        two-pass encoder (omf_plan_encode_strategy)."""
+        (three launches: "qsgd_spec_all") serves bit widths 1-4, hands int32 payloads (s >= 7) to
+        the ring and s = 5, 6 to the two-pass encoder (omf_plan_encode_strategy)."""
         if self.strategy == "bracket" and not 1 <= int(bit_width) <= 4:
-            return "qsgd_encode_ordered"
+            return "qsgd_encode_pc" if storage_width(2 ** int(bit_width)) == 32 else "qsgd_encode_ordered"
         return {"ring": "qsgd_encode_pc", "bracket": "qsgd_spec_all", "grid": "qsgd_encode_grid"}.get(
             self.strategy, "qsgd_encode_ordered")
 

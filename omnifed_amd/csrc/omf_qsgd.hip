@@ -2108,8 +2108,9 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     ++p->grid_launches;
     return OMF_OK;
   }
-  // Bracketed single-read encoder: fp32 values with on-device draws (other formats and
-  // caller uniforms take the two-pass encoder).  Four launches, no host interaction.
+  // Bracketed single-read encoder: fp32 values with on-device draws at s <= 4 (int32 payloads
+  // take the ring, other formats and caller uniforms the two-pass encoder).  Three launches, no
+  // host interaction.
   if (p->strategy == 3 && !norm_only && !u && fmt == 0 && s >= kSpecMinBits && s <= kSpecMaxBits) {
     // (the fused PS step too: the pass divides, stores the average and quantises it)
     SpecArgs sa;
@@ -2165,8 +2166,13 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     OMF_HIP(hipGetLastError());
     return OMF_OK;
   }
-  // The ring also serves the fused PS step (divide + encode in one launch) under any strategy.
-  if ((p->strategy == 2 || p->strategy == 4 || divisor != 0.0f) && !norm_only) {
+  // The ring also serves the fused PS step (divide + encode in one launch) under any strategy,
+  // and the bracketed plans' int32-wire encodes (s >= 7, fp32, on-device draws): Llama-400M s = 8
+  // 0.68 ms against 0.74 for the two-pass encoder, whose second pass rewrites the 4 N payload
+  // after re-reading x (scripts/exp/s8_strategies.sh).  bf16 / fp16 values and caller uniforms
+  // stay on the two-pass encoder (0.61 / 0.78 ms against the ring's 0.70 / 0.83).
+  const bool wide_ring = p->strategy == 3 && width == 4 && !u && fmt == 0;
+  if ((p->strategy == 2 || p->strategy == 4 || divisor != 0.0f || wide_ring) && !norm_only) {
     omf::ring::Args r;
     r.x = x; r.u = u; r.q = q; r.norm_out = norm_out;
     r.items = p->d_ring; r.tinfo = p->d_ring_t; r.gran = p->d_ring_gran;
