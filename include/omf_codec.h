@@ -120,9 +120,9 @@ int omf_plan_set_debug(omf_plan* plan, uint32_t ring_dbg, uint32_t spec_dbg, int
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy);
 /* The plan's encode strategy (0-3 as above).  A new plan picks 3 (bracketed single-read) for
  * arenas of >= 2^25 elements and 2 (the ring) below: the measured crossover;
- * OMF_ENCODE_STRATEGY overrides.  Strategy 3 serves fp32 values with on-device draws at
- * bit_width 1-4; its int32-wire encodes (bit_width >= 7, fp32, on-device draws) take the ring (2),
- * its other encodes the two-pass encoder (1). */
+ * OMF_ENCODE_STRATEGY overrides.  Strategy 3 serves fp32 / bf16 / fp16 values with on-device
+ * draws at bit_width 1-4; its int32-wire encodes (bit_width >= 7, fp32, on-device draws) take the
+ * ring (2), its other encodes (caller uniforms, s = 5, 6) the two-pass encoder (1). */
 int32_t omf_plan_encode_strategy(const omf_plan* plan);
 /* Diagnostics of the last bracketed single-read encode (strategy 3; synchronises `stream`,
  * not for the hot path): out[0] tensors requantised whole (norm outside the sampled bracket,

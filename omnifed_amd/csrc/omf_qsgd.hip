@@ -475,9 +475,11 @@ __device__ __forceinline__ float4 scale_alpha(float4 v, float alpha) {
   return v;
 }
 
-// x * alpha, then / divisor for the fused PS step (divisor 0: none) — the pass's arithmetic.
-__device__ __forceinline__ float4 spec_prologue(float4 v, float alpha, float divisor) {
+// x * alpha (rounded to the value format when alpha != 1: torch.mul on a bf16 / fp16 tensor),
+// then / divisor for the fused PS step (divisor 0: none) — the pass's arithmetic.
+__device__ __forceinline__ float4 spec_prologue(float4 v, float alpha, float divisor, uint32_t fmt) {
   v = scale_alpha(v, alpha);
+  if (fmt && alpha != 1.0f) v = round_fmt4(v, fmt);
   if (divisor != 0.0f) {
     v.x = __fdiv_rn(v.x, divisor); v.y = __fdiv_rn(v.y, divisor);
     v.z = __fdiv_rn(v.z, divisor); v.w = __fdiv_rn(v.w, divisor);
@@ -540,7 +542,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     }
     float acc = 0.0f;
 #pragma unroll
-    for (int i = 0; i < PER; ++i) acc = sq4(spec_prologue(v[i], alpha, a.divisor), acc);
+    for (int i = 0; i < PER; ++i) acc = sq4(spec_prologue(v[i], alpha, a.divisor, a.e.fmt), acc);
     s1 = acc;
   } else {
     // runs of 64 elements at a hashed position inside each of R <= 512 balanced strata (of
@@ -562,7 +564,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     }
 #pragma unroll
     for (int i = 0; i < PASSES; ++i) {
-      float sr = live[i] ? sq4(spec_prologue(v[i], alpha, a.divisor), 0.0f) : 0.0f;
+      float sr = live[i] ? sq4(spec_prologue(v[i], alpha, a.divisor, a.e.fmt), 0.0f) : 0.0f;
 #pragma unroll
       for (int o = LPR / 2; o > 0; o >>= 1) sr += __shfl_xor(sr, o, LPR);  // the run's sum in every lane
       if (live[i] && j == 0) {
@@ -584,6 +586,13 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     ss = S1 * ((double)n / ((double)kSpecRun * Rd));
     k = (double)a.zsig * sqrt(var / Rd) / m + 0x1p-10;  // 6 sigma of the run-sum estimate + 0.1 %
   }
+  // bf16 / fp16 values: the norm is rounded to the format (at most half an ulp: 2^-8 / 2^-11
+  // relative, so (1 + 2^-8)^2 < 1 + 2^-7 + 2^-14 on its square), and so is x / n, whose
+  // rounding the multipliers absorb by the same relative bound (spec_quad_fmt).
+  const uint32_t fmt = a.e.fmt;
+  const double kf = fmt == kFmtBF16 ? 0x1p-7 + 0x1p-14 : (fmt == kFmtF16 ? 0x1p-10 + 0x1p-20 : 0.0);
+  const double mf = fmt == kFmtBF16 ? 0x1p-8 + 0x1p-16 : (fmt == kFmtF16 ? 0x1p-11 + 0x1p-22 : 0.0);
+  k += kf;
   SpecBracket o{0.f, 0.f, 0.f, 0.f, 1u, {0u, 0u, 0u}};  // deferred: c = 0 decides every level as 0
   if (ss > 0.0 && ss < 1e300 && k < 0.5) {
     const float n_lo = nextafterf((float)sqrt(ss * (1.0 - k)), 0.0f);
@@ -592,8 +601,8 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
       const double L = (double)a.e.levels;
       o.n_lo = n_lo;
       o.n_hi = n_hi;
-      o.c_lo = nextafterf((float)(L / (double)n_hi * (1.0 - 0x1p-20)), 0.0f);
-      o.c_hi = nextafterf((float)(L / (double)n_lo * (1.0 + 0x1p-20)), INFINITY);
+      o.c_lo = nextafterf((float)(L / (double)n_hi * (1.0 - 0x1p-20) * (1.0 - mf)), 0.0f);
+      o.c_hi = nextafterf((float)(L / (double)n_lo * (1.0 + 0x1p-20) * (1.0 + mf)), INFINITY);
       o.mode = 0u;
     }
   }
@@ -611,6 +620,26 @@ __device__ __forceinline__ void spec_quad(float4 x, float4 u, float c_lo, float 
     const float ax = fabsf(xs[c]);
     const float kl = ceilf(fmaf(ax, c_lo, -fmaxf(us[c], 0x1p-26f)));
     const float kh = ceilf(fmaf(ax, c_hi, -us[c]));
+    und |= kl != kh;
+    q[c] = (int32_t)copysignf(kh, xs[c]);
+  }
+}
+
+// The same for bf16 / fp16 values (vn = x / n rounded to the format, a = |vn| L): the bracket's
+// multipliers carry the format's relative rounding bound (qsgd_spec_bracket), and fp16's
+// subnormal quotients (|vn| < 2^-14: an absolute step of 2^-24, i.e. at most 2^-25 L on a) take
+// an absolute slack `dl` on both sides (u + dl is exact: u is a multiple of 2^-24 below 1).
+// Every level between the two bounds' is then the level for some norm of the bracket, so
+// kl == kh decides it; bf16 subnormals (|vn| < 2^-126) fall under the u == 0
+// rule as in fp32.
+__device__ __forceinline__ void spec_quad_fmt(float4 x, float4 u, float c_lo, float c_hi, float dl, int32_t (&q)[4],
+                                              bool& und) {
+  const float xs[4] = {x.x, x.y, x.z, x.w}, us[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float ax = fabsf(xs[c]);
+    const float kl = ceilf(fmaf(ax, c_lo, -(fmaxf(us[c], 0x1p-26f) + dl)));
+    const float kh = ceilf(fmaf(ax, c_hi, dl - us[c]));
     und |= kl != kh;
     q[c] = (int32_t)copysignf(kh, xs[c]);
   }
@@ -642,7 +671,7 @@ __device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t 
 // One block's pass: loads issued first, the Philox draws (independent of x) computed while
 // they are in flight, then the partial, the levels and the undecided list.  FULL: a whole
 // 4 Ki block (straight-line code, no bounds checks).
-template <int WIDTH, bool FULL, bool DIV>
+template <int WIDTH, bool FULL, bool DIV, uint32_t FMT>
 __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t end, int32_t t, int64_t tb,
                                            const SpecBracket& br, uint32_t* slot, uint64_t* part) {
   const EncArgs& e = a.e;
@@ -661,6 +690,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
   for (int k = 0; k < kSpecV; ++k) {
     v[k].x = __fmul_rn(v[k].x, alpha); v[k].y = __fmul_rn(v[k].y, alpha);
     v[k].z = __fmul_rn(v[k].z, alpha); v[k].w = __fmul_rn(v[k].w, alpha);
+    if (FMT != kFmtF32 && alpha != 1.0f) v[k] = round_fmt4(v[k], FMT);  // torch.mul on the half tensor
     if (DIV) {  // fused PS step: the average, stored once (nontemporal) and quantised from registers
       const float d = a.divisor;
       v[k].x = __fdiv_rn(v[k].x, d); v[k].y = __fdiv_rn(v[k].y, d);
@@ -685,7 +715,8 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
       const bool live = FULL || el < end;
       int32_t qq[4];
       bool und = false;
-      spec_quad(v[k], uu[k], br.c_lo, br.c_hi, qq, und);
+      if (FMT == kFmtF32) spec_quad(v[k], uu[k], br.c_lo, br.c_hi, qq, und);
+      else spec_quad_fmt(v[k], uu[k], br.c_lo, br.c_hi, FMT == kFmtF16 ? 0x1p-25f * e.levels : 0.0f, qq, und);
       if (live) store_quad<WIDTH>(e, el, FULL ? el + 4 : end, qq);
       const uint64_t m = __ballot(live && und);
       if (m) {  // rare: list this wave's undecided quads
@@ -711,7 +742,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
 
 // The per-tensor tables are __restrict__ const kernel arguments so that they are read with
 // scalar loads (a vector load there is waited for before the x loads are issued).
-template <int WIDTH, bool DIV>
+template <int WIDTH, bool DIV, uint32_t FMT = kFmtF32>
 __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
                                                             const int64_t* __restrict__ begins) {
   const int64_t blk = blockIdx.x;
@@ -730,8 +761,8 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const Sp
     return;
   }
   const int64_t end = min(b + kSpecBlk, it.end);
-  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV>(a, b, end, it.tensor, tb, br, slot, part);
-  else spec_block<WIDTH, false, DIV>(a, b, end, it.tensor, tb, br, slot, part);
+  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, FMT>(a, b, end, it.tensor, tb, br, slot, part);
+  else spec_block<WIDTH, false, DIV, FMT>(a, b, end, it.tensor, tb, br, slot, part);
 }
 
 // One fold segment (a workgroup of the finish launch); the last arriver of the tensor folds the
@@ -769,7 +800,7 @@ __device__ void spec_fold(const SpecArgs& a, const SpecFoldItem& fi) {
     tot = block_sum_f64(q, red);
   }
   if (threadIdx.x != 0) return;
-  const float norm = finish_norm(tot, kFmtF32);
+  const float norm = finish_norm(tot, a.e.fmt);
   a.e.norm_out[t] = norm;
   const SpecBracket br = a.br[t];
   const uint32_t fl = a.flags[t];
@@ -852,7 +883,7 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
       bool bad;
       if (spec_norm_wait(a, t, norm, bad)) {
         const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
-        const Divisor dv(norm);
+        const Divisor dv(norm, e.fmt);
         for (uint32_t j = 0; j < cnt; ++j) {
           const uint32_t q = slots[blk * kSpecSlot + kSpecPerWave * w + j];
           const float4* rec = recs + 2 * (ws * kSpecPerWave + j);
@@ -2108,10 +2139,11 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     ++p->grid_launches;
     return OMF_OK;
   }
-  // Bracketed single-read encoder: fp32 values with on-device draws at s <= 4 (int32 payloads
-  // take the ring, other formats and caller uniforms the two-pass encoder).  Three launches, no
-  // host interaction.
-  if (p->strategy == 3 && !norm_only && !u && fmt == 0 && s >= kSpecMinBits && s <= kSpecMaxBits) {
+  // Bracketed single-read encoder: fp32 / bf16 / fp16 values with on-device draws at s <= 4
+  // (int32 payloads take the ring, caller uniforms the two-pass encoder; the fused PS step is
+  // fp32).  Three launches, no host interaction.
+  if (p->strategy == 3 && !norm_only && !u && (fmt == 0 || divisor == 0.0f) && s >= kSpecMinBits &&
+      s <= kSpecMaxBits) {
     // (the fused PS step too: the pass divides, stores the average and quantises it)
     SpecArgs sa;
     a.items = p->d_flat;
@@ -2145,7 +2177,9 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     // the fix stores / the fix, bit 4 the fold — the payload is then not the encoder's.
     if (!(p->spec_skip & 1u)) hipLaunchKernelGGL(qsgd_spec_bracket, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
     const bool div = divisor != 0.0f;
-    if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    if (fmt == kFmtBF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtBF16>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    else if (fmt == kFmtF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF16>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    else if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
     else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
     else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
     else hipLaunchKernelGGL((qsgd_spec_quant<4, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
