@@ -433,9 +433,12 @@ def encode_updates_dict(updates: Dict[str, torch.Tensor], compressor: Optional[G
 
 
 def _topk_batchable(tensors) -> bool:
-    """The batched Top-K path takes non-empty fp32 tensors (others: the per-layer path)."""
-    return bool(tensors) and all(isinstance(t, torch.Tensor) and t.dtype == torch.float32 and t.numel() > 0
-                                 for t in tensors)
+    """The batched Top-K path takes non-empty tensors of one dtype, fp32 or fp16 (others: the
+    per-layer path — a bf16 dict there raises the reference's TypeError at its first layer)."""
+    if not tensors or not all(isinstance(t, torch.Tensor) and t.numel() > 0 for t in tensors):
+        return False
+    dts = {t.dtype for t in tensors}
+    return dts == {torch.float32} or dts == {torch.float16}
 
 
 def _encode_topk_updates(updates, compressor: TopKCompression, weight) -> list:

@@ -151,12 +151,72 @@ class TopKCompression(Compression):
             arena[plan.offsets[t]:plan.offsets[t] + plan.sizes[t]].fill_(-0.0)
         return arena, 1
 
+    def _residual_arena_half(self, names, plan, dt):
+        """``_residual_arena`` for a dict of ``dt`` (fp16 / bf16) tensors: the residuals live in a
+        ``dt`` arena (the reference keeps them in the tensor's dtype); a fresh name gets -0.0, the
+        additive identity in half precision too.  Returns (arena, any residual present)."""
+        key = (tuple(names), tuple(plan.sizes), str(plan.device), dt)
+        arena = self._arenas.get(key)
+        if arena is None:
+            if len(self._arenas) >= 4:
+                self._arenas.pop(next(iter(self._arenas)))
+            arena = torch.empty(max(plan.arena_end, 4), dtype=dt, device=plan.device)
+            self._arenas[key] = arena
+        base, isz = arena.data_ptr(), arena.element_size()
+        fresh = []
+        for t, name in enumerate(names):
+            o, n = plan.offsets[t], plan.sizes[t]
+            r = self.residual.residuals.get(name)
+            if r is None:
+                fresh.append(t)
+            elif not (r.data_ptr() == base + isz * o and r.numel() == n and r.dtype == dt and r.device == plan.device):
+                if r.numel() != n:
+                    raise ValueError(f"residual for {name!r} has {r.numel()} elements, tensor has {n}")
+                arena[o:o + n].copy_(r.reshape(-1))
+        for t in fresh:
+            arena[plan.offsets[t]:plan.offsets[t] + plan.sizes[t]].fill_(-0.0)
+        return arena, len(fresh) < len(names)
+
+    def _encode_arena_half(self, names, flats, alpha, out):
+        """``encode_arena`` for a dict of one half dtype: the weighting and ``compensate`` are the
+        reference's torch expressions in that dtype over the whole dict's arena (as _compress_half
+        per tensor), then ONE fp32 selection launch on the exactly widened t'."""
+        dt = flats[0].dtype
+        dev = compute_device(flats[0], self.device)
+        plan = codec.Plan.get([int(f.numel()) for f in flats], device=dev)
+        ks = plan.topk_ks(self.compress_ratio)
+        K = sum(ks)
+        h = torch.empty(plan.arena_end, dtype=dt, device=dev)
+        for f, o, n in zip(flats, plan.offsets, plan.sizes):
+            h[o:o + n].copy_(f.detach().reshape(-1))
+        if float(alpha) != 1.0:
+            h = torch.mul(h, float(alpha))
+        res, present = self._residual_arena_half(names, plan, dt)
+        if present:
+            h = self.residual.beta * res + self.residual.gamma * h
+        x = h.float()  # exact widening (padding is never read)
+        r = torch.empty(plan.arena_end, dtype=torch.float32, device=dev)
+        if out is None:
+            out = torch.empty(topk_index_offset(K) + 8 * K, dtype=torch.uint8, device=dev)
+        io = topk_index_offset(K)
+        values = out[:4 * K].view(torch.float32)
+        indices = out[io:io + 8 * K].view(torch.int64)
+        plan.topk_encode(x, self.compress_ratio, residual=r, residual_mode=2, values=values, indices=indices)
+        res[:plan.arena_end].copy_(r)  # exact narrowing (t' and zeros are dt values)
+        for t, name in enumerate(names):
+            o, n = plan.offsets[t], plan.sizes[t]
+            self.residual.residuals[name] = res[o:o + n]
+        return plan, values, indices, ks
+
     def encode_arena(self, names, flats, alpha: float = 1.0, out: "torch.Tensor" = None):
         """``compress_weighted(flat, name, alpha)`` for every (name, flat) in ONE encode call
         (flats: non-empty fp32 tensors; the residuals become views of one arena).  Returns
         ``(plan, values, indices, ks)``: tensor t's selection at ``[sum(ks[:t]), + ks[t])``.
         ``out`` (optional uint8 device buffer): values are written at its start and indices at
-        byte ``topk_index_offset(K)``, so one device-to-host copy fetches both."""
+        byte ``topk_index_offset(K)``, so one device-to-host copy fetches both.  A dict of one
+        half dtype (fp16 / bf16) keeps its residuals in that dtype (``_encode_arena_half``)."""
+        if flats[0].dtype in (torch.float16, torch.bfloat16):
+            return self._encode_arena_half(names, flats, alpha, out)
         dev = compute_device(flats[0], self.device)
         plan = codec.Plan.get([int(f.numel()) for f in flats], device=dev)
         ks = plan.topk_ks(self.compress_ratio)

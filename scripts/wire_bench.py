@@ -93,6 +93,15 @@ progress("per-layer Top-K loop, copy threads, device-side steps")
 tper = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
 res["topk_1pct"]["per_layer_encode_ms"] = tm(lambda: [encode_layer_state(n, t, tper) for n, t in upd.items()],
                                              reps=3, warm=1)
+# an fp16 model's update (the reference's default scheme on a half-precision model): one batched
+# selection launch over the dict, residuals in fp16 (round 4), against the per-layer loop
+upd16 = {n: t.half() for n, t in upd.items()}
+t16 = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+res["topk_1pct"]["fp16_encode_updates_dict_ms"] = tm(lambda: encode_updates_dict(upd16, t16), reps=5, warm=2)
+t16p = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+res["topk_1pct"]["fp16_per_layer_encode_ms"] = tm(lambda: [encode_layer_state(n, t, t16p) for n, t in upd16.items()],
+                                                  reps=3, warm=1)
+del upd16, t16, t16p
 # the host copies on the calling thread vs worker threads (hostio.set_workers), same process
 res["by_copy_threads"] = {}
 for nthr in (0, 2, 4, 8):

@@ -107,3 +107,35 @@ def test_topk_decode_onto_half_base_keeps_its_dtype(gpu):
     t_dev = tgt.to(gpu)
     decode_updates_into([L], {"w": t_dev})
     assert torch.equal(t_dev.cpu(), torch.from_numpy(flat.reshape(10, 100)))
+
+
+def test_topk_fp16_dict_batched_equals_per_layer(gpu):
+    """encode_updates_dict of an fp16 dict is ONE selection launch (the weighting and compensate as
+    the reference's fp16 expressions over the dict's arena, residuals kept in fp16 views of one
+    arena): byte-identical LayerStates and bit-identical residuals to the per-layer path over 3
+    weighted error-feedback calls, with a name missing from one call and a residual replaced by
+    the caller; a bf16 dict raises the reference's TypeError."""
+    from omnifed_amd.hybrid.communicator.global_grpc_compression import _topk_batchable
+
+    g = torch.Generator(device=gpu).manual_seed(21)
+    shapes = {"a": (64, 33), "b": (4099,), "c": (1,), "d": (300, 301), "e": (1 << 18,)}
+    a = TopKCompression(device=gpu, compress_ratio=0.02)
+    b = TopKCompression(device=gpu, compress_ratio=0.02)
+    for call in range(3):
+        upd = {n: (torch.randn(*s, device=gpu, generator=g) * 1e-2).half() for n, s in shapes.items()}
+        if call == 1:
+            upd.pop("c")
+        if call == 2:
+            a.residual.residuals["a"] = b.residual.residuals["a"].clone()
+        assert _topk_batchable(list(upd.values()))
+        w = 3.0 if call != 1 else None
+        got = encode_updates_dict(upd, a, weight=w)
+        want = [encode_layer_state(n, t, b, weight=w) for n, t in upd.items()]
+        for L, P in zip(got, want):
+            assert L.SerializeToString() == P.SerializeToString(), (call, L.layer_name)
+        for n in upd:
+            ra, rb = a.residual.residuals[n], b.residual.residuals[n]
+            assert ra.dtype == torch.float16 and np.array_equal(_bits(ra.reshape(-1)), _bits(rb.reshape(-1))), (call, n)
+    with pytest.raises(TypeError, match="BFloat16"):
+        encode_updates_dict({n: torch.randn(*s, device=gpu).bfloat16() for n, s in shapes.items()},
+                            TopKCompression(device=gpu, compress_ratio=0.02))
