@@ -64,9 +64,17 @@ class TopKCompression(Compression):
         """topk.py:33-42: ``((values, indices), (numel, shape))``; mutates the residual of ``name``."""
         return self.compress_weighted(tensor, name, 1.0)
 
+    def _unit_residual_weights(self) -> None:
+        """The error-feedback kernels compute t' = residual + x: ResidualUpdates' beta = gamma = 1,
+        the only values the reference's TopKCompression constructs (topk.py:29)."""
+        if self.residual.beta != 1.0 or self.residual.gamma != 1.0:
+            raise ValueError(f"Top-K error feedback runs with beta = gamma = 1 (got beta={self.residual.beta}, "
+                             f"gamma={self.residual.gamma})")
+
     def compress_weighted(self, tensor: torch.Tensor, name: str, alpha: float):
         """``compress(fl32(alpha * tensor), name)`` with the weighting fused into the encoder (the
         client weighting param * batch_samples, global_grpc.py:101-123)."""
+        self._unit_residual_weights()
         if tensor.dtype in (torch.float16, torch.bfloat16):
             return self._compress_half(tensor, name, alpha)
         if tensor.is_floating_point() and tensor.dtype != torch.float32:
@@ -215,6 +223,7 @@ class TopKCompression(Compression):
         ``out`` (optional uint8 device buffer): values are written at its start and indices at
         byte ``topk_index_offset(K)``, so one device-to-host copy fetches both.  A dict of one
         half dtype (fp16 / bf16) keeps its residuals in that dtype (``_encode_arena_half``)."""
+        self._unit_residual_weights()
         if flats[0].dtype in (torch.float16, torch.bfloat16):
             return self._encode_arena_half(names, flats, alpha, out)
         dev = compute_device(flats[0], self.device)
