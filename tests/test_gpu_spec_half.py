@@ -76,3 +76,30 @@ def test_bracketed_half_equals_two_pass_given_its_norms(gpu):
         other.check()
         for o, n in zip(plan.offsets, SIZES):
             assert torch.equal(q[o:o + n], q2[o:o + n]), (fmt, o, n)
+
+
+def test_bracketed_half_requantise_whole_path(gpu):
+    """A norm outside its bracket sends the tensor to the exact whole-tensor requantisation (the
+    finish workgroups, quant_sub with the format's rounding): brackets left from an arena 100x
+    smaller (the bracket launch skipped: test hook spec bit 0) put every sampled tensor there.
+    Payload equal to the oracle's given the GPU norms."""
+    plan = codec.Plan(SIZES, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(31)
+    x0 = (torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-4).bfloat16().float()
+    plan.qsgd_encode(x0, 4, seed=1, offset=1, value_format=1)
+    plan.check()
+    x = (torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-2).bfloat16().float()
+    try:
+        plan.set_debug(spec=1)  # keep x0's brackets
+        q, norms = plan.qsgd_encode(x, 4, alpha=3.0, seed=2, offset=5, value_format=1)
+        stats = plan.spec_stats()
+        plan.check()
+    finally:
+        plan.set_debug()
+    assert stats["whole"] >= len(SIZES) - 1, stats
+    qh, nh, xh = q.cpu().numpy(), norms.cpu().numpy(), x.cpu()
+    for t, (o, n) in enumerate(zip(plan.offsets, SIZES)):
+        v = torch.mul(xh[o:o + n].bfloat16(), 3.0)
+        u = torch.from_numpy(oracle.philox_uniforms(2, 5, t, n))
+        want, _, _, _ = oracle.qsgd_quantize(v, 4, norm=float(nh[t]), u=u)
+        assert qh[o:o + n].tobytes() == want.numpy().tobytes(), t
