@@ -62,7 +62,7 @@ extern "C" {
 typedef struct omf_plan omf_plan;
 
 /* ABI version (major*100 + minor). */
-#define OMF_ABI_VERSION 106
+#define OMF_ABI_VERSION 107
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -219,6 +219,13 @@ int omf_ps_apply_encode(omf_plan* plan, const float* acc, float divisor, float* 
  */
 int omf_qsgd_decode(omf_plan* plan, const void* q, int32_t width, int32_t levels, const float* norm,
                     float* y_out, int32_t accumulate, void* stream);
+/* omf_qsgd_decode over the arena's 4096-element decode blocks that overlap [elem_begin,
+ * elem_end) only (every element of those blocks is written, so the payload of those whole blocks
+ * must be in place).  Lets a caller decode an arena chunk by chunk as its payload arrives and
+ * copy each decoded chunk out while the next is staged (the CPU placement of
+ * decode_updates_dict, global_grpc_compression.py:214-223).  Same results as one full decode. */
+int omf_qsgd_decode_range(omf_plan* plan, const void* q, int32_t width, int32_t levels, const float* norm,
+                          float* y_out, int32_t accumulate, int64_t elem_begin, int64_t elem_end, void* stream);
 
 /*
  * y_i = fl32(y_i / divisor) over n elements (PS averaging,

@@ -54,6 +54,7 @@ SIGNATURES = {
     "omf_ps_apply_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p,
                                            _c_p]),
     "omf_qsgd_decode": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
+    "omf_qsgd_decode_range": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_i64, _c_i64, _c_p]),
     "omf_div_f32": (ctypes.c_int, [_c_p, _c_i64, _c_f32, _c_p]),
     "omf_qsgd_packed_bits": (_c_i32, [_c_i32]),
     "omf_qsgd_pack": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p]),
@@ -80,7 +81,7 @@ class CodecError(RuntimeError):
     pass
 
 
-ABI_VERSION = 106  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+ABI_VERSION = 107  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
 
 
 def lib() -> ctypes.CDLL:

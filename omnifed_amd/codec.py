@@ -79,6 +79,9 @@ def _need(t: torch.Tensor, name: str, dtype, device, numel: int, align: int):
 STRATEGIES = ("resident", "ordered", "ring", "bracket", "grid")
 
 
+DECODE_BLOCK = 4096  # elements per decode block (omf_qsgd_decode_range granularity)
+
+
 class Plan:
     """An ``omf_plan`` over fixed tensor sizes/offsets on one device (cached, reusable)."""
 
@@ -326,7 +329,9 @@ class Plan:
 
     def qsgd_decode(self, q: torch.Tensor, width: int, levels: int, norm: torch.Tensor,
                     y_out: Optional[torch.Tensor] = None, accumulate: bool = False,
-                    stream: Optional[int] = None) -> torch.Tensor:
+                    stream: Optional[int] = None, elems: Optional[Tuple[int, int]] = None) -> torch.Tensor:
+        """omf_qsgd_decode; ``elems=(begin, end)``: omf_qsgd_decode_range (only the decode blocks
+        of ``DECODE_BLOCK`` elements overlapping that arena range are decoded)."""
         width, levels = int(width), int(levels)
         if width not in (8, 32):
             raise ValueError(f"unsupported width={width}")
@@ -342,6 +347,11 @@ class Plan:
             y_out = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
         _need(y_out, "y_out", torch.float32, dev, self.arena_end, 16)
         st = stream if stream is not None else _stream(dev)
+        if elems is not None:
+            check(lib().omf_qsgd_decode_range(self._h, _ptr(q), width, levels, _ptr(norm), _ptr(y_out),
+                                              1 if accumulate else 0, int(elems[0]), int(elems[1]),
+                                              ctypes.c_void_p(st)), "omf_qsgd_decode_range")
+            return y_out
         check(lib().omf_qsgd_decode(self._h, _ptr(q), width, levels, _ptr(norm), _ptr(y_out),
                                     1 if accumulate else 0, ctypes.c_void_p(st)), "omf_qsgd_decode")
         return y_out

@@ -1240,8 +1240,9 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_arena(DecArgs a, const u
                                                               const float* __restrict__ norms,
                                                               const int64_t* __restrict__ begins,
                                                               const int64_t* __restrict__ sizes, int32_t nt,
-                                                              int64_t qlast) {
-  const int64_t base = (int64_t)blockIdx.x * kDecBlk;
+                                                              int64_t qlast, uint32_t blk0) {
+  const uint32_t bid = blk0 + blockIdx.x;  // a range launch starts at block blk0
+  const int64_t base = (int64_t)bid * kDecBlk;
   int32_t raw[kDecV][WIDTH == 1 ? 1 : 4];
 #pragma unroll
   for (int k = 0; k < kDecV; ++k) {  // unconditional (clamped) nontemporal loads
@@ -1253,7 +1254,7 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_arena(DecArgs a, const u
       raw[k][0] = t[0]; raw[k][1] = t[1]; raw[k][2] = t[2]; raw[k][3] = t[3];
     }
   }
-  const uint32_t info = binfo[blockIdx.x];
+  const uint32_t info = binfo[bid];
   const int32_t t0 = (int32_t)(info & 0x7fffffffu);
   if (info >> 31) {  // the whole block lies inside tensor t0
     const float norm = norms[t0];
@@ -2308,8 +2309,8 @@ int omf_qsgd_norms(omf_plan* plan, const float* x, float alpha, float* norm_out,
   return encode_impl(plan, x, alpha, 0, nullptr, 0, 0, nullptr, nullptr, norm_out, true, stream);
 }
 
-int omf_qsgd_decode(omf_plan* p, const void* q, int32_t width, int32_t levels, const float* norm, float* y,
-                    int32_t accumulate, void* stream) {
+static int decode_blocks(omf_plan* p, const void* q, int32_t width, int32_t levels, const float* norm, float* y,
+                         int32_t accumulate, int64_t b0, int64_t b1, void* stream) {
   if (!p) return fail(OMF_EINVAL, "plan is NULL");
   if (width != 8 && width != 32) return fail(OMF_EINVAL, "width must be 8 or 32");
   if (levels <= 0) return fail(OMF_EINVAL, "levels must be > 0");
@@ -2323,7 +2324,10 @@ int omf_qsgd_decode(omf_plan* p, const void* q, int32_t width, int32_t levels, c
   a.levels = (float)levels;
   const bool pow2 = (levels & (levels - 1)) == 0;
   a.inv_levels = pow2 ? 1.0f / (float)levels : 0.0f;  // exact for a power of two
-  const dim3 grid((unsigned)p->n_dec_blocks), blk(kThreads);
+  b0 = std::max<int64_t>(b0, 0);
+  b1 = std::min<int64_t>(b1, p->n_dec_blocks);
+  if (b1 <= b0) return OMF_OK;
+  const dim3 grid((unsigned)(b1 - b0)), blk(kThreads);
   hipStream_t st = (hipStream_t)stream;
   // the last whole quad of the payload the caller holds (width 8: round_up(arena_end, 4) bytes
   // are not promised, so a clamped load never passes the last full quad)
@@ -2332,7 +2336,7 @@ int omf_qsgd_decode(omf_plan* p, const void* q, int32_t width, int32_t levels, c
   do {                                                                                                           \
     if (qlast >= 0)                                                                                              \
       hipLaunchKernelGGL((qsgd_decode_arena<W, A, P>), grid, blk, 0, st, a, (const uint32_t*)p->d_dec_binfo,     \
-                         norm, (const int64_t*)p->d_begins, (const int64_t*)p->d_sizes, p->nt, qlast);           \
+                         norm, (const int64_t*)p->d_begins, (const int64_t*)p->d_sizes, p->nt, qlast, (uint32_t)b0);           \
     else /* a payload of < 4 elements: the item decoder's byte loads */                                          \
       hipLaunchKernelGGL((qsgd_decode_flat<W, A, P>), dim3((unsigned)p->n_flat), blk, 0, st, a);                \
   } while (0)
@@ -2346,6 +2350,22 @@ int omf_qsgd_decode(omf_plan* p, const void* q, int32_t width, int32_t levels, c
 #undef OMF_DEC
   OMF_HIP(hipGetLastError());
   return OMF_OK;
+}
+
+int omf_qsgd_decode(omf_plan* p, const void* q, int32_t width, int32_t levels, const float* norm, float* y,
+                    int32_t accumulate, void* stream) {
+  if (!p) return fail(OMF_EINVAL, "plan is NULL");
+  return decode_blocks(p, q, width, levels, norm, y, accumulate, 0, p->n_dec_blocks, stream);
+}
+
+int omf_qsgd_decode_range(omf_plan* p, const void* q, int32_t width, int32_t levels, const float* norm, float* y,
+                          int32_t accumulate, int64_t elem_begin, int64_t elem_end, void* stream) {
+  if (!p) return fail(OMF_EINVAL, "plan is NULL");
+  if (elem_begin < 0 || elem_end < elem_begin) return fail(OMF_EINVAL, "omf_qsgd_decode_range: bad element range");
+  if (p->arena_end < 4)  // the item decoder of tiny payloads has no block ranges: decode it all
+    return decode_blocks(p, q, width, levels, norm, y, accumulate, 0, p->n_dec_blocks, stream);
+  return decode_blocks(p, q, width, levels, norm, y, accumulate, elem_begin / kDecBlk,
+                       (elem_end + kDecBlk - 1) / kDecBlk, stream);
 }
 
 int omf_div_f32(float* y, int64_t n, float divisor, void* stream) {

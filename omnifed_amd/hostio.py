@@ -251,6 +251,10 @@ def device_to_bytes(src: torch.Tensor, spans: Sequence[Tuple[int, int]], stream=
             events[-1].synchronize() if events else None  # an abandoned generator: the copies land first
 
 
+def _nbytes(m) -> int:
+    return m.numel() * m.element_size() if isinstance(m, torch.Tensor) else m.nbytes
+
+
 class _HostLease:
     """The owner of one hand-out of a pooled host buffer: numpy arrays made from it (through
     ``__array_interface__``) keep it as their base, torch tensors made from those keep the arrays,
@@ -261,8 +265,8 @@ class _HostLease:
     def __init__(self, mem, nbytes: int, pool: "HostArenaPool"):
         self.mem = mem
         self.pool = pool
-        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (mem.ctypes.data, False),
-                                    "version": 3}
+        ptr = mem.data_ptr() if isinstance(mem, torch.Tensor) else mem.ctypes.data
+        self.__array_interface__ = {"shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 3}
 
     def __del__(self):
         self.pool._returned.append(self.mem)  # list.append is atomic: no lock in a finaliser
@@ -281,11 +285,12 @@ class HostArenaPool:
     GRAIN = 64 << 20      # sizes rounded up to this above it (to 1 MiB below)
     MIN_BYTES = 1 << 20   # smaller arenas are not pooled
 
-    def __init__(self, max_bytes: int = 8 << 30):
+    def __init__(self, max_bytes: int = 8 << 30, pinned: bool = False):
         import numpy as np
 
         self._np = np
         self.max_bytes = int(max_bytes)
+        self.pinned = bool(pinned)
         self._free: List[object] = []
         self._returned: List[object] = []
         self._lock = threading.Lock()
@@ -293,12 +298,12 @@ class HostArenaPool:
     def _drain(self) -> None:
         while self._returned:
             self._free.append(self._returned.pop())
-        self._free.sort(key=lambda m: m.nbytes)
+        self._free.sort(key=_nbytes)
         kept, total = [], 0
         for m in self._free:  # the smallest first: drop what exceeds the budget
-            if total + m.nbytes <= self.max_bytes:
+            if total + _nbytes(m) <= self.max_bytes:
                 kept.append(m)
-                total += m.nbytes
+                total += _nbytes(m)
         self._free = kept
 
     def empty(self, nbytes: int) -> torch.Tensor:
@@ -308,66 +313,128 @@ class HostArenaPool:
             return torch.empty(nbytes, dtype=torch.uint8)
         with self._lock:
             self._drain()
-            pick = next((i for i, m in enumerate(self._free) if nbytes <= m.nbytes <= 2 * nbytes + self.GRAIN), None)
+            pick = next((i for i, m in enumerate(self._free) if nbytes <= _nbytes(m) <= 2 * nbytes + self.GRAIN), None)
             mem = self._free.pop(pick) if pick is not None else None
         if mem is None:
             grain = self.GRAIN if nbytes >= self.GRAIN else self.MIN_BYTES
-            mem = self._np.empty(-(-nbytes // grain) * grain, dtype=self._np.uint8)
+            size = -(-nbytes // grain) * grain
+            mem = (torch.empty(size, dtype=torch.uint8, pin_memory=True) if self.pinned
+                   else self._np.empty(size, dtype=self._np.uint8))
         return torch.from_numpy(self._np.asarray(_HostLease(mem, nbytes, self)))
 
     def free_bytes(self) -> int:
         with self._lock:
             self._drain()
-            return sum(m.nbytes for m in self._free)
+            return sum(_nbytes(m) for m in self._free)
 
 
 HOST_ARENAS = HostArenaPool()
+PINNED_ARENAS = HostArenaPool(pinned=True)  # page-locked: the DMA lands in them directly
 RING_CHUNK_BYTES = 8 << 20
+
+
+class D2HRing:
+    """Device-to-host copies into a host destination (``dst_ptr``) through a ring of ``slots``
+    pinned chunks of ``limit`` bytes, fed by a thread of its own: ``submit(src, dst_off, after)``
+    returns at once; the feeder makes ``stream`` wait for the event ``after`` (work queued on
+    another stream), queues each chunk's DMA on ``stream`` once its slot is free and hands the
+    landed chunk to a worker thread's memmove.  So a caller can keep queueing host-to-device work
+    on its own stream while earlier results flow out (PCIe is full duplex).  ``close()`` (or the
+    context's exit) returns when every byte has landed; a failure in the feeder is raised there."""
+
+    def __init__(self, dst_ptr: int, stream, key: str = "d2h", limit: int = RING_CHUNK_BYTES,
+                 slots: Optional[int] = None):
+        import queue
+
+        self.dst, self.stream, self.limit = int(dst_ptr), stream, int(limit)
+        self.n_slots = slots or max(4, 2 * workers())
+        self._cm = STAGING.lease(key, self.n_slots * self.limit)
+        self._lease = self._cm.__enter__()
+        self._base = self._lease.buf.data_ptr()
+        self._busy: List[Optional[object]] = [None] * self.n_slots
+        self._g = 0
+        self._q = queue.Queue()
+        self._err: Optional[BaseException] = None
+        self._t = threading.Thread(target=self._feed, name="omf-d2h", daemon=True)
+        self._t.start()
+
+    @staticmethod
+    def _land(ev, d, s, n):
+        ev.synchronize()
+        ctypes.memmove(d, s, n)
+
+    def _feed(self) -> None:
+        ex = pool()
+        while True:
+            req = self._q.get()
+            if req is None:
+                break
+            if self._err is not None:
+                continue
+            src, off, after = req
+            try:
+                with torch.cuda.device(self.stream.device), torch.cuda.stream(self.stream):
+                    if after is not None:
+                        self.stream.wait_event(after)
+                    total = src.numel()
+                    for a in range(0, total, self.limit):
+                        b = min(a + self.limit, total)
+                        s = self._g % self.n_slots
+                        self._g += 1
+                        if self._busy[s] is not None:
+                            self._busy[s].result()  # the slot's previous chunk is out
+                        self._lease.buf[s * self.limit:s * self.limit + (b - a)].copy_(src[a:b], non_blocking=True)
+                        ev = torch.cuda.Event()
+                        ev.record(self.stream)
+                        self._busy[s] = ex.submit(self._land, ev, self.dst + off + a, self._base + s * self.limit, b - a)
+            except BaseException as e:  # reported by close()
+                self._err = e
+
+    def submit(self, src: torch.Tensor, dst_off: int, after=None) -> None:
+        """Copy the bytes of the device tensor ``src`` (a uint8 view) to ``dst_ptr + dst_off``
+        once the event ``after`` (if any) has completed."""
+        self._q.put((src, int(dst_off), after))
+
+    def close(self) -> None:
+        self._q.put(None)
+        self._t.join()
+        try:
+            for f in self._busy:
+                if f is not None:
+                    f.result()
+        finally:
+            self._cm.__exit__(None, None, None)
+        if self._err is not None:
+            raise self._err
+
+    def __enter__(self) -> "D2HRing":
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.close()
 
 
 def device_to_host(src: torch.Tensor, stream=None, key: str = "d2h", limit: int = RING_CHUNK_BYTES,
                    slots: Optional[int] = None, pool_memory: bool = True) -> torch.Tensor:
-    """A pageable CPU copy of the device tensor ``src`` (1-D, same dtype), through a ring of
-    ``slots`` pinned chunks of ``limit`` bytes: chunk g's DMA is queued on ``stream`` (default: the
-    current stream of ``src``'s device, behind the work already there) once the worker draining
-    slot g mod ``slots`` is done, and a worker copies it out when its event has completed.  The
-    destination comes from ``HOST_ARENAS`` (``pool_memory``) or a plain ``torch.empty``.  Returns
-    when every byte has landed."""
+    """A CPU copy of the device tensor ``src`` (1-D, same dtype), queued on ``stream`` (default the
+    current stream of ``src``'s device) behind the work already there: with ``pool_memory`` into
+    a pooled page-locked arena (``PINNED_ARENAS``: one DMA at the link's rate, the pages reused
+    round after round), else into a fresh pageable tensor through a ``D2HRing`` (``slots`` pinned
+    chunks of ``limit`` bytes).  Returns when every byte has landed."""
     if stream is None:
         stream = torch.cuda.current_stream(src.device)
     raw = src.reshape(-1).view(torch.uint8)
-    out = (HOST_ARENAS.empty(raw.numel()) if pool_memory else torch.empty(raw.numel(), dtype=torch.uint8)).view(
-        src.dtype)
-    total = raw.numel()
-    if total == 0:
+    if pool_memory and raw.numel() >= HostArenaPool.MIN_BYTES:  # pooled page-locked arena: one DMA
+        out = PINNED_ARENAS.empty(raw.numel())
+        with torch.cuda.stream(stream):
+            out.copy_(raw, non_blocking=True)
+        stream.synchronize()
+        return out.view(src.dtype)
+    out = torch.empty(raw.numel(), dtype=torch.uint8).view(src.dtype)
+    if raw.numel() == 0:
         return out
-    n_slots = slots or max(4, 2 * workers())
-    ex = pool()
-    dst = out.data_ptr()
-
-    def land(ev, d, s, n):
-        ev.synchronize()
-        ctypes.memmove(d, s, n)
-
-    with STAGING.lease(key, n_slots * limit) as h:
-        ring = h.buf
-        base = ring.data_ptr()
-        busy: List[Optional[object]] = [None] * n_slots
-        try:
-            with torch.cuda.stream(stream):
-                for g, a in enumerate(range(0, total, limit)):
-                    b = min(a + limit, total)
-                    s = g % n_slots
-                    if busy[s] is not None:
-                        busy[s].result()  # the slot's previous chunk is out
-                    ring[s * limit:s * limit + (b - a)].copy_(raw[a:b], non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record(stream)
-                    busy[s] = ex.submit(land, ev, dst + a, base + s * limit, b - a)
-        finally:
-            for f in busy:
-                if f is not None:
-                    f.result()
+    with D2HRing(out.data_ptr(), stream, key, limit, slots) as ring:
+        ring.submit(raw, 0)
     return out
 
 
@@ -427,9 +494,11 @@ def stage_payloads(items: Sequence[Tuple[int, Callable[[], bytes]]], base: int, 
 
 def bytes_to_device(items: Sequence[Tuple[int, Callable[[], bytes]]], dst: torch.Tensor, total_bytes: int,
                     stream=None, key: str = "decode", limit: int = CHUNK_BYTES,
-                    check: Optional[Callable[[int, bytes], None]] = None) -> None:
+                    check: Optional[Callable[[int, bytes], None]] = None,
+                    after_flush: Optional[Callable[[int, int], None]] = None) -> None:
     """``stage_payloads`` into pinned staging (a lease), each chunk's host-to-device copy into the
-    device buffer ``dst`` queued on ``stream`` as soon as the chunk is complete.  Returns once the
+    device buffer ``dst`` queued on ``stream`` as soon as the chunk is complete, then
+    ``after_flush(a, b)`` (optional) with the chunk's byte range.  Returns once the
     last copy is queued (the staging goes back to its pool with an event the next holder waits for)."""
     if stream is None:
         stream = torch.cuda.current_stream(dst.device)
@@ -440,6 +509,8 @@ def bytes_to_device(items: Sequence[Tuple[int, Callable[[], bytes]]], dst: torch
         def flush(a: int, b: int) -> None:
             with torch.cuda.stream(stream):
                 raw[a:b].copy_(staged[a:b], non_blocking=True)
+            if after_flush is not None:  # e.g. decode what has arrived (queued behind this copy)
+                after_flush(a, b)
 
         try:
             stage_payloads(items, staged.data_ptr(), total_bytes, flush, limit, check)

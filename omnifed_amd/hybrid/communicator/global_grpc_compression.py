@@ -537,14 +537,17 @@ def _encode_updates(updates, compressor, weight) -> list:
     return layers
 
 
-def _decode_qsgd_batch(layers, dev: torch.device):
+def _decode_qsgd_batch(layers, dev: torch.device, host: bool = False):
     """Decode QSGD layers that share (width, level) in ONE launch.
 
     The payloads are staged in a plan's arena layout through pinned memory, chunk by chunk
     (hostio.bytes_to_device: each chunk's host-to-device copy overlaps the reading of the next
     chunk's payloads), and decoded by one ``omf_qsgd_decode``; returns the decoded fp32 arena
-    and the plan (layer i at ``[plan.offsets[i], + plan.sizes[i])``).
+    and the plan (layer i at ``[plan.offsets[i], + plan.sizes[i])``).  ``host``: the arena is
+    returned on the CPU (``_decode_qsgd_to_host``).
     """
+    if host and layers[0].compression_type != QSGD_PACKED_COMPRESSION_NAME:
+        return _decode_qsgd_to_host(layers, dev)
     width, level = layers[0].width, layers[0].level
     sizes = [max(int(np.prod(tuple(L.original_shape))), 1) for L in layers]
     plan = codec.Plan.get(sizes, device=dev)
@@ -565,6 +568,62 @@ def _decode_qsgd_batch(layers, dev: torch.device):
         hostio.bytes_to_device(items, qd, isz * plan.arena_end, check=lambda i, p: _check_qsgd_payload(layers[i], p))
         y = plan.qsgd_decode(qd, width, level, nd)
     return y, plan  # stream-ordered (the staging's lease carries the event its copies complete by)
+
+
+def _decode_qsgd_to_host(layers, dev: torch.device):
+    """The CPU placement of a QSGD batch, pipelined: as each staged chunk's payload is queued
+    host-to-device, the decode blocks it completes are decoded (omf_qsgd_decode_range) and an
+    event recorded, and a second stream copies those decoded elements into the host arena while
+    the next chunk is read out of its messages — the payload in and the fp32 out overlap on the
+    full-duplex link.  Same bytes as
+    one decode followed by one copy.  Under the host-memory policy the arena is a pooled
+    page-locked one (hostio.PINNED_ARENAS: each chunk is one DMA); otherwise a fresh pageable
+    tensor fed through a hostio.D2HRing."""
+    width, level = layers[0].width, layers[0].level
+    sizes = [max(int(np.prod(tuple(L.original_shape))), 1) for L in layers]
+    plan = codec.Plan.get(sizes, device=dev)
+    norms = np.zeros(plan.nt, dtype=np.float32)
+    for i, L in enumerate(layers):
+        norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
+    st = torch.cuda.current_stream(dev)
+    nd = torch.from_numpy(norms).to(dev)
+    isz = width // 8
+    N = plan.arena_end
+    qd = torch.empty(N, dtype=_QSGD_TORCH_DTYPES[width], device=dev)
+    y = torch.empty(N, dtype=torch.float32, device=dev)
+    yb = y.view(torch.uint8)
+    pinned = bool(_HOST_POLICY)
+    ob = hostio.PINNED_ARENAS.empty(4 * N) if pinned else torch.empty(4 * N, dtype=torch.uint8)
+    out = ob.view(torch.float32)
+    blk = codec.DECODE_BLOCK
+    side = torch.cuda.Stream(dev)
+    done = [0]
+    ring = None if pinned else hostio.D2HRing(out.data_ptr(), side, key="d2h_qsgd")
+    try:
+        def emit(upto: int) -> None:
+            if upto <= done[0]:
+                return
+            plan.qsgd_decode(qd, width, level, nd, y_out=y, elems=(done[0], upto), stream=st.cuda_stream)
+            ev = torch.cuda.Event()
+            ev.record(st)
+            a, b = 4 * done[0], 4 * upto
+            if pinned:  # the decoded chunk's DMA into the page-locked arena, on the side stream
+                with torch.cuda.stream(side):
+                    side.wait_event(ev)
+                    ob[a:b].copy_(yb[a:b], non_blocking=True)
+            else:
+                ring.submit(yb[a:b], a, after=ev)
+            done[0] = upto
+
+        items = [(o * isz, (lambda L=L: L.values_data)) for L, o in zip(layers, plan.offsets)]
+        hostio.bytes_to_device(items, qd, isz * N, stream=st, check=lambda i, p: _check_qsgd_payload(layers[i], p),
+                               after_flush=lambda a, b: emit((b // isz) // blk * blk))
+        emit(N)
+    finally:
+        if ring is not None:
+            ring.close()
+        side.synchronize()
+    return out, plan
 
 
 def read_topk_layer(layer):
@@ -688,9 +747,9 @@ def decode_updates_dict(proto_layers, *, base_updates: Optional[Dict[str, torch.
     if groups:
         dev = _gpu_for(out_dev)
         for layers in groups.values():
-            y, plan = _decode_qsgd_batch(layers, dev)
-            if out_dev.type == "cpu":
-                y = hostio.device_to_host(y, pool_memory=_HOST_POLICY)  # one chunked D2H; tensors are views
+            y, plan = _decode_qsgd_batch(layers, dev, host=out_dev.type == "cpu")
+            if out_dev.type == "cpu" and y.is_cuda:  # the packed wire: one chunked D2H
+                y = hostio.device_to_host(y, pool_memory=_HOST_POLICY)
             for L, o, n in zip(layers, plan.offsets, plan.sizes):
                 decoded[L.layer_name] = y[o:o + n].view(tuple(L.original_shape))
     if base_updates is not None:  # overlays decode layer by layer, on their bases' devices

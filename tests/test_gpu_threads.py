@@ -11,11 +11,13 @@ the Top-K encoder's per-thread verdict word (omf_topk.hip), and the pinned stagi
 import threading
 from concurrent.futures import ThreadPoolExecutor
 
+import numpy as np
 import pytest
 import torch
 
 from omnifed_amd.hybrid.communicator.global_grpc_compression import (
     build_global_compressor,
+    decode_updates_dict,
     decode_updates_into,
     encode_updates_dict,
 )
@@ -179,9 +181,10 @@ def test_client_and_ps_threads_unlocked_on_different_plans(gpu):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.int8])
 def test_device_to_host_ring_equals_cpu(gpu, dtype):
-    """hostio.device_to_host (the CPU placement's chunked D2H): same bytes as .cpu() for empty,
-    odd-sized and many-chunk tensors, the ring wrapping several times (small chunks, 3 slots), from
-    the main thread and from concurrent threads (each call leases its own ring)."""
+    """hostio.device_to_host (the CPU placement's D2H): same bytes as .cpu() for empty, odd-sized
+    and many-chunk tensors — through the D2HRing into pageable memory (the ring wrapping several
+    times: small chunks, 3 slots; from the main thread and from concurrent threads, each call
+    leasing its own ring) and into the pooled page-locked arenas."""
     from omnifed_amd import hostio
 
     g = torch.Generator(device=gpu).manual_seed(5)
@@ -190,11 +193,45 @@ def test_device_to_host_ring_equals_cpu(gpu, dtype):
         t = torch.randn(n, device=gpu, generator=g) * 100
         srcs.append(t.to(dtype))
     for s in srcs:
-        out = hostio.device_to_host(s, limit=1 << 16, slots=3)
+        out = hostio.device_to_host(s, limit=1 << 16, slots=3, pool_memory=False)  # the D2HRing
         assert out.device.type == "cpu" and out.dtype == dtype and not out.is_pinned()
         assert torch.equal(out, s.cpu())
-        assert torch.equal(hostio.device_to_host(s), s.cpu())
+        pooled = hostio.device_to_host(s)  # a pooled page-locked arena from 1 MiB up
+        assert pooled.dtype == dtype and torch.equal(pooled, s.cpu())
+        assert pooled.is_pinned() == (s.numel() * s.element_size() >= hostio.HostArenaPool.MIN_BYTES)
     with ThreadPoolExecutor(4) as ex:
-        outs = list(ex.map(lambda s: hostio.device_to_host(s, limit=1 << 16, slots=3), srcs * 2))
+        outs = list(ex.map(lambda s: hostio.device_to_host(s, limit=1 << 16, slots=3, pool_memory=False), srcs * 2))
     for o, s in zip(outs, srcs * 2):
         assert torch.equal(o, s.cpu())
+
+
+@pytest.mark.parametrize("bits", [4, 8])
+def test_qsgd_cpu_placement_pipeline_equals_device_decode(gpu, bits):
+    """decode_updates_dict() on the CPU (the reference's placement) decodes chunk by chunk as the
+    payloads arrive and copies the decoded chunks out on a second stream: bit-identical to the
+    device decode copied afterwards, for a message of several staging chunks (int8 and int32
+    wire), padding between tensors included."""
+    g = torch.Generator(device=gpu).manual_seed(40 + bits)
+    sizes = {"a": (4099,), "b": (3, 7), "c": (9 << 20,), "d": (1,), "e": (12 << 20,), "f": (1000, 1001)}
+    upd = {n: torch.randn(*s, device=gpu, generator=g) * 1e-2 for n, s in sizes.items()}
+    comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=bits, device=gpu)
+    layers = encode_updates_dict(upd, comp)
+    on_cpu = decode_updates_dict(layers)
+    on_gpu = decode_updates_dict(layers, device="cuda")
+    for L in layers:
+        a, b = on_cpu[L.layer_name], on_gpu[L.layer_name]
+        assert a.device.type == "cpu" and a.dtype == torch.float32 and a.shape == b.shape
+        assert np.array_equal(a.numpy().view(np.int32), b.cpu().numpy().view(np.int32)), L.layer_name
+
+
+def test_pinned_arena_pool_tensors_are_page_locked(gpu):
+    """The pooled page-locked arenas the CPU placement returns are seen by torch as pinned, so the
+    device-to-host copies into them are asynchronous DMAs."""
+    from omnifed_amd import hostio
+
+    t = hostio.PINNED_ARENAS.empty(4 << 20)
+    assert t.is_pinned()
+    src = torch.arange(1 << 20, device=gpu, dtype=torch.float32)
+    t.view(torch.float32).copy_(src, non_blocking=True)
+    torch.cuda.synchronize()
+    assert torch.equal(t.view(torch.float32), src.cpu())
