@@ -1460,11 +1460,11 @@ __global__ __launch_bounds__(kThreads) void topk_check_idx(int64_t* __restrict__
 // first placed into per-super-tile buckets (64 Ki arena elements each; a bucket's capacity is
 // twice the selection's expected count there + 256, fixed per (plan, ratio); what does not fit
 // goes to an overflow list), then one workgroup per super-tile stages its bucket in LDS, builds
-// each 8 Ki-element sub-tile in LDS (zeros + its values) and streams it out with 16-byte
+// each 16 Ki-element sub-tile in LDS (zeros + its values) and streams it out with 16-byte
 // non-temporal stores; a last kernel applies the (normally empty) overflow list.
 constexpr int kDecSuperBits = 16;
 #ifndef OMF_DEC_SUB_BITS  // experiment builds may override it (scripts/exp/tk_dec_ab.sh)
-#define OMF_DEC_SUB_BITS 13
+#define OMF_DEC_SUB_BITS 14
 #endif
 constexpr int kDecSubBits = OMF_DEC_SUB_BITS;
 constexpr int kDecSubs = 1 << (kDecSuperBits - kDecSubBits);
@@ -1581,7 +1581,7 @@ __global__ __launch_bounds__(kThreads) void topk_dec_place(const float* __restri
 }
 
 // One workgroup per super-tile: its bucket staged in LDS (up to kDecStage entries; a larger
-// one is read from L2 per sub-tile), then per 8 Ki-element sub-tile: zeros in LDS, its values,
+// one is read from L2 per sub-tile), then per 16 Ki-element sub-tile: zeros in LDS, its values,
 // 16-byte non-temporal stores (the arena's partial last sub-tile element by element).
 __global__ __launch_bounds__(kDecTileThreads) void topk_dec_tiles(const uint64_t* __restrict__ pairs,
                                                                   const uint32_t* __restrict__ cap_base,
