@@ -1470,7 +1470,10 @@ constexpr int kDecSubBits = OMF_DEC_SUB_BITS;
 constexpr int kDecSubs = 1 << (kDecSuperBits - kDecSubBits);
 constexpr int kDecMaxSuper = 16384;  // LDS bins of a place block (arenas <= 2^30 elements)
 constexpr int kDecChunk = 4096;      // selected values per place block
-constexpr int kDecTileThreads = 512;
+#ifndef OMF_DEC_TILE_THREADS  // experiment builds may override it (scripts/exp/tk_dec_ab.sh)
+#define OMF_DEC_TILE_THREADS 512
+#endif
+constexpr int kDecTileThreads = OMF_DEC_TILE_THREADS;
 #ifndef OMF_DEC_STAGE
 #define OMF_DEC_STAGE 2048
 #endif

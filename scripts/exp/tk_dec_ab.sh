@@ -14,10 +14,17 @@ build() {
   timeout -k 10 200 hipcc --offload-arch=gfx950 -shared -fPIC -o $d/lib.so $d/*.o || exit 1
   echo "built $d" >> gpurun_out/tkd_progress.txt  # a long silent build looks hung to the box
 }
-VARS="s13 s14 s15"
-build s13 -DOMF_DEC_SUB_BITS=13
-build s14 -DOMF_DEC_SUB_BITS=14
-build s15 -DOMF_DEC_SUB_BITS=15
+VARS="${VARS:-s13 s14 s15}"
+for v in $VARS; do
+  case $v in
+    s13) build s13 -DOMF_DEC_SUB_BITS=13 ;;
+    s14) build s14 -DOMF_DEC_SUB_BITS=14 ;;
+    s15) build s15 -DOMF_DEC_SUB_BITS=15 ;;
+    t1024) build t1024 -DOMF_DEC_SUB_BITS=14 -DOMF_DEC_TILE_THREADS=1024 ;;
+    t256) build t256 -DOMF_DEC_SUB_BITS=14 -DOMF_DEC_TILE_THREADS=256 ;;
+    k4) build k4 -DOMF_DEC_SUB_BITS=14 -DOMF_DEC_STAGE=4096 ;;
+  esac
+done
 echo built
 for rep in 1 2; do
 for v in $VARS; do
