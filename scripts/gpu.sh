@@ -66,19 +66,27 @@ case "$task" in
     cat gpurun_out/${T}_pmc_traffic.json
     ;;
   sq)
-    # SQ counter passes (VALU work, wave-cycle split) over the ResNet-18 encoder A/B
-    # (scripts/exp/r18_ab.py: ring, grid, two-launch encoders and the decoder), one pass per group
+    # SQ counter passes (VALU work, wave-cycle split, LDS stalls), one pass per group: by default
+    # over the ResNet-18 encoder A/B (scripts/exp/r18_ab.py: ring, grid, two-launch encoders and
+    # the decoder); SQ_PROG=topk over the Llama-400M Top-K encode + decode (bench.py --codec topk)
     T=${1:-r04_r18}
+    if [ "${SQ_PROG:-r18}" = topk ]; then
+      PROG=("$R/bench.py" --codec topk --steps 5 --warmup 2 --no-cpu-baseline --no-extras); CFG=llama400m
+    else
+      PROG=("$R/scripts/exp/r18_ab.py" 3 1); CFG=resnet18
+    fi
     i=0
     for grp in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_SALU" \
-               "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAVES SQ_INSTS_SMEM"; do
+               "SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_ACTIVE_INST_SCA SQ_WAVES SQ_INSTS_SMEM" \
+               "SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT SQ_LDS_IDX_ACTIVE SQ_LDS_ATOMIC_RETURN SQ_LDS_UNALIGNED_STALL"; do
       i=$((i+1))
       rm -rf gpurun_out/${T}_sq$i
+      echo "sq pass $i: $grp"
       timeout -s KILL 120 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$R/gpurun_out/${T}_sq$i" -o run \
-        -- python3 "$R/scripts/exp/r18_ab.py" 3 1 > gpurun_out/${T}_sq$i.log 2>&1 || { tail -20 gpurun_out/${T}_sq$i.log; exit 2; }
+        -- python3 "${PROG[@]}" > gpurun_out/${T}_sq$i.log 2>&1 || { tail -20 gpurun_out/${T}_sq$i.log; exit 2; }
     done
-    E=$(python3 -c "from omnifed_amd import shapes; print(sum(shapes.numel(s) for _, s in shapes.model_shapes('resnet18')))")
-    python3 scripts/sq_summary.py gpurun_out/${T}_sq.json "$E" gpurun_out/${T}_sq1 gpurun_out/${T}_sq2 || exit 3
+    E=$(python3 -c "from omnifed_amd import shapes; print(sum(shapes.numel(s) for _, s in shapes.model_shapes('$CFG')))")
+    python3 scripts/sq_summary.py gpurun_out/${T}_sq.json "$E" gpurun_out/${T}_sq1 gpurun_out/${T}_sq2 gpurun_out/${T}_sq3 || exit 3
     ;;
   py)
     S=$1
