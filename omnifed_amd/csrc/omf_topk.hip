@@ -1477,6 +1477,9 @@ constexpr int kDecTileThreads = OMF_DEC_TILE_THREADS;
 #ifndef OMF_DEC_STAGE
 #define OMF_DEC_STAGE 2048
 #endif
+#ifndef OMF_DEC_MASK  // experiment builds may override it (scripts/exp/tk_dec_ab.sh)
+#define OMF_DEC_MASK 0
+#endif
 constexpr int kDecStage = OMF_DEC_STAGE;  // bucket entries a tile workgroup stages in LDS (more: read from L2)
 
 __device__ __forceinline__ int dec_tensor_of(const int64_t* __restrict__ koff, int lo, int hi, int64_t j) {
@@ -1593,6 +1596,9 @@ __global__ __launch_bounds__(kDecTileThreads) void topk_dec_tiles(const uint64_t
   __shared__ float4 tile[(1 << kDecSubBits) / 4];
   __shared__ uint64_t stage[kDecStage];
   __shared__ uint32_t s_fill;
+#if OMF_DEC_MASK
+  __shared__ uint32_t s_mask[(1 << kDecSubBits) / 32];  // which tile elements this sub-tile set
+#endif
   float* tf = reinterpret_cast<float*>(tile);
   const uint32_t s = blockIdx.x;
   const uint32_t base = cap_base[s];
@@ -1610,6 +1616,39 @@ __global__ __launch_bounds__(kDecTileThreads) void topk_dec_tiles(const uint64_t
   for (int sub = 0; sub < kDecSubs; ++sub) {
     const int64_t b0 = ((int64_t)s << kDecSuperBits) + ((int64_t)sub << kDecSubBits);
     if (b0 >= arena_end) break;  // block-uniform
+#if OMF_DEC_MASK
+    // a bit per element instead of a zeroed tile: 2 KiB of LDS writes per sub-tile, not 64
+    for (int i = threadIdx.x; i < (1 << kDecSubBits) / 32; i += kDecTileThreads) s_mask[i] = 0u;
+    __syncthreads();  // (also: the staged bucket is complete)
+    for (uint32_t p = threadIdx.x; p < cnt; p += kDecTileThreads) {
+      const uint64_t pr = src[p];
+      const uint32_t in = (uint32_t)(pr >> 32);
+      if ((int)(in >> kDecSubBits) == sub) {
+        const uint32_t l = in & ((1u << kDecSubBits) - 1);
+        tf[l] = __uint_as_float((uint32_t)pr);
+        atomicOr(&s_mask[l >> 5], 1u << (l & 31));
+      }
+    }
+    __syncthreads();
+    if (b0 + (1 << kDecSubBits) <= arena_end) {
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const int e = 4 * (threadIdx.x + q * kDecTileThreads);
+        const uint32_t m = (s_mask[e >> 5] >> (e & 31)) & 0xfu;
+        float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (m) {  // elements of this sub-tile's earlier contents are stale: take the set ones only
+          const float4 t = tile[threadIdx.x + q * kDecTileThreads];
+          o.x = (m & 1u) ? t.x : 0.f; o.y = (m & 2u) ? t.y : 0.f;
+          o.z = (m & 4u) ? t.z : 0.f; o.w = (m & 8u) ? t.w : 0.f;
+        }
+        store_nt(y + b0 + e, o);
+      }
+    } else {
+      for (int64_t e = threadIdx.x; b0 + e < arena_end; e += kDecTileThreads)
+        y[b0 + e] = ((s_mask[e >> 5] >> (e & 31)) & 1u) ? tf[e] : 0.f;
+    }
+    __syncthreads();
+#else
 #pragma unroll
     for (int q = 0; q < Q; ++q) tile[threadIdx.x + q * kDecTileThreads] = make_float4(0.f, 0.f, 0.f, 0.f);
     __syncthreads();  // (also: the staged bucket is complete)
@@ -1629,6 +1668,7 @@ __global__ __launch_bounds__(kDecTileThreads) void topk_dec_tiles(const uint64_t
       for (int64_t e = threadIdx.x; b0 + e < arena_end; e += kDecTileThreads) y[b0 + e] = tf[e];
     }
     __syncthreads();
+#endif
   }
 }
 

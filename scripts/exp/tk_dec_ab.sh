@@ -1,7 +1,8 @@
 #!/bin/bash
-# Experiment (GPU box): the tiled Top-K decode's sub-tile size: 8 Ki elements (the default: 32 KiB
-# LDS tile + 2 Ki staged entries, 3 workgroups per CU) against 4 Ki (round 3) and 16 / 32 Ki
-# (round 4: 64 / 128 KiB tiles, more stores in flight per barrier phase, 2 / 1 workgroups per CU).
+# Experiment (GPU box): the tiled Top-K decode's shape, interleaved variants of one build each:
+# sub-tile size (s13 / s14 = the default 16 Ki, 64 KiB LDS tile / s15), tile threads (t256 / t1024),
+# staged entries (k4), and a bit per element in place of the zeroed tile (m1 / m15).  Variants
+# named in CHECK also run the Top-K GPU tests on their build first.
 set -o pipefail
 cd "$(dirname "$0")/../.." && export TMPDIR=/tmp
 F="--offload-arch=gfx950 -O3 -std=c++20 -fPIC -ffp-contract=off -fno-gpu-flush-denormals-to-zero -fhip-fp32-correctly-rounded-divide-sqrt -Iinclude"
@@ -23,9 +24,17 @@ for v in $VARS; do
     t1024) build t1024 -DOMF_DEC_SUB_BITS=14 -DOMF_DEC_TILE_THREADS=1024 ;;
     t256) build t256 -DOMF_DEC_SUB_BITS=14 -DOMF_DEC_TILE_THREADS=256 ;;
     k4) build k4 -DOMF_DEC_SUB_BITS=14 -DOMF_DEC_STAGE=4096 ;;
+    m1) build m1 -DOMF_DEC_SUB_BITS=14 -DOMF_DEC_MASK=1 ;;
+    m15) build m15 -DOMF_DEC_SUB_BITS=15 -DOMF_DEC_MASK=1 ;;
   esac
 done
 echo built
+for v in ${CHECK:-}; do
+  OMF_CODEC_LIB_EXPERIMENT=/tmp/omf_dec_$v/lib.so timeout -k 10 600 python3 -u -m pytest -x -q --timeout 120 \
+      --timeout-method thread -m gpu tests/test_gpu_topk_wire.py tests/test_gpu_topk_ps.py tests/test_gpu_topk_half.py \
+      > gpurun_out/tkd_check_$v.log 2>&1 || { tail -30 gpurun_out/tkd_check_$v.log; exit 4; }
+  tail -1 gpurun_out/tkd_check_$v.log
+done
 for rep in 1 2; do
 for v in $VARS; do
   o=gpurun_out/tkd_${v}_$rep; rm -rf $o
