@@ -54,7 +54,10 @@ constexpr int kShift = 21;  // key (31 bits) >> 21 -> 10-bit bin (exact path)
 constexpr int kSBits = 13;  // sample histogram: exponent + 5 mantissa bits
 constexpr int kSBins = 1 << kSBits;
 constexpr int kSShift = 31 - kSBits;
-constexpr int kSRun = 16;       // a sample is a 64-byte run of 16 consecutive elements,
+#ifndef OMF_SRUN  // experiment builds may override it (scripts/exp/tk_srun_ab.sh)
+#define OMF_SRUN 16
+#endif
+constexpr int kSRun = OMF_SRUN;  // a sample is a 64-byte run of 16 consecutive elements,
 constexpr int kSStride = 256;   // one run per >= 256 elements,
 // default: at most 2 Ki runs (32 Ki samples) per tensor (OMF_TOPK_SAMPLE_RUNS).  Llama-400M encode:
 // 1.024 ms at 2 Ki runs, 1.097 at 4 Ki, 1.142 at 8 Ki, 1.194 at 16 Ki (scripts/exp/tk_runs_sweep.py):
@@ -354,7 +357,10 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
                                                     uint32_t* __restrict__ thi, uint32_t* __restrict__ fmap,
                                                     uint32_t* __restrict__ tlo, uint32_t* __restrict__ fcount,
                                                     uint32_t* __restrict__ fhist, uint32_t blk0, float2 sure_zc) {
-  constexpr int U = kSRunsPerBlock / 256;  // runs per lane group, all loads in flight at once
+  constexpr int kLanesPerRun = kSRun / 4;  // one float4 per lane
+  constexpr int kGroups = 1024 / kLanesPerRun;
+  constexpr int U = kSRunsPerBlock / kGroups;  // runs per lane group, all loads in flight at once
+  static_assert(U * kGroups == kSRunsPerBlock && U >= 1, "runs per block: a multiple of the lane groups");
   __shared__ uint32_t h[kSBins];
   __shared__ uint32_t s_last;
   const uint32_t bid = blk0 + blockIdx.x;  // launches cover ranges of tensors (pipeline groups)
@@ -366,13 +372,13 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   const int64_t stride = sample_stride(n, max_runs), nr = (n + stride - 1) / stride;
   const int64_t r1 = min(r0 + (int64_t)kSRunsPerBlock, nr);
   const uint32_t salt = (uint32_t)t * 0x9E3779B9u;
-  const int q = threadIdx.x & 3;  // float4 of the run
+  const int q = threadIdx.x & (kLanesPerRun - 1);  // float4 of the run
   float4 xv[U], rv[U];
   int64_t rel[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {  // every load issued unconditionally (no branch around a load:
     // hipcc would wait for each one in turn); past-the-end runs clamped
-    const int64_t j = min(r0 + (threadIdx.x >> 2) + (int64_t)u * 256, r1 - 1);
+    const int64_t j = min(r0 + (int64_t)(threadIdx.x / kLanesPerRun) + (int64_t)u * kGroups, r1 - 1);
     const int64_t lo = j * stride;
     const int64_t span = min(stride, n - lo);
     const int64_t runs = max((int64_t)1, span / kSRun);
@@ -384,7 +390,7 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   __syncthreads();  // h cleared
 #pragma unroll
   for (int u = 0; u < U; ++u) {
-    if (r0 + (threadIdx.x >> 2) + (int64_t)u * 256 >= r1) continue;
+    if (r0 + (int64_t)(threadIdx.x / kLanesPerRun) + (int64_t)u * kGroups >= r1) continue;
     const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
     const float rs[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
 #pragma unroll
