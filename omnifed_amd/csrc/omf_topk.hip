@@ -63,6 +63,14 @@ constexpr int kSStride = 256;   // one run per >= 256 elements,
 // 1.024 ms at 2 Ki runs, 1.097 at 4 Ki, 1.142 at 8 Ki, 1.194 at 16 Ki (scripts/exp/tk_runs_sweep.py):
 // the sample's random sectors cost more than the tighter threshold saves in the bucket kernels.
 constexpr int kSMaxRuns = 2048;
+// The threshold bin's margin over the expected k*S/n samples: OMF_THR_Z sigma + OMF_THR_C (a
+// performance knob only — a tensor left with fewer than k candidates takes the exact redo).
+#ifndef OMF_THR_Z  // experiment builds may override them (scripts/exp/tk_thr_ab.sh)
+#define OMF_THR_Z 6.0
+#endif
+#ifndef OMF_THR_C
+#define OMF_THR_C 32.0
+#endif
 constexpr int kV = 16;
 constexpr int64_t kSub = (int64_t)kV * kThreads * 4;
 // Composite candidate key: index << 39 | tensor << 31 | (2^31 - 1 - |t'|bits).  Candidates are
@@ -261,7 +269,7 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, flo
     return S - inc;
   }();
   const double m = (double)kk[t] * (double)S / (double)max(n, (int64_t)1);
-  const double want = m + 6.0 * sqrt(m) + 32.0;
+  const double want = m + (double)OMF_THR_Z * sqrt(m) + (double)OMF_THR_C;
   __shared__ uint32_t s_thr, s_hikey, s_min, s_max;
   if (threadIdx.x == 0) {
     s_thr = 0;
