@@ -126,10 +126,10 @@ def affinity_cores() -> int:
         return os.cpu_count() or 1
 
 
-def cgroup_cpu_quota():
+def cgroup_cpu_quota(path: str = "/sys/fs/cgroup/cpu.max"):
     """The cgroup v2 CPU quota in whole CPUs (``cpu.max``: quota period), None when unlimited or absent."""
     try:
-        with open("/sys/fs/cgroup/cpu.max") as f:
+        with open(path) as f:
             quota, period = f.read().split()[:2]
     except (OSError, ValueError):
         return None
