@@ -62,7 +62,7 @@ extern "C" {
 typedef struct omf_plan omf_plan;
 
 /* ABI version (major*100 + minor). */
-#define OMF_ABI_VERSION 107
+#define OMF_ABI_VERSION 108
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -124,6 +124,11 @@ int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy);
  * draws at bit_width 1-4; its int32-wire encodes (bit_width >= 7, fp32, on-device draws) take the
  * ring (2), its other encodes (caller uniforms, s = 5, 6) the two-pass encoder (1). */
 int32_t omf_plan_encode_strategy(const omf_plan* plan);
+/* The encoder the plan's latest encode (or fused PS step) launched: 0 register-resident +
+ * two-pass, 1 two-pass, 2 ring, 3 bracketed, 4 grid, 5 levels with caller norms (norm_in);
+ * -1 before the first.  Lets a test assert which path a configuration takes (e.g. the int32
+ * wire of a bracketed plan: the ring). */
+int32_t omf_plan_last_encoder(const omf_plan* plan);
 /* Diagnostics of the last bracketed single-read encode (strategy 3; synchronises `stream`,
  * not for the hot path): out[0] tensors requantised whole (norm outside the sampled bracket,
  * a wave's undecided-quad slot overflowed, or a degenerate sample), out[1] of those the
@@ -285,6 +290,13 @@ int64_t omf_topk_k(int64_t numel, double ratio);
  * bin's margin.  A negative argument keeps the current setting. */
 int omf_plan_set_topk(omf_plan* plan, int32_t groups, int32_t force_fallback, int64_t sample_runs, float sure_z,
                       float sure_c);
+/* The plan's Top-K encoder counters (diagnostics; no synchronisation): out6[0] calls of the
+ * sampled path, [1] of those that took the bucket-sort fast path, [2] of those that completed a
+ * tensor with its lowest-index exact zeros (zero mode: fewer than k non-zero t', e.g. the PS
+ * re-encoding an average of sparse Top-K updates), [3] calls that took the device-wide
+ * radix-sort fallback, [4] of those that redid a tensor exactly, [5] calls of the exact path
+ * (plans of > 256 tensors or a tensor over 2^25 elements).  reset != 0 zeroes them after reading. */
+int omf_topk_stats(omf_plan* plan, int64_t* out6, int32_t reset);
 size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio);
 int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,
                     float alpha, float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream);

@@ -39,6 +39,7 @@ SIGNATURES = {
     "omf_plan_check": (ctypes.c_int, [_c_p, _c_p]),
     "omf_plan_set_encode_strategy": (ctypes.c_int, [_c_p, _c_i32]),
     "omf_plan_encode_strategy": (_c_i32, [_c_p]),
+    "omf_plan_last_encoder": (_c_i32, [_c_p]),
     "omf_plan_resident_capacity": (_c_i64, [_c_p]),
     "omf_plan_set_resident_capacity": (ctypes.c_int, [_c_p, _c_i64, _c_i64]),
     "omf_plan_set_ring": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i64, _c_i64]),
@@ -61,6 +62,7 @@ SIGNATURES = {
     "omf_qsgd_decode_packed": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
     "omf_topk_k": (_c_i64, [_c_i64, _c_f64]),
     "omf_plan_set_topk": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i64, _c_f32, _c_f32]),
+    "omf_topk_stats": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64), _c_i32]),
     "omf_topk_workspace_bytes": (_c_size, [_c_p, _c_f64]),
     "omf_topk_encode": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_f64, _c_f32, _c_p, _c_p, _c_p, _c_size, _c_p]),
     "omf_topk_decode": (ctypes.c_int, [_c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i32, _c_p]),
@@ -81,7 +83,7 @@ class CodecError(RuntimeError):
     pass
 
 
-ABI_VERSION = 107  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+ABI_VERSION = 108  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
 
 
 def lib() -> ctypes.CDLL:

@@ -175,6 +175,15 @@ class Plan:
             check(lib().omf_plan_set_topk(self._h, int(groups), int(fallback), int(sample_runs), z, c),
                   "omf_plan_set_topk")
 
+    def topk_stats(self, reset: bool = False) -> dict:
+        """The plan's Top-K encoder counters (omf_topk_stats): sampled-path calls, bucket-sort fast
+        path, zero fills (tensors completed with their lowest-index zeros), radix-sort fallbacks,
+        exact redos, exact-path calls."""
+        out = (ctypes.c_int64 * 6)()
+        with self._lock:
+            check(lib().omf_topk_stats(self._h, out, 1 if reset else 0), "omf_topk_stats")
+        return dict(zip(("calls", "fast", "zero_fill", "fallback", "redo", "exact"), (int(v) for v in out)))
+
     def set_debug(self, ring: int = 0, spec: int = 0, lds_wait_us: int = 0) -> None:
         """Test / experiment hook (omf_plan_set_debug): switches that change what an encode
         writes (never set in production); all zero restores the production behaviour."""
@@ -195,6 +204,13 @@ class Plan:
         code = STRATEGIES.index(strategy)
         check(lib().omf_plan_set_encode_strategy(self._h, code), "omf_plan_set_encode_strategy")
         self.strategy = strategy
+
+    @property
+    def last_encoder(self) -> str:
+        """The encoder the latest encode launched (omf_plan_last_encoder): one of STRATEGIES,
+        "norm_in" (levels with caller norms) or "none"."""
+        code = int(lib().omf_plan_last_encoder(self._h))
+        return STRATEGIES[code] if 0 <= code < len(STRATEGIES) else ("norm_in" if code == 5 else "none")
 
     @property
     def encoder_kernel(self) -> str:

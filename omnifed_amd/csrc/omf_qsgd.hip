@@ -1329,6 +1329,7 @@ struct omf_plan {
   int64_t cap = 0;               // tensors of <= cap items take the register-resident path
   int32_t strategy = 2;          // 0 register-resident + two-pass, 1 ticket-ordered two-pass, 2 single-read ring,
                                  // 3 bracketed single-read (default by size: omf_plan_create)
+  int32_t last_encoder = -1;     // the encoder the latest encode launched (omf_plan_last_encoder)
   uint64_t wait_ticks = kWaitTicks;      // norm waits (ring: expiry recomputes; bracketed fix: expiry fails)
   uint64_t lds_wait_ticks = kWaitTicks;  // the ring's on-chip hand-off waits (expiry aborts the workgroup)
   uint32_t epoch = 0;            // last granule tag used (host-side launch counter)
@@ -1934,6 +1935,7 @@ int64_t omf_plan_encode_items(const omf_plan* plan) {
 }
 
 int32_t omf_plan_encode_strategy(const omf_plan* plan) { return plan ? plan->strategy : -1; }
+int32_t omf_plan_last_encoder(const omf_plan* plan) { return plan ? plan->last_encoder : -1; }
 
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
@@ -2104,6 +2106,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     a.items = p->d_flat;
     a.tinfo = p->d_tinfo[0];
     const dim3 grid4((unsigned)(p->n_flat * 4));  // 4 blocks of 4 Ki elements per 16 Ki item
+    p->last_encoder = 5;
     if (width == 1) {
       if (u) hipLaunchKernelGGL((qsgd_quant_sub<1, true, 4, false>), grid4, blk, 0, st, a);
       else hipLaunchKernelGGL((qsgd_quant_sub<1, false, 4, false>), grid4, blk, 0, st, a);
@@ -2138,6 +2141,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     // counted only once the launch is in: the device's monotonic arrival counter advances by
     // grid_wgs per launch that ran, so a failed launch must not move the host's target
     ++p->grid_launches;
+    p->last_encoder = 4;
     return OMF_OK;
   }
   // Bracketed single-read encoder: fp32 / bf16 / fp16 values with on-device draws at s <= 4
@@ -2150,6 +2154,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     a.items = p->d_flat;
     a.tinfo = p->d_tinfo[1];
     sa.e = a;
+    p->last_encoder = 3;
     sa.begins = p->d_begins;
     sa.sizes = p->d_sizes;
     sa.br_items = p->d_spec_br_items;
@@ -2228,6 +2233,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     r.dbg = p->ring_dbg;
     r.prof = p->d_ring_prof;
     const int grid = (int)std::min<int64_t>(p->ring_grid, std::max<int64_t>(p->n_ring, 1));
+    p->last_encoder = 2;
     if (omf::ring::launch(p->ring_cfg, width, u != nullptr, r, grid, st) != 0)
       return fail(OMF_EHIP, "ring encoder launch failed");
     OMF_HIP(hipGetLastError());
@@ -2242,6 +2248,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
   a.items = p->d_enc[strat];
   a.tinfo = p->d_tinfo[strat];
   const dim3 grid((unsigned)p->n_enc[strat]);
+  if (!norm_only) p->last_encoder = strat;
 #define OMF_ENC(EV)                                                                              \
   do {                                                                                           \
     if (norm_only) {                                                                             \

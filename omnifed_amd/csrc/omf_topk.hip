@@ -242,14 +242,20 @@ __device__ __forceinline__ int64_t sample_stride(int64_t n, int64_t max_runs) {
 #endif
 constexpr int kSRunsPerBlock = OMF_SRUNS_PER_BLOCK;
 
-// The tensor's threshold from its sample histogram h (LDS, kSBins, loaded; 1024 threads):
-// the threshold bin — the bin whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of the S samples
-// (0 = every element, for tensors too small to sample) — the "sure" bin, and the fine-bin map.
+// The tensor's threshold from its sample histogram h (LDS, kSBins, loaded; 1024 threads) of
+// the non-zero samples and its count of exact-zero samples `zeros`: the threshold bin — the bin
+// whose suffix holds k*S/n + 6 sqrt(k*S/n) + 32 of the S samples — the "sure" bin, and the
+// fine-bin map.  The threshold is stored as a magnitude key (tkey): bin << 18, or 1 — every
+// non-zero element, the zeros excluded — when the target is not reached above bin 0 (too few
+// samples to trust, or fewer non-zero samples than the target: an exact-zero-heavy tensor such
+// as the PS's average of sparse Top-K updates).  Exact zeros are never candidates: when a tensor
+// has fewer than k non-zeros, its selection is completed by its lowest-index zeros (topk_plan
+// and topk_zero_fill), the order the exact path's stable sort gives ties.
 // Also clears the tensor's redo histogram, its items' candidate counts and its fine bins.
-__device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, float2 sure_zc,
+__device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, uint32_t zeros, float2 sure_zc,
                                         const int64_t* __restrict__ kk,
                                         const uint32_t* __restrict__ tfirst, const uint32_t* __restrict__ tlast,
-                                        uint32_t* __restrict__ tbin, uint32_t* __restrict__ hist,
+                                        uint32_t* __restrict__ tkey, uint32_t* __restrict__ hist,
                                         uint32_t* __restrict__ item_cnt, uint32_t* __restrict__ thi,
                                         uint32_t* __restrict__ fmap, uint32_t* __restrict__ tlo,
                                         uint32_t* __restrict__ fcount, uint32_t* __restrict__ fhist) {
@@ -268,6 +274,7 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, flo
     const uint32_t inc = block_scan_incl<1024>(loc, s_w, S);
     return S - inc;
   }();
+  S += zeros;  // every sample, for the expected counts
   const double m = (double)kk[t] * (double)S / (double)max(n, (int64_t)1);
   const double want = m + (double)OMF_THR_Z * sqrt(m) + (double)OMF_THR_C;
   __shared__ uint32_t s_thr, s_hikey, s_min, s_max;
@@ -345,7 +352,7 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, flo
   const uint32_t off = inc - (1u << rbits);
   fmap[(size_t)t * kCoarse + threadIdx.x] = off | (rbits << 16);
   if (threadIdx.x == 0) {
-    tbin[t] = thr;
+    tkey[t] = thr > 0 ? thr << kSShift : 1u;  // 1: every non-zero (zero mode)
     thi[t] = max(s_hikey, (thr + 1u) << kSShift);  // a magnitude key: sure keys are candidates
     tlo[t] = lo;
     fcount[t] = F;
@@ -358,9 +365,10 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
                                                     float alpha, const int64_t* __restrict__ tbegin,
                                                     const int64_t* __restrict__ tsize, const uint32_t* __restrict__ smap,
                                                     int64_t max_runs, uint32_t* __restrict__ gh,
+                                                    uint32_t* __restrict__ gz,
                                                     uint32_t* __restrict__ arrive, uint32_t* __restrict__ status,
                                                     const int64_t* __restrict__ kk, const uint32_t* __restrict__ tfirst,
-                                                    const uint32_t* __restrict__ tlast, uint32_t* __restrict__ tbin,
+                                                    const uint32_t* __restrict__ tlast, uint32_t* __restrict__ tkey,
                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ item_cnt,
                                                     uint32_t* __restrict__ thi, uint32_t* __restrict__ fmap,
                                                     uint32_t* __restrict__ tlo, uint32_t* __restrict__ fcount,
@@ -370,12 +378,13 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   constexpr int U = kSRunsPerBlock / kGroups;  // runs per lane group, all loads in flight at once
   static_assert(U * kGroups == kSRunsPerBlock && U >= 1, "runs per block: a multiple of the lane groups");
   __shared__ uint32_t h[kSBins];
-  __shared__ uint32_t s_last;
+  __shared__ uint32_t s_last, s_zero;
   const uint32_t bid = blk0 + blockIdx.x;  // launches cover ranges of tensors (pipeline groups)
   const int t = (int)smap[2 * bid];
   const int64_t r0 = smap[2 * bid + 1];
   if (bid == 0 && threadIdx.x < 4) status[threadIdx.x] = 0u;
   for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
+  if (threadIdx.x == 0) s_zero = 0;
   const int64_t base = tbegin[t], n = tsize[t];
   const int64_t stride = sample_stride(n, max_runs), nr = (n + stride - 1) / stride;
   const int64_t r1 = min(r0 + (int64_t)kSRunsPerBlock, nr);
@@ -396,24 +405,34 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
     rv[u] = MODE == 1 ? *reinterpret_cast<const float4*>(r + e) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();  // h cleared
+  uint32_t zc = 0;  // exact-zero samples: counted apart (one LDS atomic per wave, not per sample)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (r0 + (int64_t)(threadIdx.x / kLanesPerRun) + (int64_t)u * kGroups >= r1) continue;
     const float xs[4] = {xv[u].x, xv[u].y, xv[u].z, xv[u].w};
     const float rs[4] = {rv[u].x, rv[u].y, rv[u].z, rv[u].w};
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (rel[u] + c < n) atomicAdd(&h[mag_key(tprime<MODE>(xs[c], rs[c], alpha)) >> kSShift], 1u);
+    for (int c = 0; c < 4; ++c) {
+      if (rel[u] + c >= n) continue;
+      const uint32_t key = mag_key(tprime<MODE>(xs[c], rs[c], alpha));
+      if (key) atomicAdd(&h[key >> kSShift], 1u);
+      else ++zc;
+    }
   }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) zc += __shfl_xor(zc, o, 64);
+  if ((threadIdx.x & 63) == 0 && zc) atomicAdd(&s_zero, zc);
   __syncthreads();
   const uint32_t nblk = (uint32_t)((nr + kSRunsPerBlock - 1) / kSRunsPerBlock);
   if (nblk == 1) {  // the tensor's whole sample is in this block's histogram (the usual case)
-    sample_threshold_tensor(t, n, h, sure_zc, kk, tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
+    sample_threshold_tensor(t, n, h, s_zero, sure_zc, kk, tfirst, tlast, tkey, hist, item_cnt, thi, fmap, tlo, fcount,
+                            fhist);
     return;
   }
   uint32_t* g = gh + (size_t)t * kSBins;
   for (int b = threadIdx.x; b < kSBins; b += 1024)
     if (h[b]) atomicAdd(&g[b], h[b]);
+  if (threadIdx.x == 0 && s_zero) atomicAdd(&gz[t], s_zero);
   // Arrival (cdna_hip_programming.md §6 Guideline 16, row 1): every wave waits for its
   // histogram atomics (vmcnt(0); agent-scope RMWs are performed past the XCD's L2), a workgroup
   // barrier, then one agent-scope add.  No __threadfence: on gfx950 an agent-scope release
@@ -428,8 +447,10 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   __syncthreads();
   if (!s_last) return;
   for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = atomicExch(&g[b], 0u);  // read + clear for the next call
+  if (threadIdx.x == 0) s_zero = atomicExch(&gz[t], 0u);
   __syncthreads();
-  sample_threshold_tensor(t, n, h, sure_zc, kk, tfirst, tlast, tbin, hist, item_cnt, thi, fmap, tlo, fcount, fhist);
+  sample_threshold_tensor(t, n, h, s_zero, sure_zc, kk, tfirst, tlast, tkey, hist, item_cnt, thi, fmap, tlo, fcount,
+                          fhist);
 }
 
 // Fine bin of a candidate magnitude (monotone in mag; below / above the mapped range clamp
@@ -547,7 +568,7 @@ template <int MODE>
 __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__ x, float* __restrict__ r, float alpha,
                                                        const Item* __restrict__ items,
                                                        const int64_t* __restrict__ tbegin,
-                                                       const uint32_t* __restrict__ tbin,
+                                                       const uint32_t* __restrict__ tkey,
                                                        const uint32_t* __restrict__ thi,
                                                        uint32_t* __restrict__ sub_cnt, uint32_t* __restrict__ item_cnt,
                                                        uint64_t* __restrict__ cand, uint32_t sub0) {
@@ -559,7 +580,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
     if (threadIdx.x == 0) sub_cnt[bid] = 0;
     return;
   }
-  const uint32_t thr = tbin[it.tensor], hi = thi[it.tensor];
+  const uint32_t thr = tkey[it.tensor], hi = thi[it.tensor];
   const int64_t base = tbegin[it.tensor];
   const uint32_t lim = (uint32_t)(min(b + kSubPer, it.end) - b);
   const uint32_t o = 4u * threadIdx.x;
@@ -587,7 +608,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
   }
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    if (o + c < lim && (mag_key(vv[c]) >> kSShift) >= thr) selm |= 1u << c;
+    if (o + c < lim && mag_key(vv[c]) >= thr) selm |= 1u << c;
   if (MODE != 0) {
     float rr[4];
 #pragma unroll
@@ -996,25 +1017,31 @@ __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restric
 
 // Fast path, plan (one block per tensor): suffix counts of the fine bins from the top; the
 // bins that start above rank k are kept, bin i goes to bucket floor(se_i / kBucketHalf)
-// (se_i = keys in higher bins), a bucket starts at its smallest se.  Flags the tensor for
-// the exact redo when it has fewer than k candidates, and the call for the fallback sort
-// when a kept fine bin holds more than kBucketHalf keys.  status[1] |= redo, [2] |= overflow.
+// (se_i = keys in higher bins), a bucket starts at its smallest se.  A tensor with fewer than
+// k candidates is flagged for the exact redo — unless its threshold was every non-zero (zero
+// mode, tkey == 1): then every candidate is selected (ranks [0, c)) and the rest of its
+// selection is its k - c lowest-index exact zeros, written by topk_zero_fill; zcnt[t] = c for
+// such a tensor, 0xffffffff otherwise.  Flags the call for the fallback sort when a kept fine
+// bin holds more than kBucketHalf keys.  status[0] |= zero fill, [1] |= redo, [2] |= overflow.
+constexpr uint32_t kNoZeroFill = 0xffffffffu;
 __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
                                  const uint32_t* __restrict__ fhist, const uint32_t* __restrict__ bbase,
                                  int32_t* __restrict__ fbucket, uint32_t* __restrict__ bstart,
                                  BucketRec* __restrict__ brec, uint32_t* __restrict__ bfill,
                                  const int64_t* __restrict__ kb2, uint32_t* __restrict__ flag,
-                                 uint32_t* __restrict__ status, uint32_t* __restrict__ fse, int dbg);
+                                 uint32_t* __restrict__ status, uint32_t* __restrict__ fse,
+                                 const uint32_t* __restrict__ tkey, uint32_t* __restrict__ zcnt, int dbg);
 __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
                                                   const uint32_t* __restrict__ fhist,
                                                   const uint32_t* __restrict__ bbase, int32_t* __restrict__ fbucket,
                                                   uint32_t* __restrict__ bstart, BucketRec* __restrict__ brec,
                                                   uint32_t* __restrict__ bfill, const int64_t* __restrict__ kb2,
                                                   uint32_t* __restrict__ flag, uint32_t* __restrict__ status,
-                                                  uint32_t* __restrict__ fse, int dbg, uint32_t* __restrict__ done,
+                                                  uint32_t* __restrict__ fse, const uint32_t* __restrict__ tkey,
+                                                  uint32_t* __restrict__ zcnt, int dbg, uint32_t* __restrict__ done,
                                                   uint32_t* host, uint32_t seq, int32_t t0, uint32_t total) {
   topk_plan_tensor((int)(t0 + blockIdx.x), kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2, flag, status,
-                   fse, dbg);
+                   fse, tkey, zcnt, dbg);
   // The last block to finish publishes the call's verdict straight into mapped, coherent host
   // memory (no copy packet in the stream, so the bucket kernels behind this one start at once):
   // the data words, then the sequence number with release semantics at system scope; the host
@@ -1040,13 +1067,15 @@ __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const ui
                                  int32_t* __restrict__ fbucket, uint32_t* __restrict__ bstart,
                                  BucketRec* __restrict__ brec, uint32_t* __restrict__ bfill,
                                  const int64_t* __restrict__ kb2, uint32_t* __restrict__ flag,
-                                 uint32_t* __restrict__ status, uint32_t* __restrict__ fse, int dbg) {
+                                 uint32_t* __restrict__ status, uint32_t* __restrict__ fse,
+                                 const uint32_t* __restrict__ tkey, uint32_t* __restrict__ zcnt, int dbg) {
   constexpr int PER = kFineMax / 1024;
   __shared__ uint32_t s_bs[kPlanMaxBuckets];
   __shared__ uint32_t part[1024];
   __shared__ uint32_t s_kend, s_nb, s_over;
   const uint32_t F = fcount[t];
-  const uint64_t k = (uint64_t)kk[t];
+  const bool zero_mode = tkey[t] == 1u;
+  uint64_t k = (uint64_t)kk[t];
   const uint32_t b0 = bbase[t], nbmax = bbase[t + 1] - b0;
   const uint32_t* ht = fhist + (size_t)t * kFineMax;
   uint32_t h[PER], loc = 0;
@@ -1065,14 +1094,21 @@ __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const ui
   uint32_t tot32;
   const uint32_t inc = block_scan_incl<1024>(loc, part, tot32);
   const uint64_t total = tot32;
-  if (total < k) {  // the sampled threshold was too high: exact redo (fallback path)
+  if (total < k && !zero_mode) {  // the sampled threshold was too high: exact redo (fallback path)
     if (threadIdx.x == 0) {
       flag[t] = 1u;
+      zcnt[t] = kNoZeroFill;
       atomicOr(&status[1], 1u);
     }
     for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) brec[b0 + j] = BucketRec{0, 0, 0};
     return;
   }
+  const bool zero_fill = total < k;  // zero mode: every candidate selected, then zeros
+  if (threadIdx.x == 0) {
+    zcnt[t] = zero_fill ? tot32 : kNoZeroFill;
+    if (zero_fill) atomicOr(&status[0], 1u);
+  }
+  if (zero_fill) k = total;  // the lowest candidate bin ends the kept range
   uint64_t se = tot32 - inc;  // keys in the bins of higher threads
   int32_t* fb = fbucket + (size_t)t * kFineMax;
   for (int j = PER - 1; j >= 0; --j) {
@@ -1369,6 +1405,96 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(OMF_SORT_WA
     } else if (r && sure && !(dbg & 2)) {
       r[base + idx] = v;  // a "sure" key that was not selected after all: t' back
     }
+  }
+}
+
+// Fast path, zero mode (topk_plan_tensor): a tensor with c < k non-zero t' selects all of them
+// (ranks [0, c), written by the bucket sort) and then its k - c lowest-index exact zeros, at
+// ranks [c, k) in index order — the (|t'| descending, index ascending) order.  Since the tensor
+// has only c non-zeros, its first k elements hold at least k - c zeros, so only the sub-chunks
+// (1 Ki elements) below index k are visited: one 256-thread block per such sub-chunk (zmap =
+// (tensor, sub) pairs of the plan-owned table).  A block counts the non-zeros before its sub
+// (the fused pass's per-sub candidate counts: in zero mode exactly the non-zeros), marks its
+// sub's non-zeros from their candidate keys in an LDS bitmap, and ranks its zeros with a block
+// scan; value = t' (the sign of the zero), residual := t' - t' (+0).  Launched only when the
+// plan's verdict reports a zero fill.
+__global__ __launch_bounds__(kThreads) void topk_zero_fill(const uint2* __restrict__ zmap,
+                                                           const uint32_t* __restrict__ zcnt,
+                                                           const int64_t* __restrict__ kk,
+                                                           const int64_t* __restrict__ koff,
+                                                           const int64_t* __restrict__ tbegin,
+                                                           const int64_t* __restrict__ tsize,
+                                                           const uint32_t* __restrict__ tfirst,
+                                                           const Item* __restrict__ items,
+                                                           const uint32_t* __restrict__ sub_cnt,
+                                                           const uint64_t* __restrict__ cand,
+                                                           const float* __restrict__ tp, float scale,
+                                                           float* __restrict__ r, float* __restrict__ values,
+                                                           int64_t* __restrict__ indices) {
+  __shared__ uint32_t s_bm[kSubPer / 32];
+  __shared__ uint32_t s_w[kWaves];
+  __shared__ uint32_t s_sum[kWaves];
+  const uint2 zm = zmap[blockIdx.x];
+  const int t = (int)zm.x;
+  const uint32_t x = zm.y;
+  const uint32_t c = zcnt[t];
+  if (c == kNoZeroFill) return;  // block-uniform
+  const int64_t k = kk[t], n = tsize[t], base = tbegin[t];
+  const int64_t rel0 = (int64_t)x * kSubPer;
+  const uint32_t s0 = tfirst[t] * (uint32_t)kSubsPerItem;
+  // non-zeros before this sub
+  uint32_t nz = 0;
+  for (uint32_t j = threadIdx.x; j < x; j += kThreads) nz += sub_cnt[s0 + j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) nz += __shfl_xor(nz, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) s_sum[wave] = nz;
+  if (threadIdx.x < kSubPer / 32) s_bm[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t nzb = 0;
+#pragma unroll
+  for (int w2 = 0; w2 < kWaves; ++w2) nzb += s_sum[w2];
+  const int64_t z = k - (int64_t)c;                 // zeros to select
+  const int64_t zr0 = rel0 - (int64_t)nzb;          // zeros before this sub
+  if (zr0 >= z) return;                             // block-uniform
+  const uint32_t g = s0 + x;
+  const int64_t b = items[g / kSubsPerItem].begin + (int64_t)(g % kSubsPerItem) * kSubPer;
+  const uint32_t cx = sub_cnt[g];
+  for (uint32_t e = threadIdx.x; e < cx; e += kThreads) {
+    const uint32_t rel = (uint32_t)(cand[b + e] >> 32) - (uint32_t)rel0;  // < kSubPer
+    atomicOr(&s_bm[rel >> 5], 1u << (rel & 31));
+  }
+  __syncthreads();
+  const uint32_t o = 4u * threadIdx.x;
+  const uint32_t bits = (s_bm[o >> 5] >> (o & 31)) & 0xFu;
+  uint32_t zmask = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+    if (rel0 + o + q < n && !((bits >> q) & 1u)) zmask |= 1u << q;
+  const uint32_t mine = (uint32_t)__popc(zmask);
+  uint32_t inc = mine;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = __shfl_up(inc, d, 64);
+    if (lane >= d) inc += u;
+  }
+  if (lane == 63) s_w[wave] = inc;
+  __syncthreads();
+  uint32_t pos = inc - mine;
+#pragma unroll
+  for (int w2 = 0; w2 < kWaves; ++w2)
+    if (w2 < wave) pos += s_w[w2];
+  const int64_t out0 = koff[t] + (int64_t)c;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (!((zmask >> q) & 1u)) continue;
+    const int64_t zr = zr0 + (int64_t)pos++;
+    if (zr >= z) break;
+    const int64_t idx = rel0 + o + q;
+    const float v = __fmul_rn(tp[base + idx], scale);  // +-0
+    values[out0 + zr] = v;
+    indices[out0 + zr] = idx;
+    if (r) r[base + idx] = __fsub_rn(v, v);
   }
 }
 
@@ -1726,7 +1852,6 @@ struct HostSync {
   uint32_t* pinned = nullptr;  // host view
   uint32_t* dev = nullptr;     // device view of the same bytes
   uint32_t seq = 0;
-  double verdict_us = 0.0;     // recent launch-to-verdict time (fast to fall, slow to rise)
   hipStream_t side = nullptr;  // the pipeline's second stream (made on first use)
   hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t fused[2] = {nullptr, nullptr};  // per stream: its latest group's streaming pass issued
@@ -1736,11 +1861,12 @@ struct HostSync {
 // ends (~90 % into the call; the bucket kernels are queued behind it, so the GPU stays busy while
 // the host reads it).  The host first sleeps for 60 % of the recent launch-to-verdict time — the
 // thread is descheduled instead of spinning a core for ~0.8 ms a call — then spins on the mapped
-// word (an event or a copy packet would add tens of us).  If it has not come after 200 ms,
+// word (an event or a copy packet would add tens of us).  The time is the plan's (TopkStats).
+// If it has not come after 200 ms,
 // synchronise the stream (which reports a failed launch or fault) and look again.
-int wait_status(HostSync* h, uint32_t seq, hipStream_t st, std::chrono::steady_clock::time_point t0) {
-  if (h->verdict_us > 200.0) {
-    const auto nap = std::chrono::microseconds((int64_t)(0.6 * h->verdict_us));
+int wait_status(HostSync* h, uint32_t seq, hipStream_t st, std::chrono::steady_clock::time_point t0, TopkStats* ps) {
+  if (ps->verdict_us > 200.0) {
+    const auto nap = std::chrono::microseconds((int64_t)(0.6 * ps->verdict_us));
     if (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq) std::this_thread::sleep_until(t0 + nap);
   }
   while (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq) {
@@ -1753,7 +1879,7 @@ int wait_status(HostSync* h, uint32_t seq, hipStream_t st, std::chrono::steady_c
     __builtin_ia32_pause();
   }
   const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-  h->verdict_us = (h->verdict_us == 0.0 || us < h->verdict_us) ? us : 0.9 * h->verdict_us + 0.1 * us;
+  ps->verdict_us = (ps->verdict_us == 0.0 || us < ps->verdict_us) ? us : 0.9 * ps->verdict_us + 0.1 * us;
   return OMF_OK;
 }
 HostSync* host_sync(int dev) {
@@ -1904,7 +2030,7 @@ size_t sort_tmp_bytes(const omf_plan* p) {
 // Workspace: everything up to `zero_end` is cleared once per call on the exact path; the
 // sampled path clears its redo histograms in topk_sample and writes the rest.
 struct WsLayout {
-  size_t hist, bin, cnt, flag, status, zero_end, tbin, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
+  size_t hist, bin, cnt, flag, status, zero_end, tkey, zcnt, koff, kk, tfirst, tlast, seg_b, seg_e, cstart,
       sub_cnt, item_cnt, item_off, cand, sorted, tmp, total, tmp_bytes, bbase, kb2, fmap, tlo, fcount, fhist,
       fbucket, fse, bstart, brec, bfill, nb_max, sbase, thi;
 };
@@ -1947,7 +2073,8 @@ WsLayout layout_uncached(const omf_plan* p) {
   L.flag = o; o = align256(o + 4 * (size_t)nt);
   L.status = o; o = align256(o + 16);
   L.zero_end = o;
-  L.tbin = o; o = align256(o + 4 * (size_t)nt);
+  L.tkey = o; o = align256(o + 4 * (size_t)nt);
+  L.zcnt = o; o = align256(o + 4 * (size_t)nt);
   L.koff = o; o = align256(o + 8 * (size_t)(nt + 1));
   L.kk = o; o = align256(o + 8 * (size_t)nt);
   L.tfirst = o; o = align256(o + 4 * (size_t)nt);
@@ -1990,9 +2117,10 @@ WsLayout layout_uncached(const omf_plan* p) {
 // sample (per tensor) and plan kernels (likewise).
 struct SetupTable {
   int64_t *kk, *koff, *kb2;
-  uint32_t *tfirst, *tlast, *bbase, *sbase, *smap, *gh, *done, *arrive;
+  uint32_t *tfirst, *tlast, *bbase, *sbase, *smap, *gh, *gz, *done, *arrive;
   uint32_t* supinfo;  // per super-item {tensor, first item, items, 0}
-  int32_t nsb;
+  uint32_t* zmap;     // per zero-fill block {tensor, sub-chunk}: the sub-chunks below index k_t
+  int32_t nsb, nzb;
 };
 
 // Runs sampled per tensor at most (a performance knob only: the selection is exact for any
@@ -2033,6 +2161,14 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
     }
     item0 += ni;
   }
+  std::vector<uint32_t> zmap;  // topk_zero_fill's blocks
+  for (int32_t t = 0; t < nt; ++t) {
+    const int64_t k = std::min(omf_topk_k(sizes[t], ratio), sizes[t]);
+    for (int64_t x = 0; x * kSubPer < k; ++x) {
+      zmap.push_back((uint32_t)t);
+      zmap.push_back((uint32_t)x);
+    }
+  }
   size_t o = 0;
   const size_t o_kk = o; o = align256(o + 8 * (size_t)nt);
   const size_t o_koff = o; o = align256(o + 8 * ((size_t)nt + 1));
@@ -2043,8 +2179,10 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
   const size_t o_sb = o; o = align256(o + 4 * ((size_t)nt + 1));
   const size_t o_sm = o; o = align256(o + 4 * smap.size());
   const size_t o_si = o; o = align256(o + 4 * supinfo.size());
+  const size_t o_zm = o; o = align256(o + 4 * std::max<size_t>(zmap.size(), 2));
   const size_t o_done = o; o = align256(o + 16);
   const size_t o_arr = o; o = align256(o + 4 * (size_t)nt);
+  const size_t o_gz = o; o = align256(o + 4 * (size_t)nt);
   const size_t o_gh = o; o = align256(o + 4 * (size_t)nt * kSBins);
   bool fresh = false;
   uint64_t* host = nullptr;
@@ -2065,11 +2203,16 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
   out->done = reinterpret_cast<uint32_t*>(d + o_done);
   out->arrive = reinterpret_cast<uint32_t*>(d + o_arr);
   out->gh = reinterpret_cast<uint32_t*>(d + o_gh);
+  out->gz = reinterpret_cast<uint32_t*>(d + o_gz);
+  out->zmap = reinterpret_cast<uint32_t*>(d + o_zm);
   out->nsb = (int32_t)(smap.size() / 2);
+  out->nzb = (int32_t)(zmap.size() / 2);
   if (fresh) {
-    OMF_HIP(hipMemsetAsync(out->done, 0, o - o_done, st));  // the arrival counters and gh
+    OMF_HIP(hipMemsetAsync(out->done, 0, o - o_done, st));  // the arrival counters, gz and gh
     OMF_HIP(hipMemcpyAsync(out->smap, smap.data(), 4 * smap.size(), hipMemcpyHostToDevice, st));
     OMF_HIP(hipMemcpyAsync(out->supinfo, supinfo.data(), 4 * supinfo.size(), hipMemcpyHostToDevice, st));
+    if (!zmap.empty())
+      OMF_HIP(hipMemcpyAsync(out->zmap, zmap.data(), 4 * zmap.size(), hipMemcpyHostToDevice, st));
     hipLaunchKernelGGL(topk_setup, dim3(1), dim3(kThreads), 0, st, omf_plan_access::d_sizes(p), nt, ratio, out->kk,
                        out->koff, out->tfirst, out->tlast, out->bbase, out->kb2, out->sbase, status, 0u);
     OMF_HIP(hipGetLastError());
@@ -2099,6 +2242,15 @@ int omf_plan_set_topk(omf_plan* plan, int32_t groups, int32_t force_fallback, in
   if (sample_runs >= 0) k.sample_runs = sample_runs;
   if (sure_z >= 0.f) k.sure_z = sure_z;
   if (sure_c >= 0.f) k.sure_c = sure_c;
+  return OMF_OK;
+}
+
+int omf_topk_stats(omf_plan* plan, int64_t* out6, int32_t reset) {
+  if (!plan || !out6) return fail(OMF_EINVAL, "plan and out6 must be non-NULL");
+  TopkStats& s = omf_plan_access::topk_knobs(plan).stats;
+  const int64_t v[6] = {s.calls, s.fast, s.zero_fill, s.fallback, s.redo, s.exact};
+  std::memcpy(out6, v, sizeof v);
+  if (reset) s.calls = s.fast = s.zero_fill = s.fallback = s.redo = s.exact = 0;
   return OMF_OK;
 }
 
@@ -2137,7 +2289,8 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);
   uint32_t* flag = reinterpret_cast<uint32_t*>(w + L.flag);
   uint32_t* status = reinterpret_cast<uint32_t*>(w + L.status);
-  uint32_t* tbin = reinterpret_cast<uint32_t*>(w + L.tbin);
+  uint32_t* tkey = reinterpret_cast<uint32_t*>(w + L.tkey);
+  uint32_t* zcnt = reinterpret_cast<uint32_t*>(w + L.zcnt);
   int64_t* koff = reinterpret_cast<int64_t*>(w + L.koff);
   int64_t* kk = reinterpret_cast<int64_t*>(w + L.kk);
   uint32_t* tfirst = reinterpret_cast<uint32_t*>(w + L.tfirst);
@@ -2183,6 +2336,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   // the per-(plan, ratio) constant tables: made by topk_setup on the first call at this ratio
   SetupTable tb;
   const TopkKnobs& kn = knobs(plan);
+  TopkStats& stats = omf_plan_access::topk_knobs(plan).stats;
   const int64_t max_runs = sample_max_runs(kn);
   const float2 sure_zc = sure_margin(kn);
   if (int r = setup_table(plan, ratio, max_runs, st, status, &tb)) return r;
@@ -2204,11 +2358,11 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       if (G.nsb) {
         if (residual_mode == 1)
           hipLaunchKernelGGL((topk_sample<1>), dim3(G.nsb), sblk, 0, s, x, residual, alpha, d_begins, d_sizes,
-                             (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin,
+                             (const uint32_t*)tb.smap, max_runs, tb.gh, tb.gz, tb.arrive, status, kk, tfirst, tlast, tkey,
                              hist, item_cnt, thi, fmap, tlo, fcount, fhist, G.sb0, sure_zc);
         else
           hipLaunchKernelGGL((topk_sample<0>), dim3(G.nsb), sblk, 0, s, x, residual, alpha, d_begins, d_sizes,
-                             (const uint32_t*)tb.smap, max_runs, tb.gh, tb.arrive, status, kk, tfirst, tlast, tbin,
+                             (const uint32_t*)tb.smap, max_runs, tb.gh, tb.gz, tb.arrive, status, kk, tfirst, tlast, tkey,
                              hist, item_cnt, thi, fmap, tlo, fcount, fhist, G.sb0, sure_zc);
       }
       if (gi == 0 && groups.size() > 1) {
@@ -2221,13 +2375,13 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       if (gi > 0) OMF_HIP(hipStreamWaitEvent(s, hsync->fused[(gi - 1) & 1], 0));
       const dim3 fgrid(G.nsub);
       if (residual_mode == 1)
-        hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt,
+        hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
                            item_cnt, cand, G.sub0);
       else if (residual_mode == 2)
-        hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt,
+        hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
                            item_cnt, cand, G.sub0);
       else
-        hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tbin, thi, sub_cnt,
+        hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
                            item_cnt, cand, G.sub0);
       if (groups.size() > 1) OMF_HIP(hipEventRecord(hsync->fused[gi & 1], s));
       // fast path: exact fine-bin histograms, bucket plan
@@ -2238,7 +2392,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       // memory; the bucket kernels are enqueued before the host waits for it (they do nothing
       // when the verdict is a fallback), so the GPU does not idle while the host reads it
       hipLaunchKernelGGL(topk_plan, dim3((unsigned)(G.t1 - G.t0)), sblk, 0, s, kk, fcount, fhist, bbase, fbucket,
-                         bstart, brec, bfill, kb2, flag, status, fse, dbg, tb.done, hsync->dev, seq, G.t0,
+                         bstart, brec, bfill, kb2, flag, status, fse, tkey, zcnt, dbg, tb.done, hsync->dev, seq, G.t0,
                          (uint32_t)nt);
       if (!forced) {
         hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo,
@@ -2253,11 +2407,24 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       OMF_HIP(hipEventRecord(hsync->join, hsync->side));
       OMF_HIP(hipStreamWaitEvent(st, hsync->join, 0));
     }
-    if (int rc = wait_status(hsync, seq, st, t_call)) return rc;
+    if (int rc = wait_status(hsync, seq, st, t_call, &stats)) return rc;
     uint32_t host_status[4];
     std::memcpy(host_status, hsync->pinned, 16);
-    if (kn.dbg & 4) fprintf(stderr, "omf_topk: redo %u overflow %u\n", host_status[1], host_status[2]);
-    if (!host_status[1] && !host_status[2] && !forced) return OMF_OK;
+    if (kn.dbg & 4)
+      fprintf(stderr, "omf_topk: zero fill %u redo %u overflow %u\n", host_status[0], host_status[1], host_status[2]);
+    ++stats.calls;
+    if (!host_status[1] && !host_status[2] && !forced) {
+      ++stats.fast;
+      if (host_status[0]) {  // zero mode: complete the short tensors with their lowest-index zeros
+        ++stats.zero_fill;
+        hipLaunchKernelGGL(topk_zero_fill, dim3((unsigned)tb.nzb), blk, 0, st, (const uint2*)tb.zmap, zcnt, kk, koff,
+                           d_begins, d_sizes, tfirst, items, sub_cnt, cand, tp, scale, rz, values, indices);
+        OMF_HIP(hipGetLastError());
+      }
+      return OMF_OK;
+    }
+    ++stats.fallback;
+    if (host_status[1]) ++stats.redo;
     // fallback (a redo, a fine bin over kBucketHalf keys, or forced): device-wide radix sort
     if (rz) hipLaunchKernelGGL(topk_restore, grid, blk, 0, st, cand, items, sub_cnt, d_begins, rz);
     auto scan_and_check = [&]() -> int {
@@ -2284,6 +2451,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     // magnitude bits alone yields (tensor, |t'| descending, index ascending)
     OMF_HIP(rocprim::radix_sort_keys(w + L.tmp, tmp_bytes, sorted, cand, (size_t)total, 0, kSortBits, st, false));
   } else {
+    ++stats.exact;
     if (residual_mode == 0)
       hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
     else if (residual_mode == 1)

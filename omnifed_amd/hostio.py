@@ -18,9 +18,9 @@ This module overlaps the first two with the third:
   messages are read.
 * ``device_to_host``: a decoded arena into an ordinary (pageable) CPU tensor — the reference's
   CPU placement — through a ring of pinned chunks, each drained by a worker thread's memmove
-  while the next chunks' DMAs run (the first touch of the destination's fresh pages is spread
-  over the workers too): 56 ms for Llama-400M's 1.6 GB against 126 ms for a plain ``.cpu()``
-  (``scripts/exp/d2h_probe.py``).
+  while the next chunks' DMAs run, into pooled pages the next round reuses: 56 ms for
+  Llama-400M's 1.6 GB into fresh memory against 126 ms for a plain ``.cpu()``.  Page-locked
+  result arenas (one DMA each) are opt-in and bounded (``set_pinned_arenas``).
 
 Nothing here changes bytes: the payload is the encoder's, byte for byte.
 """
@@ -272,15 +272,46 @@ class _HostLease:
         self.pool._returned.append(self.mem)  # list.append is atomic: no lock in a finaliser
 
 
+def _register(ptr: int, nbytes: int) -> bool:
+    """Page-lock host memory in place (hipHostRegister through torch's runtime binding)."""
+    try:
+        return int(torch._C._cudart.cudaHostRegister(ptr, nbytes, 0)) == 0
+    except Exception:  # pragma: no cover - no HIP runtime
+        return False
+
+
+def _unregister(ptr: int) -> None:
+    try:
+        torch._C._cudart.cudaHostUnregister(ptr)
+    except Exception:  # pragma: no cover
+        pass
+
+
+def _pin_budget_from_env() -> int:
+    """``OMF_PIN_HOST_ARENAS``: unset or 0 = no page-locked arenas (the default); 1 = up to 4 GiB;
+    any other number = that many MiB."""
+    v = os.environ.get("OMF_PIN_HOST_ARENAS", "0").strip()
+    if not v.isdigit() or int(v) == 0:
+        return 0
+    return (4 << 30) if int(v) == 1 else int(v) << 20
+
+
 class HostArenaPool:
-    """Pageable host buffers for decoded arenas returned to the caller (the CPU placement).
+    """Host buffers for decoded arenas returned to the caller (the CPU placement).
 
     A fresh 1.6 GB ``torch.empty`` every round is mmap'd, its 400 K pages faulted in by the copy and
     unmapped again when the caller drops the tensors (glibc serves blocks above 32 MiB by mmap, and
     ``M_MMAP_THRESHOLD`` cannot go higher): most of the CPU placement's cost.  Here the memory of a
     dropped arena goes back to a pool and the next round's arena reuses its pages.  The tensors
     handed out are ordinary, writable CPU tensors (numpy-backed storage); the pool keeps at most
-    ``max_bytes`` of free buffers (the rest goes back to the OS)."""
+    ``max_bytes`` of free buffers (the rest goes back to the OS).
+
+    ``pinned``: the buffers are page-locked in place (hipHostRegister on numpy memory), so a DMA
+    lands in them directly — opt-in (``OMF_PIN_HOST_ARENAS`` / ``set_pinned_arenas``), because
+    page-locking gigabytes on a PS host is a resource-policy change the reference never makes.
+    Every page-locked byte, handed out or pooled, counts against ``max_bytes``: ``empty`` returns
+    None when a new buffer would exceed it (the caller then takes the pageable path), and a buffer
+    trimmed from the pool is unregistered before its memory goes back to the OS."""
 
     GRAIN = 64 << 20      # sizes rounded up to this above it (to 1 MiB below)
     MIN_BYTES = 1 << 20   # smaller arenas are not pooled
@@ -291,9 +322,15 @@ class HostArenaPool:
         self._np = np
         self.max_bytes = int(max_bytes)
         self.pinned = bool(pinned)
+        self.live_bytes = 0  # pinned pools: page-locked bytes, handed out or free
         self._free: List[object] = []
         self._returned: List[object] = []
         self._lock = threading.Lock()
+
+    def _release(self, m) -> None:
+        if self.pinned:
+            _unregister(m.ctypes.data)
+            self.live_bytes -= _nbytes(m)
 
     def _drain(self) -> None:
         while self._returned:
@@ -304,22 +341,38 @@ class HostArenaPool:
             if total + _nbytes(m) <= self.max_bytes:
                 kept.append(m)
                 total += _nbytes(m)
+            else:
+                self._release(m)
         self._free = kept
 
-    def empty(self, nbytes: int) -> torch.Tensor:
-        """An uninitialised uint8 CPU tensor of ``nbytes`` backed by pooled memory."""
+    def set_max_bytes(self, max_bytes: int) -> None:
+        with self._lock:
+            self.max_bytes = int(max_bytes)
+            self._drain()
+
+    def empty(self, nbytes: int) -> Optional[torch.Tensor]:
+        """An uninitialised uint8 CPU tensor of ``nbytes`` backed by pooled memory (a pinned pool:
+        None when its budget cannot hold a new buffer)."""
         nbytes = int(nbytes)
-        if nbytes < self.MIN_BYTES:  # small: malloc's own free lists serve it
+        if nbytes < self.MIN_BYTES and not self.pinned:  # small: malloc's own free lists serve it
             return torch.empty(nbytes, dtype=torch.uint8)
         with self._lock:
             self._drain()
             pick = next((i for i, m in enumerate(self._free) if nbytes <= _nbytes(m) <= 2 * nbytes + self.GRAIN), None)
             mem = self._free.pop(pick) if pick is not None else None
-        if mem is None:
-            grain = self.GRAIN if nbytes >= self.GRAIN else self.MIN_BYTES
-            size = -(-nbytes // grain) * grain
-            mem = (torch.empty(size, dtype=torch.uint8, pin_memory=True) if self.pinned
-                   else self._np.empty(size, dtype=self._np.uint8))
+            if mem is None:
+                grain = self.GRAIN if nbytes >= self.GRAIN else self.MIN_BYTES
+                size = -(-nbytes // grain) * grain
+                if self.pinned:
+                    while self._free and self.live_bytes + size > self.max_bytes:  # make room: drop free ones
+                        self._release(self._free.pop())
+                    if self.live_bytes + size > self.max_bytes:
+                        return None
+                mem = self._np.empty(size, dtype=self._np.uint8)
+                if self.pinned:
+                    if not _register(mem.ctypes.data, size):
+                        return None
+                    self.live_bytes += size
         return torch.from_numpy(self._np.asarray(_HostLease(mem, nbytes, self)))
 
     def free_bytes(self) -> int:
@@ -329,7 +382,23 @@ class HostArenaPool:
 
 
 HOST_ARENAS = HostArenaPool()
-PINNED_ARENAS = HostArenaPool(pinned=True)  # page-locked: the DMA lands in them directly
+# page-locked arenas: off unless OMF_PIN_HOST_ARENAS / set_pinned_arenas gives them a budget
+PINNED_ARENAS = HostArenaPool(max_bytes=_pin_budget_from_env(), pinned=True)
+
+
+def set_pinned_arenas(max_bytes: int) -> None:
+    """Budget of page-locked decoded arenas (0 = off, the default): the CPU
+    placement's results then land by one DMA each instead of through the pinned chunk ring."""
+    PINNED_ARENAS.set_max_bytes(max(0, int(max_bytes)))
+
+
+def pinned_arena(nbytes: int) -> Optional[torch.Tensor]:
+    """A page-locked pooled arena of ``nbytes`` if the budget allows, else None."""
+    if PINNED_ARENAS.max_bytes <= 0:
+        return None
+    return PINNED_ARENAS.empty(nbytes)
+
+
 RING_CHUNK_BYTES = 8 << 20
 
 
@@ -417,20 +486,23 @@ class D2HRing:
 def device_to_host(src: torch.Tensor, stream=None, key: str = "d2h", limit: int = RING_CHUNK_BYTES,
                    slots: Optional[int] = None, pool_memory: bool = True) -> torch.Tensor:
     """A CPU copy of the device tensor ``src`` (1-D, same dtype), queued on ``stream`` (default the
-    current stream of ``src``'s device) behind the work already there: with ``pool_memory`` into
-    a pooled page-locked arena (``PINNED_ARENAS``: one DMA at the link's rate, the pages reused
-    round after round), else into a fresh pageable tensor through a ``D2HRing`` (``slots`` pinned
-    chunks of ``limit`` bytes).  Returns when every byte has landed."""
+    current stream of ``src``'s device) behind the work already there.  Into a page-locked pooled
+    arena when ``set_pinned_arenas`` / ``OMF_PIN_HOST_ARENAS`` gave them a budget that holds it
+    (one DMA at the link's rate); otherwise through a ``D2HRing`` (``slots`` pinned chunks of
+    ``limit`` bytes) into pageable memory — pooled (``HOST_ARENAS``: the pages reused round after
+    round) with ``pool_memory``, else a fresh tensor.  Returns when every byte has landed."""
     if stream is None:
         stream = torch.cuda.current_stream(src.device)
     raw = src.reshape(-1).view(torch.uint8)
-    if pool_memory and raw.numel() >= HostArenaPool.MIN_BYTES:  # pooled page-locked arena: one DMA
-        out = PINNED_ARENAS.empty(raw.numel())
+    big = raw.numel() >= HostArenaPool.MIN_BYTES
+    out = pinned_arena(raw.numel()) if pool_memory and big else None
+    if out is not None:  # page-locked: one DMA
         with torch.cuda.stream(stream):
             out.copy_(raw, non_blocking=True)
         stream.synchronize()
         return out.view(src.dtype)
-    out = torch.empty(raw.numel(), dtype=torch.uint8).view(src.dtype)
+    out = (HOST_ARENAS.empty(raw.numel()) if pool_memory and big else torch.empty(raw.numel(), dtype=torch.uint8))
+    out = out.view(src.dtype)
     if raw.numel() == 0:
         return out
     with D2HRing(out.data_ptr(), stream, key, limit, slots) as ring:

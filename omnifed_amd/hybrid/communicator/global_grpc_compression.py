@@ -68,9 +68,9 @@ def _host_memory_policy() -> bool:
             logging.getLogger("omnifed_amd").info(
                 "omnifed_amd: glibc malloc now keeps freed wire-message memory for reuse (mmap threshold 32 MiB, "
                 "trim threshold 1 GiB per arena; resident size may stay ~one round's payload higher), and "
-                "decoded arenas returned on the CPU reuse pooled pages (hostio.HOST_ARENAS, up to 8 GiB kept). "
-                "OMF_RETAIN_HOST_MEMORY=0 leaves glibc's defaults alone and allocates every arena afresh "
-                "(INTEGRATION.md §3c).")
+                "decoded arenas returned on the CPU reuse pooled pageable pages (hostio.HOST_ARENAS, up to 8 GiB "
+                "kept; page-locked only if OMF_PIN_HOST_ARENAS gives them a budget). OMF_RETAIN_HOST_MEMORY=0 "
+                "leaves glibc's defaults alone and allocates every arena afresh (INTEGRATION.md §3c).")
     return _HOST_POLICY
 
 
@@ -576,9 +576,10 @@ def _decode_qsgd_to_host(layers, dev: torch.device):
     event recorded, and a second stream copies those decoded elements into the host arena while
     the next chunk is read out of its messages — the payload in and the fp32 out overlap on the
     full-duplex link.  Same bytes as
-    one decode followed by one copy.  Under the host-memory policy the arena is a pooled
-    page-locked one (hostio.PINNED_ARENAS: each chunk is one DMA); otherwise a fresh pageable
-    tensor fed through a hostio.D2HRing."""
+    one decode followed by one copy.  The arena is a page-locked pooled one when the opt-in budget
+    of hostio.set_pinned_arenas holds it (each chunk is one DMA); otherwise pageable memory —
+    pooled under the host-memory policy (hostio.HOST_ARENAS), else fresh — fed through a
+    hostio.D2HRing."""
     width, level = layers[0].width, layers[0].level
     sizes = [max(int(np.prod(tuple(L.original_shape))), 1) for L in layers]
     plan = codec.Plan.get(sizes, device=dev)
@@ -592,8 +593,10 @@ def _decode_qsgd_to_host(layers, dev: torch.device):
     qd = torch.empty(N, dtype=_QSGD_TORCH_DTYPES[width], device=dev)
     y = torch.empty(N, dtype=torch.float32, device=dev)
     yb = y.view(torch.uint8)
-    pinned = bool(_HOST_POLICY)
-    ob = hostio.PINNED_ARENAS.empty(4 * N) if pinned else torch.empty(4 * N, dtype=torch.uint8)
+    ob = hostio.pinned_arena(4 * N) if _HOST_POLICY else None
+    pinned = ob is not None
+    if ob is None:
+        ob = hostio.HOST_ARENAS.empty(4 * N) if _HOST_POLICY else torch.empty(4 * N, dtype=torch.uint8)
     out = ob.view(torch.float32)
     blk = codec.DECODE_BLOCK
     side = torch.cuda.Stream(dev)

@@ -7,7 +7,9 @@ decode_updates_dict : LayerStates -> pinned staging (worker threads) -> chunked 
                       decode call (device="cuda": stays on the GPU; default: CPU tensors)
 decode_updates_into : client downlink straight into the model's device tensors
 accumulate_layers   : the PS's SendUpdate decode-accumulate of one client (DeviceAggregator)
-apply_and_encode    : the PS's GetUpdatedModel: average + re-encode + LayerStates
+apply_and_encode    : the PS's GetUpdatedModel: average + re-encode + LayerStates (Top-K: the
+                      sparse average of two clients' Top-K decodes, the reference's steady state;
+                      the dense accumulator is timed beside it)
 host round trip     : host fp32 tensors in -> LayerStates -> host fp32 tensors out (the rate
                       including the H<->D copies, north_star)
 
@@ -65,14 +67,42 @@ def leg(comp, tag):
     r["decode_updates_dict_cpu_ms"] = tm(lambda: decode_updates_dict(layers), reps=3, warm=1)
     agg = DeviceAggregator(named, device=dev)
     r["agg_accumulate_layers_ms"] = tm(lambda: agg.accumulate_layers(layers, number_samples=1))
-    # GetUpdatedModel: the server's compressor re-encodes the average (apply_and_encode) of a
-    # dense accumulator (the model parameters / the average of many clients' updates; one sparse
-    # Top-K update alone leaves 99 % zeros, whose ties at 0 send a Top-K re-encode to the exact path)
+    # GetUpdatedModel: the server's compressor re-encodes the average (apply_and_encode).  A dense
+    # accumulator (QSGD decodes are dense; a Top-K average over many clients' updates):
     srv = build_global_compressor(enabled=True, scheme=tag, bit_width=4, compress_ratio=0.01, device=dev)
     agg.acc.copy_(torch.randn(agg.acc.numel(), device=dev, generator=g) * 4e-2)
     agg.total_samples = 40
-    r["ps_apply_and_encode_ms"] = tm(lambda: agg.apply_and_encode(srv, total_samples=40))
+    r["ps_apply_and_encode_dense_ms"] = tm(lambda: agg.apply_and_encode(srv, total_samples=40))
+    r["ps_apply_and_encode_ms"] = r["ps_apply_and_encode_dense_ms"]
     del agg
+    if tag == "topk":
+        # The reference's steady state for Top-K (scheme: topk, aggregate_payload: params,
+        # conf/base.yaml:194-198): the PS sums the clients' zero-filled Top-K decodes
+        # (global_grpc_server.py:147-153), divides (:155-171) and re-encodes that SPARSE average per
+        # request (:213-234) — at most C k non-zeros per tensor.  Two clients with error feedback on
+        # (their second call's selections), overlapping (client 1 = client 0's gradient + 5 % noise)
+        # and disjoint (independent gradients) selections.
+        plan_t = codec.Plan.get([t.numel() for t in upd.values()], device=dev)
+        for label, noise in (("overlap", 0.05), ("disjoint", None)):
+            agg2 = DeviceAggregator(named, device=dev)
+            for c in range(2):
+                cc = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+                if noise is None and c:
+                    u = {n: torch.randn(t.shape, device=dev, generator=g) * 1e-3 for n, t in upd.items()}
+                else:
+                    u = {n: t + (noise * c) * torch.randn(t.shape, device=dev, generator=g) * 1e-3
+                         for n, t in upd.items()}
+                encode_updates_dict(u, cc)
+                agg2.accumulate_layers(encode_updates_dict(u, cc), number_samples=1)
+                del u, cc
+            nnz = int((agg2.acc != 0).sum())
+            srv2 = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+            plan_t.topk_stats(reset=True)
+            r[f"ps_apply_and_encode_sparse_{label}_ms"] = tm(lambda: agg2.apply_and_encode(srv2, total_samples=2))
+            r[f"sparse_{label}_nnz_per_k"] = round(nnz / sum(plan_t.topk_ks(0.01)), 3)
+            r[f"sparse_{label}_topk_stats"] = plan_t.topk_stats(reset=True)
+            del agg2, srv2
+        r["ps_apply_and_encode_ms"] = r["ps_apply_and_encode_sparse_overlap_ms"]
     # host round trip: host fp32 tensors in, LayerStates, host fp32 tensors out
     host = {n: t.cpu().pin_memory() for n, t in upd.items()}
     r["host_roundtrip_ms"] = tm(lambda: decode_updates_dict(encode_updates_dict(host, comp)), reps=3, warm=1)

@@ -7,6 +7,11 @@ with alpha = 3, and of Llama-150M at s = 4 — is compared with ``oracle.qsgd_qu
 (qsgd.py:36-64 restated) given the GPU's norm and ``oracle.philox_uniforms``: payload bytes
 equal, and the decode equal to ``oracle.qsgd_dequantize``.  The bracketed encoder's finish
 pass (the undecided quads it lists and fixes) must have run: spec_stats()["listed"] > 0.
+
+Round 5 adds the int32 wire (``bit_width: 8``, the reference's default, conf/base.yaml:200;
+qsgd.py:18-21 stores levels > 127 as int32): on these bracketed plans an s = 8 encode takes the
+ring encoder (omf_qsgd.hip encode_impl, ``wide_ring``), asserted through the plan's record of
+the encoder it launched; Llama-400M (alpha 1) and Llama-150M (alpha 2), every tensor.
 """
 
 from concurrent.futures import ThreadPoolExecutor
@@ -30,7 +35,8 @@ def _threads() -> int:
         return 8
 
 
-@pytest.mark.parametrize("cfg,s,alpha", [("llama400m", 4, 1.0), ("llama400m", 3, 3.0), ("llama150m", 4, 1.0)])
+@pytest.mark.parametrize("cfg,s,alpha", [("llama400m", 4, 1.0), ("llama400m", 3, 3.0), ("llama150m", 4, 1.0),
+                                         ("llama400m", 8, 1.0), ("llama150m", 8, 2.0)])
 def test_headline_arena_every_tensor_equals_oracle(gpu, cfg, s, alpha):
     named = shapes.model_shapes(cfg)
     sizes = [shapes.numel(sh) for _, sh in named]
@@ -41,11 +47,17 @@ def test_headline_arena_every_tensor_equals_oracle(gpu, cfg, s, alpha):
     x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
     seed, off = 0x5EED, 7
     q, norms = plan.qsgd_encode(x, s, alpha=alpha, seed=seed, offset=off)
-    stats = plan.spec_stats()
+    width = codec.storage_width(2**s)
+    if s <= 4:
+        assert plan.last_encoder == "bracket"
+        stats = plan.spec_stats()
+        assert stats["listed"] > 0, stats  # the finish pass fixed undecided quads
+    else:
+        assert width == 32 and q.dtype == torch.int32
+        assert plan.last_encoder == "ring"  # the int32 wire of a bracketed plan
     plan.check()
-    assert stats["listed"] > 0, stats  # the finish pass fixed undecided quads
     L = 2**s
-    y = plan.qsgd_decode(q, 8, L, norms)
+    y = plan.qsgd_decode(q, width, L, norms)
     xh = x.cpu().numpy()
     qh = q.cpu().numpy()
     yh = y.cpu().numpy()

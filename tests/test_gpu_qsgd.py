@@ -303,8 +303,9 @@ def test_full_config_parity_mt_stream(gpu, cfg, bits):
 @pytest.mark.parametrize("cfg,s", [("llama400m", 4), ("llama150m", 4), ("llama150m", 8)])
 def test_full_config_properties(gpu, cfg, s):
     """Full-size arenas: size-independent properties + exact oracle spot checks on 3 tensors.
-    llama150m s=4 is the bench's other_configs arena on the bracketed encoder (s=8 takes the
-    two-pass encoder)."""
+    llama150m s=4 is the bench's other_configs arena on the bracketed encoder; s=8 (the int32
+    wire) takes the ring encoder on these bracketed plans — every tensor of it is pinned to the
+    oracle in test_gpu_headline_pin.py."""
     named = shapes.model_shapes(cfg)
     sizes = [shapes.numel(sh) for _, sh in named]
     plan = codec.Plan.get(sizes, device=gpu)

@@ -225,13 +225,62 @@ def test_qsgd_cpu_placement_pipeline_equals_device_decode(gpu, bits):
 
 
 def test_pinned_arena_pool_tensors_are_page_locked(gpu):
-    """The pooled page-locked arenas the CPU placement returns are seen by torch as pinned, so the
-    device-to-host copies into them are asynchronous DMAs."""
+    """Page-locked arenas are opt-in and bounded (round 5): the product pool has no budget unless
+    OMF_PIN_HOST_ARENAS gives it one; a pinned pool's tensors are seen by torch as pinned (the
+    copies into them are asynchronous DMAs); every page-locked byte, handed out or free, counts
+    against the budget (a request beyond it gets None); a trimmed buffer is unregistered."""
+    import gc
+    import os
+
     from omnifed_amd import hostio
 
-    t = hostio.PINNED_ARENAS.empty(4 << 20)
-    assert t.is_pinned()
+    if not os.environ.get("OMF_PIN_HOST_ARENAS"):
+        assert hostio.PINNED_ARENAS.max_bytes == 0 and hostio.pinned_arena(4 << 20) is None
+    MiB = 1 << 20
+    P = hostio.HostArenaPool(max_bytes=8 * MiB, pinned=True)
+    t = P.empty(4 * MiB)
+    assert t.is_pinned() and P.live_bytes == 4 * MiB
     src = torch.arange(1 << 20, device=gpu, dtype=torch.float32)
     t.view(torch.float32).copy_(src, non_blocking=True)
     torch.cuda.synchronize()
     assert torch.equal(t.view(torch.float32), src.cpu())
+    u = P.empty(4 * MiB)
+    assert u is not None and P.live_bytes == 8 * MiB
+    assert P.empty(2 * MiB) is None  # over the budget: the caller takes the pageable path
+    del u
+    gc.collect()
+    w = P.empty(2 * MiB)  # the free 4 MiB buffer serves it (no new page-locked memory)
+    assert w is not None and P.live_bytes == 8 * MiB
+    del t, w
+    gc.collect()
+    P.set_max_bytes(0)  # trims every free buffer: unregistered, memory released
+    assert P.free_bytes() == 0 and P.live_bytes == 0
+
+
+def test_cpu_placement_returns_pageable_memory_by_default(gpu):
+    """decode_updates_dict's CPU placement hands the caller pageable (pooled) memory unless pinned
+    arenas were asked for; with a budget (hostio.set_pinned_arenas) the same bytes come back
+    page-locked."""
+    import os
+
+    from omnifed_amd import hostio
+    from omnifed_amd.hybrid.communicator.global_grpc_compression import (
+        build_global_compressor, decode_updates_dict, encode_updates_dict)
+
+    if os.environ.get("OMF_PIN_HOST_ARENAS"):
+        pytest.skip("pinned arenas enabled by the environment")
+    g = torch.Generator(device=gpu).manual_seed(5)
+    upd = {f"w{i}": torch.randn(n, device=gpu, generator=g) for i, n in enumerate((1 << 20, 700_001, 3000))}
+    for scheme in ("qsgd", "topk"):
+        comp = build_global_compressor(enabled=True, scheme=scheme, bit_width=4, compress_ratio=0.05, device=gpu)
+        layers = encode_updates_dict(upd, comp)
+        a = decode_updates_dict(layers)
+        assert not any(t.is_pinned() for t in a.values()), scheme
+        hostio.set_pinned_arenas(256 << 20)
+        try:
+            b = decode_updates_dict(layers)
+            assert a["w0"].numel() * 4 < hostio.HostArenaPool.MIN_BYTES or b["w0"].is_pinned(), scheme
+        finally:
+            hostio.set_pinned_arenas(0)
+        for n in upd:
+            assert a[n].numpy().tobytes() == b[n].numpy().tobytes(), (scheme, n)
