@@ -261,11 +261,12 @@ def pmc_traffic(kernel, config, bits):
             tj = json.load(f)
     except (OSError, ValueError):
         return None, "no PMC file"
-    if tj.get("config") != config or tj.get("bits") != bits:
-        return None, "PMC file is for another config"
+    run = tj.get("runs", {}).get(f"{config}/s{bits}")
+    if run is None:
+        return None, f"PMC file has no {config}/s{bits} run"
     if tj.get("source_sha") != source_digest():
         return None, f"PMC file measured on other kernel sources (commit {tj.get('commit')}, {tj.get('date')})"
-    return tj.get("bytes_per_launch", {}).get(kernel), f"rocprofv3 PMC, commit {tj.get('commit')}, {tj.get('date')}"
+    return run.get("bytes_per_launch", {}).get(kernel), f"rocprofv3 PMC, commit {tj.get('commit')}, {tj.get('date')}"
 
 
 def event_ms(torch, st, fn, reps):

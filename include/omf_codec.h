@@ -213,6 +213,25 @@ int omf_ps_apply_encode(omf_plan* plan, const float* acc, float divisor, float* 
                         const float* u, uint64_t seed, uint64_t offset, void* q_out, float* norm_out, void* stream);
 
 /*
+ * The PS round's last step in one pass: the last arriving client's decode-accumulate
+ * (SendUpdate: acc[name] += update, global_grpc_server.py:108-111, 147-153), the average
+ * (_apply_model_updates, :155-171) and its downlink encode (_send_current_model, :213-234):
+ *   sum_i   = fl32(acc_i + fl32(fl32(norm_in[t] * q_in_i) / levels_in))   (omf_qsgd_decode's accumulate)
+ *   avg_out = sum / divisor,  q_out / norm_out = the QSGD encode of avg_out (as omf_ps_apply_encode)
+ * acc_out: where sum is stored (acc itself, a disjoint arena, or NULL: not stored — the caller
+ * no longer needs the accumulator).  q_in: the last client's payload arena (width_in 8 or 32,
+ * LayerState.width; levels_in = LayerState.level), norm_in its per-tensor norms (0 for a tensor
+ * absent from its message).  avg_out disjoint from acc and acc_out.  Bracketed plans (bit_width
+ * 1-4, on-device draws) read acc and q_in once in the encoder's pass (10 B per element at s = 4
+ * instead of 18 for decode-accumulate then omf_ps_apply_encode); other plans run those two.
+ * Bytes equal to omf_qsgd_decode(accumulate=1) followed by omf_ps_apply_encode.
+ */
+int omf_ps_accumulate_apply_encode(omf_plan* plan, const float* acc, const void* q_in, int32_t width_in,
+                                   int32_t levels_in, const float* norm_in, float* acc_out, float divisor,
+                                   float* avg_out, int32_t bit_width, const float* u, uint64_t seed, uint64_t offset,
+                                   void* q_out, float* norm_out, void* stream);
+
+/*
  * QSGD decode, all tensors in one launch.
  * Replaces QSGDQuantCompression.decompress_quantized (qsgd.py:84-96) as called by
  * _decode_qsgd_layer (global_grpc_compression.py:163-182), and — with

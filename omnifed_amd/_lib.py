@@ -54,6 +54,8 @@ SIGNATURES = {
     "omf_qsgd_norms_ex": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_i32, _c_p, _c_p]),
     "omf_ps_apply_encode": (ctypes.c_int, [_c_p, _c_p, _c_f32, _c_p, _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p,
                                            _c_p]),
+    "omf_ps_accumulate_apply_encode": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_f32, _c_p,
+                                                      _c_i32, _c_p, _c_u64, _c_u64, _c_p, _c_p, _c_p]),
     "omf_qsgd_decode": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_p]),
     "omf_qsgd_decode_range": (ctypes.c_int, [_c_p, _c_p, _c_i32, _c_i32, _c_p, _c_p, _c_i32, _c_i64, _c_i64, _c_p]),
     "omf_div_f32": (ctypes.c_int, [_c_p, _c_i64, _c_f32, _c_p]),

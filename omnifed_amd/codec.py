@@ -330,6 +330,49 @@ class Plan:
                   "omf_ps_apply_encode")
         return avg_out, q_out, norm_out
 
+    def ps_accumulate_apply_encode(self, acc: torch.Tensor, q_in: torch.Tensor, width_in: int, levels_in: int,
+                                   norm_in: torch.Tensor, divisor: float, bit_width: int,
+                                   acc_out: Optional[torch.Tensor] = None, avg_out: Optional[torch.Tensor] = None,
+                                   u: Optional[torch.Tensor] = None, seed: int = 0, offset: int = 0,
+                                   q_out: Optional[torch.Tensor] = None, norm_out: Optional[torch.Tensor] = None,
+                                   stream: Optional[int] = None):
+        """The PS round's last step (omf_ps_accumulate_apply_encode): ``sum = acc + decode(q_in)`` (the
+        last client's payload), ``avg = sum / divisor`` and its QSGD payload, acc and q_in read once.
+        ``acc_out``: where ``sum`` is stored (``acc`` itself, another arena, or None: not stored).
+        Returns ``(avg, q, norms)``."""
+        s = int(bit_width)
+        if not 0 <= s <= 30:
+            raise ValueError("bit_width must be in [0, 30]")
+        if not float(divisor) != 0.0:
+            raise ValueError("divisor must be non-zero")
+        width = storage_width(2 ** s)
+        qdt = torch.int8 if width == 8 else torch.int32
+        dev = self.device
+        wi = int(width_in)
+        _need(acc, "acc", torch.float32, dev, self.arena_end, 16)
+        _need(q_in, "q_in", torch.int8 if wi == 8 else torch.int32, dev, self.arena_end, 4 if wi == 8 else 16)
+        _need(norm_in, "norm_in", torch.float32, dev, self.nt, 4)
+        if acc_out is not None:
+            _need(acc_out, "acc_out", torch.float32, dev, self.arena_end, 16)
+        if avg_out is None:
+            avg_out = torch.empty(self.arena_end, dtype=torch.float32, device=dev)
+        _need(avg_out, "avg_out", torch.float32, dev, self.arena_end, 16)
+        if q_out is None:
+            q_out = torch.empty(self.payload_elems(width), dtype=qdt, device=dev)
+        _need(q_out, "q_out", qdt, dev, self.payload_elems(width), 4 if width == 8 else 16)
+        if norm_out is None:
+            norm_out = torch.empty(self.nt, dtype=torch.float32, device=dev)
+        _need(norm_out, "norm_out", torch.float32, dev, self.nt, 4)
+        if u is not None:
+            _need(u, "u", torch.float32, dev, self.arena_end, 16)
+        st = stream if stream is not None else _stream(dev)
+        with self._lock:
+            check(lib().omf_ps_accumulate_apply_encode(
+                self._h, _ptr(acc), _ptr(q_in), wi, int(levels_in), _ptr(norm_in), _ptr(acc_out), float(divisor),
+                _ptr(avg_out), s, _ptr(u), int(seed) & 0xFFFFFFFFFFFFFFFF, int(offset) & 0xFFFFFFFFFFFFFFFF,
+                _ptr(q_out), _ptr(norm_out), ctypes.c_void_p(st)), "omf_ps_accumulate_apply_encode")
+        return avg_out, q_out, norm_out
+
     def qsgd_norms(self, x: torch.Tensor, alpha: float = 1.0, norm_out: Optional[torch.Tensor] = None,
                    stream: Optional[int] = None, value_format: int = 0) -> torch.Tensor:
         dev = self.device
@@ -517,7 +560,8 @@ class Plan:
         """(ctypes int64 array, total) of a per-tensor count vector (cached: a message layout
         repeats every round)."""
         key = tuple(int(c) for c in counts)
-        c = self._counts_cache.get(key)
+        with self._lock:  # plans are shared by threads (gRPC workers, a client and the PS)
+            c = self._counts_cache.get(key)
         if c is None:
             if len(key) != self.nt:
                 raise ValueError(f"counts: {len(key)} entries, plan has {self.nt} tensors")
@@ -525,9 +569,11 @@ class Plan:
             need = int(lib().omf_topk_decode_counts_workspace_bytes(self._h, arr))
             if need == 0:
                 raise ValueError("counts must satisfy 0 <= counts[t] <= sizes[t]")
-            if len(self._counts_cache) >= 16:
-                self._counts_cache.pop(next(iter(self._counts_cache)))
-            c = self._counts_cache[key] = (arr, sum(key), need)
+            c = (arr, sum(key), need)
+            with self._lock:
+                while len(self._counts_cache) >= 16:
+                    self._counts_cache.pop(next(iter(self._counts_cache)))
+                self._counts_cache[key] = c
         return c
 
     def topk_check_indices(self, counts: Sequence[int], indices: torch.Tensor,

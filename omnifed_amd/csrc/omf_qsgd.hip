@@ -459,7 +459,68 @@ struct SpecArgs {
   float* xout;
   uint32_t epoch;          // per-launch tag (never 0)
   int64_t nblocks;
+  // Fused last-client decode-accumulate (omf_ps_accumulate_apply_encode; aq == NULL: none): before
+  // the divide, x := fl32(x + fl32(fl32(anorm[t] * q) / alevels)) — the decoder's accumulate, bit
+  // for bit (ainv = 2^-s for a power-of-two level count, else 0) — stored to aout when non-NULL.
+  const void* aq;
+  const float* anorm;
+  float* aout;
+  float alevels, ainv;
+  int32_t awidth;          // 8 or 32: the last client's payload (LayerState.width)
 };
+
+// The last client's payload of one float4 row (AW = 1: int8, AW = 4: int32), loaded beside x.
+template <int AW, bool FULL>
+__device__ __forceinline__ int4 acc_load(const void* q, int64_t e, int64_t end) {
+  if (AW == 1) {
+    const int8_t* q8 = static_cast<const int8_t*>(q);
+    if (FULL || e + 4 <= end)
+      return make_int4(__builtin_nontemporal_load(reinterpret_cast<const int32_t*>(q8 + e)), 0, 0, 0);
+    uint32_t w = 0;
+    for (int c = 0; c < 3; ++c)
+      if (e + c < end) w |= (uint32_t)(uint8_t)q8[e + c] << (8 * c);
+    return make_int4((int32_t)w, 0, 0, 0);
+  }
+  const int32_t* q32 = static_cast<const int32_t*>(q);
+  if (FULL || e + 4 <= end) {
+    const i32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(q32 + e));
+    return make_int4(t[0], t[1], t[2], t[3]);
+  }
+  int4 r = make_int4(0, 0, 0, 0);
+  if (e < end) r.x = q32[e];
+  if (e + 1 < end) r.y = q32[e + 1];
+  if (e + 2 < end) r.z = q32[e + 2];
+  return r;
+}
+
+// v + decode(raw): the decoder's arithmetic (qsgd_decode_arena with accumulate).
+template <int AW>
+__device__ __forceinline__ float4 acc_add4(float4 v, int4 raw, float norm, float alevels, float ainv) {
+  int32_t qi[4];
+  if (AW == 1) {
+    qi[0] = (int32_t)(int8_t)(raw.x & 0xff);
+    qi[1] = (int32_t)(int8_t)((raw.x >> 8) & 0xff);
+    qi[2] = (int32_t)(int8_t)((raw.x >> 16) & 0xff);
+    qi[3] = (int32_t)(int8_t)((raw.x >> 24) & 0xff);
+  } else {
+    qi[0] = raw.x; qi[1] = raw.y; qi[2] = raw.z; qi[3] = raw.w;
+  }
+  float y[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const float nq = __fmul_rn(norm, (float)qi[c]);
+    y[c] = ainv != 0.0f ? __fmul_rn(nq, ainv) : nq / alevels;
+  }
+  return make_float4(__fadd_rn(v.x, y[0]), __fadd_rn(v.y, y[1]), __fadd_rn(v.z, y[2]), __fadd_rn(v.w, y[3]));
+}
+
+// The bracket's view of one float4 of x at arena element e: x (+ the fused last client's decode).
+__device__ __forceinline__ float4 br_value(const SpecArgs& a, float4 v, int64_t e, int64_t end, int32_t t) {
+  if (!a.aq) return v;
+  const float nrm = a.anorm[t];
+  if (a.awidth == 32) return acc_add4<4>(v, acc_load<4, false>(a.aq, e, end), nrm, a.alevels, a.ainv);
+  return acc_add4<1>(v, acc_load<1, false>(a.aq, e, end), nrm, a.alevels, a.ainv);
+}
 
 __device__ __forceinline__ uint32_t spec_hash(uint32_t a, uint32_t b) {
   uint32_t h = a * 0x9E3779B1u ^ (b + 0x7F4A7C15u) * 0x85EBCA77u;
@@ -540,6 +601,13 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
         }
       }
     }
+    if (a.aq) {  // the fused PS step's last client, added before the divide
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int64_t e = 4 * ((int64_t)i * kBrThreads + threadIdx.x);
+        if (e < n) v[i] = br_value(a, v[i], tb + e, tb + n, t);
+      }
+    }
     float acc = 0.0f;
 #pragma unroll
     for (int i = 0; i < PER; ++i) acc = sq4(spec_prologue(v[i], alpha, a.divisor, a.e.fmt), acc);
@@ -561,6 +629,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
       const int64_t pos = (lo + (int64_t)(spec_hash((uint32_t)r, (uint32_t)t) % (uint32_t)(len - (kSpecRun - 1)))) &
                           ~(int64_t)3;
       v[i] = *reinterpret_cast<const float4*>(x + pos + 4 * j);
+      if (a.aq) v[i] = br_value(a, v[i], tb + pos + 4 * j, tb + n, t);  // the fused PS step's last client
     }
 #pragma unroll
     for (int i = 0; i < PASSES; ++i) {
@@ -671,13 +740,19 @@ __device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t 
 // One block's pass: loads issued first, the Philox draws (independent of x) computed while
 // they are in flight, then the partial, the levels and the undecided list.  FULL: a whole
 // 4 Ki block (straight-line code, no bounds checks).
-template <int WIDTH, bool FULL, bool DIV, uint32_t FMT>
+template <int WIDTH, bool FULL, bool DIV, uint32_t FMT, int AW = 0>
 __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t end, int32_t t, int64_t tb,
-                                           const SpecBracket& br, uint32_t* slot, uint64_t* part) {
+                                           const SpecBracket& br, uint32_t* slot, uint64_t* part, float anorm) {
   const EncArgs& e = a.e;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float4 v[kSpecV];
   load_f4<kSpecV, FULL, true>(e.x, b, end, v);  // x is read once: nontemporal (the fix uses the records)
+  int4 araw[AW ? kSpecV : 1];
+  if (AW) {  // the fused PS step's last client: its payload loaded beside x
+#pragma unroll
+    for (int k = 0; k < kSpecV; ++k)
+      araw[k] = acc_load<AW ? AW : 1, FULL>(a.aq, b + 4 * ((int64_t)k * kThreads + threadIdx.x), end);
+  }
   float4 uu[4];
   philox_rows(e, b, tb, t, 0, uu);
   // Branch-free from the loads to the stores, so that the scheduler can place the Philox
@@ -691,6 +766,19 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
     v[k].x = __fmul_rn(v[k].x, alpha); v[k].y = __fmul_rn(v[k].y, alpha);
     v[k].z = __fmul_rn(v[k].z, alpha); v[k].w = __fmul_rn(v[k].w, alpha);
     if (FMT != kFmtF32 && alpha != 1.0f) v[k] = round_fmt4(v[k], FMT);  // torch.mul on the half tensor
+    if (AW) {  // acc + decode(last client), stored when the caller keeps the accumulator
+      v[k] = acc_add4<AW ? AW : 1>(v[k], araw[k], anorm, a.alevels, a.ainv);
+      if (a.aout) {
+        const int64_t el = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+        if (FULL || el + 4 <= end) {
+          store_nt(a.aout + el, v[k]);
+        } else if (el < end) {
+          a.aout[el] = v[k].x;
+          if (el + 1 < end) a.aout[el + 1] = v[k].y;
+          if (el + 2 < end) a.aout[el + 2] = v[k].z;
+        }
+      }
+    }
     if (DIV) {  // fused PS step: the average, stored once (nontemporal) and quantised from registers
       const float d = a.divisor;
       v[k].x = __fdiv_rn(v[k].x, d); v[k].y = __fdiv_rn(v[k].y, d);
@@ -742,13 +830,15 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
 
 // The per-tensor tables are __restrict__ const kernel arguments so that they are read with
 // scalar loads (a vector load there is waited for before the x loads are issued).
-template <int WIDTH, bool DIV, uint32_t FMT = kFmtF32>
+template <int WIDTH, bool DIV, uint32_t FMT = kFmtF32, int AW = 0>
 __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
-                                                            const int64_t* __restrict__ begins) {
+                                                            const int64_t* __restrict__ begins,
+                                                            const float* __restrict__ anorms) {
   const int64_t blk = blockIdx.x;
   const Item it = a.e.items[blk >> 2];
   const SpecBracket br = brs[it.tensor];
   const int64_t tb = begins[it.tensor];
+  const float anorm = AW ? anorms[it.tensor] : 0.0f;
   const int64_t b = it.begin + (blk & 3) * kSpecBlk;
   const int wave = threadIdx.x >> 6;
   uint32_t* slot = a.slots + blk * kSpecSlot;
@@ -761,8 +851,8 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const Sp
     return;
   }
   const int64_t end = min(b + kSpecBlk, it.end);
-  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, FMT>(a, b, end, it.tensor, tb, br, slot, part);
-  else spec_block<WIDTH, false, DIV, FMT>(a, b, end, it.tensor, tb, br, slot, part);
+  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, FMT, AW>(a, b, end, it.tensor, tb, br, slot, part, anorm);
+  else spec_block<WIDTH, false, DIV, FMT, AW>(a, b, end, it.tensor, tb, br, slot, part, anorm);
 }
 
 // One fold segment (a workgroup of the finish launch); the last arriver of the tensor folds the
@@ -2059,27 +2149,40 @@ static int check_bits(int32_t s) {
   return OMF_OK;
 }
 
+// The fused PS step's last client (omf_ps_accumulate_apply_encode): its payload, width, level
+// count and norms, and where acc + decode(q) goes (NULL: nowhere).
+struct AccIn {
+  const void* q;
+  int32_t width, levels;
+  const float* norm;
+  float* acc_out;
+};
+
 static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, const float* u, uint64_t seed,
                          uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream,
-                         float divisor, float* xout, uint32_t fmt);
+                         float divisor, float* xout, uint32_t fmt, const AccIn* acc_in);
 
 static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, const float* u, uint64_t seed,
                        uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream,
-                       float divisor = 0.0f, float* xout = nullptr, int32_t fmt = 0) {
+                       float divisor = 0.0f, float* xout = nullptr, int32_t fmt = 0, const AccIn* acc_in = nullptr) {
   if (!p) return fail(OMF_EINVAL, "plan is NULL");
   if (fmt < 0 || fmt > 2) return fail(OMF_EINVAL, "value_format must be 0 (fp32), 1 (bf16) or 2 (fp16)");
   DeviceGuard g(p->device);
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   if (int r = plan_enter(p, (hipStream_t)stream)) return r;
   if (int r = encode_launch(p, x, alpha, s, u, seed, offset, norm_in, q, norm_out, norm_only, stream, divisor, xout,
-                            (uint32_t)fmt))
+                            (uint32_t)fmt, acc_in))
     return r;
   return plan_leave(p, (hipStream_t)stream);
 }
 
+// Whether a fused PS step with the last client's decode takes the bracketed encoder's one pass
+// (else the caller runs decode-accumulate, then the plain fused step).
+static bool spec_serves(const omf_plan* p, int32_t s, const float* u, float divisor, uint32_t fmt);
+
 static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, const float* u, uint64_t seed,
                          uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream,
-                         float divisor, float* xout, uint32_t fmt) {
+                         float divisor, float* xout, uint32_t fmt, const AccIn* acc_in) {
   if (!p) return fail(OMF_EINVAL, "plan is NULL");
   if (int r = check_bits(s)) return r;
   const int width = (1 << s) <= 127 ? 1 : 4;
@@ -2147,8 +2250,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
   // Bracketed single-read encoder: fp32 / bf16 / fp16 values with on-device draws at s <= 4
   // (int32 payloads take the ring, caller uniforms the two-pass encoder; the fused PS step is
   // fp32).  Three launches, no host interaction.
-  if (p->strategy == 3 && !norm_only && !u && (fmt == 0 || divisor == 0.0f) && s >= kSpecMinBits &&
-      s <= kSpecMaxBits) {
+  if (!norm_only && spec_serves(p, s, u, divisor, fmt)) {
     // (the fused PS step too: the pass divides, stores the average and quantises it)
     SpecArgs sa;
     a.items = p->d_flat;
@@ -2177,18 +2279,28 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.flags = p->d_spec_flags;
     sa.status = p->d_spec_status;
     sa.nblocks = p->n_spec_blocks;
+    sa.aq = acc_in ? acc_in->q : nullptr;
+    sa.anorm = acc_in ? acc_in->norm : nullptr;
+    sa.aout = acc_in ? acc_in->acc_out : nullptr;
+    sa.awidth = acc_in ? acc_in->width : 0;
+    sa.alevels = acc_in ? (float)acc_in->levels : 0.0f;
+    sa.ainv = acc_in && (acc_in->levels & (acc_in->levels - 1)) == 0 ? 1.0f / (float)acc_in->levels : 0.0f;
     const dim3 gbr((unsigned)p->n_spec_br), gb((unsigned)p->n_spec_blocks);
     // p->spec_skip: test / experiment switches (omf_plan_set_debug; 0 in production): bit 0
     // skips the bracket launch (the previous brackets stay), bit 1 the finish launch, bits 2/3
     // the fix stores / the fix, bit 4 the fold — the payload is then not the encoder's.
     if (!(p->spec_skip & 1u)) hipLaunchKernelGGL(qsgd_spec_bracket, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
     const bool div = divisor != 0.0f;
-    if (fmt == kFmtBF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtBF16>), gb, blk, 0, st, sa, sa.br, sa.begins);
-    else if (fmt == kFmtF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF16>), gb, blk, 0, st, sa, sa.br, sa.begins);
-    else if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
-    else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
-    else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false>), gb, blk, 0, st, sa, sa.br, sa.begins);
-    else hipLaunchKernelGGL((qsgd_spec_quant<4, true>), gb, blk, 0, st, sa, sa.br, sa.begins);
+    const float* an = sa.anorm;
+    const int aw = acc_in ? (acc_in->width == 32 ? 4 : 1) : 0;
+    if (fmt == kFmtBF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtBF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    else if (fmt == kFmtF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    else if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    else if (width == 1 && aw == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 1>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    else if (width == 1 && aw == 4) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 4>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    else hipLaunchKernelGGL((qsgd_spec_quant<4, true>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
     if (p->spec_skip & 2u) {  // experiment: no finish launch (timings only)
       OMF_HIP(hipGetLastError());
       return OMF_OK;
@@ -2268,6 +2380,10 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
   return OMF_OK;
 }
 
+static bool spec_serves(const omf_plan* p, int32_t s, const float* u, float divisor, uint32_t fmt) {
+  return p->strategy == 3 && !u && (fmt == 0 || divisor == 0.0f) && s >= kSpecMinBits && s <= kSpecMaxBits;
+}
+
 int omf_qsgd_encode(omf_plan* plan, const float* x, float alpha, int32_t bit_width, const float* u, uint64_t seed,
                     uint64_t offset, const float* norm_in, void* q_out, float* norm_out, void* stream) {
   return encode_impl(plan, x, alpha, bit_width, u, seed, offset, norm_in, q_out, norm_out, false, stream);
@@ -2310,6 +2426,43 @@ int omf_ps_apply_encode(omf_plan* p, const float* acc, float divisor, float* avg
     OMF_HIP(hipMemcpyAsync(avg_out, acc, 4 * (size_t)p->arena_end, hipMemcpyDeviceToDevice, (hipStream_t)stream));
   if (int r = omf_div_f32(avg_out, p->arena_end, divisor, stream)) return r;
   return encode_impl(p, avg_out, 1.0f, bit_width, u, seed, offset, nullptr, q_out, norm_out, false, stream);
+}
+
+int omf_ps_accumulate_apply_encode(omf_plan* p, const float* acc, const void* q_in, int32_t width_in,
+                                   int32_t levels_in, const float* norm_in, float* acc_out, float divisor,
+                                   float* avg_out, int32_t bit_width, const float* u, uint64_t seed, uint64_t offset,
+                                   void* q_out, float* norm_out, void* stream) {
+  if (!p) return fail(OMF_EINVAL, "plan is NULL");
+  if (!acc || !avg_out || !q_in || !norm_in)
+    return fail(OMF_EINVAL, "omf_ps_accumulate_apply_encode: acc, q_in, norm_in and avg_out must be non-NULL");
+  if (width_in != 8 && width_in != 32) return fail(OMF_EINVAL, "width_in must be 8 or 32");
+  if (levels_in <= 0) return fail(OMF_EINVAL, "levels_in must be > 0");
+  if (!(divisor != 0.0f)) return fail(OMF_EINVAL, "omf_ps_accumulate_apply_encode: divisor must be non-zero");
+  if (int r = check_bits(bit_width)) return r;
+  if (!aligned(acc, 16) || !aligned(avg_out, 16) || (acc_out && !aligned(acc_out, 16)) ||
+      !aligned(q_in, width_in == 8 ? 4 : 16))
+    return fail(OMF_EINVAL, "misaligned buffer (fp32/int32 need 16 B, int8 needs 4 B alignment)");
+  const size_t bytes = 4 * (size_t)p->arena_end;
+  auto overlap = [bytes](const void* x, const void* y) {
+    const uintptr_t a0 = (uintptr_t)x, b0 = (uintptr_t)y;
+    return a0 < b0 + bytes && b0 < a0 + bytes;
+  };
+  if (overlap(avg_out, acc) || (acc_out && overlap(avg_out, acc_out)) || (acc_out && acc_out != acc && overlap(acc_out, acc)))
+    return fail(OMF_EINVAL, "omf_ps_accumulate_apply_encode: avg_out must be disjoint from acc and acc_out; acc_out is "
+                            "acc itself or disjoint from it");
+  DeviceGuard g(p->device);
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  hipStream_t st = (hipStream_t)stream;
+  if (spec_serves(p, bit_width, u, divisor, 0u)) {  // one pass: acc and the last payload read once
+    const AccIn ai{q_in, width_in, levels_in, norm_in, acc_out};
+    return encode_impl(p, acc, 1.0f, bit_width, u, seed, offset, nullptr, q_out, norm_out, false, stream, divisor,
+                       avg_out, 0, &ai);
+  }
+  // other encoders: the decoder's accumulate, then the fused step (the same bytes)
+  float* sum = acc_out ? acc_out : avg_out;
+  if (sum != acc) OMF_HIP(hipMemcpyAsync(sum, acc, bytes, hipMemcpyDeviceToDevice, st));
+  if (int r = omf_qsgd_decode(p, q_in, width_in, levels_in, norm_in, sum, 1, stream)) return r;
+  return omf_ps_apply_encode(p, sum, divisor, avg_out, bit_width, u, seed, offset, q_out, norm_out, stream);
 }
 
 int omf_qsgd_norms(omf_plan* plan, const float* x, float alpha, float* norm_out, void* stream) {

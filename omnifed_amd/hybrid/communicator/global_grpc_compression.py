@@ -258,6 +258,16 @@ def _gpu_for(out_dev: torch.device) -> torch.device:
     return compute_device(torch.empty(0), out_dev)
 
 
+def _last_wins(v: torch.Tensor, ix: torch.Tensor, n: int):
+    """The (values, indices) that numpy's ``dense[indices] = values`` leaves when an index repeats:
+    the last one per index (a GPU scatter would keep an arbitrary one).  Only for selections that
+    must repeat an index (k > n: a malformed message); the encoders' selections never do."""
+    pos = torch.arange(ix.numel(), device=ix.device)
+    last = torch.full((n,), -1, dtype=torch.int64, device=ix.device).scatter_reduce_(0, ix, pos, "amax")
+    keep = last[ix] == pos
+    return v[keep], ix[keep]
+
+
 def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, device=None) -> torch.Tensor:
     """global_grpc_compression.py:140-160: overlay on ``base_tensor`` or zero-filled dense."""
     if not layer.values_data or not layer.indices_data:
@@ -276,6 +286,8 @@ def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, dev
     dev = _gpu_for(out_dev)
     v = torch.from_numpy(values.copy()).to(dev)
     ix = torch.from_numpy(np.array(indices, dtype=np.int64, copy=True)).to(dev)
+    if ix.numel() > numel:
+        v, ix = _last_wins(v, ix, numel)
     if base_tensor is not None:
         # the reference overlays a numpy copy of the base, so the result has the base's dtype
         # (fp32 values cast on assignment: round-to-nearest for fp16, truncation for integers) and
@@ -283,9 +295,11 @@ def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, dev
         bdt = base_tensor.dtype
         if bdt == torch.bfloat16:
             raise TypeError("Got unsupported ScalarType BFloat16")
-        if bdt == torch.float64:  # the fp32 kernel cannot hold the base exactly
-            flat = base_tensor.detach().reshape(-1).to(dev, torch.float64, copy=True)
-            flat[ix] = v.double()
+        if bdt == torch.float64 or not (bdt.is_floating_point or bdt.is_complex):
+            # the fp32 kernel cannot hold the base exactly (fp64, or integers above 2^24): the base
+            # stays in its own dtype and only the assigned values are cast, as numpy's overlay does
+            flat = base_tensor.detach().reshape(-1).to(dev, copy=True)
+            flat[ix] = v.to(bdt)
             return flat.reshape(original_shape).to(out_dev)
         y = torch.empty(max(numel, 4), dtype=torch.float32, device=dev)
         y[:numel].copy_(base_tensor.detach().reshape(-1).to(dev, torch.float32))

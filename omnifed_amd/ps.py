@@ -131,8 +131,12 @@ class DeviceAggregator:
         the whole update, then accumulates: a bad layer leaves acc as it was).  All QSGD layers go
         through ONE decode-accumulate launch, all Top-K layers through ONE index check and ONE
         scatter-add (omf_topk_decode_counts), both fed by chunked pinned staging.  A repeated name:
-        the last layer, as the reference's decoded dict."""
-        from .hybrid.communicator.global_grpc_compression import _validate_layer, check_topk_indices, stage_topk
+        the last layer, as the reference's decoded dict.  The scatter-add assumes the indices of a
+        Top-K layer are distinct, as every encoder's selection (torch.topk's, the reference's) is; a
+        layer with more values than elements (which must repeat indices) is decoded alone with
+        numpy's last-wins rule and added."""
+        from .hybrid.communicator.global_grpc_compression import (_decode_topk_layer, _validate_layer,
+                                                                  check_topk_indices, stage_topk)
 
         last: Dict[str, object] = {}
         topk_payload: Dict[str, tuple] = {}
@@ -175,14 +179,16 @@ class DeviceAggregator:
             hostio.bytes_to_device(items, qd, isz * self.plan.payload_elems(width), key="ps_decode", check=check)
             q_args = (qd, width, level, nd)
         t_args = None
+        # a Top-K layer with more values than its tensor's elements repeats indices: decoded alone
+        # with numpy's last-wins rule (_decode_topk_layer), as decode_updates_dict does
+        odd = [L for L in topk if topk_payload[L.layer_name][2] > self.plan.sizes[self.index[L.layer_name]]]
+        odd_args = [(L.layer_name, _decode_topk_layer(L, device=self.device).reshape(-1)) for L in odd]
+        topk = [L for L in topk if L not in odd]
         if topk:
             pairs = [(b"", b"")] * self.plan.nt
             for L in topk:
                 i = self.index[L.layer_name]
                 v, ix, k = topk_payload[L.layer_name]
-                if k > self.plan.sizes[i]:
-                    raise IndexError(f"Compressed layer {L.layer_name!r}: {k} values for a tensor of "
-                                     f"{self.plan.sizes[i]} elements")
                 pairs[i] = (v, ix)
             counts, values, indices = stage_topk(pairs, self.device, "ps_topk")
             check_topk_indices(self.plan, counts, indices, self.names)  # synchronises
@@ -202,7 +208,7 @@ class DeviceAggregator:
             self.plan.qsgd_decode(qd, width, level, nd, y_out=self.acc, accumulate=True)
         if t_args is not None:
             self.plan.topk_decode_counts(*t_args, y=self.acc, mode=2)
-        for name, arr in dense_args:
+        for name, arr in dense_args + odd_args:
             self._slice(name).add_(arr.reshape(-1))
         self.update_count += 1
         self.total_samples += int(number_samples)
@@ -288,6 +294,70 @@ class DeviceAggregator:
         for n, L in zip(self.names, got):
             layers.append(L if L is not None and int(np.prod(self.shapes[n])) > 0 else _encode_dense_layer(n, avg[n]))
         return avg, layers
+
+    def accumulate_apply_encode(self, layers, number_samples: int, compressor, keep_sum: bool = False):
+        """The last arriving client's ``SendUpdate`` and the round's first ``GetUpdatedModel`` in one
+        pass (global_grpc_server.py:108-125, 147-171, 213-234): ``acc + decode(update)``, the
+        average over ``total_samples`` (this client's included) and its QSGD downlink — for a QSGD
+        update and a Philox QSGD compressor on a bracketed plan, ONE encoder pass that reads the
+        accumulator and the update's payload once (omf_ps_accumulate_apply_encode; 10 B per element
+        at s = 4 instead of 18 for accumulate_layers + apply_and_encode).  The accumulator then lacks
+        this client's term unless ``keep_sum`` (the reference re-initialises it at the next round's
+        first update, :86-92, and reads it only in _apply_model_updates).  Same return as
+        ``apply_and_encode``; bytes equal to ``accumulate_layers`` followed by it.  Any other
+        message or compressor takes those two calls."""
+        from .hybrid.compression.qsgd import QSGDQuantCompression
+        from .hybrid.communicator.global_grpc_compression import (_encode_dense_layer, _validate_layer,
+                                                                  qsgd_layers_from_arena)
+
+        layers = list(layers)
+        last: Dict[str, object] = {}
+        for L in layers:
+            _validate_layer(L)
+            if L.layer_name in self.index:
+                last[L.layer_name] = L
+        kept = sorted(last.values(), key=lambda L: self.index[L.layer_name])
+        fusable = (isinstance(compressor, QSGDQuantCompression) and compressor.rng == "philox" and self.compute_mean
+                   and not compressor.packed_wire and kept
+                   and all(L.compression_type == "QSGDQuantCompression" for L in kept)
+                   and len({(L.width, L.level) for L in kept}) == 1)
+        if not fusable:
+            self.accumulate_layers(layers, number_samples)
+            return self.apply_and_encode(compressor)
+        width, level = kept[0].width, kept[0].level
+        isz = width // 8
+        norms = np.zeros(self.plan.nt, dtype=np.float32)  # absent tensors: norm 0 adds +0
+        items = []
+        for L in kept:
+            i = self.index[L.layer_name]
+            norms[i] = np.frombuffer(L.meta_tensor, dtype=np.float32).reshape(-1)[0]
+            items.append((self.plan.offsets[i] * isz, (lambda L=L: L.values_data)))
+
+        def check(k, payload):
+            n = self.plan.sizes[self.index[kept[k].layer_name]]
+            if len(payload) != n * isz:
+                raise ValueError(f"QSGD layer {kept[k].layer_name!r}: {len(payload) // isz} values, expected {n}")
+
+        qd = torch.empty(self.plan.payload_elems(width), dtype=torch.int8 if width == 8 else torch.int32,
+                         device=self.device)  # absent tensors: any level times their zero norm adds +0
+        nd = torch.from_numpy(norms).to(self.device)
+        hostio.bytes_to_device(items, qd, isz * self.plan.payload_elems(width), key="ps_decode", check=check)
+        total = self.total_samples + int(number_samples)
+        if self.avg is None:
+            self.avg = torch.empty_like(self.acc)
+        s = compressor.s
+        _, q, norms_out = self.plan.ps_accumulate_apply_encode(
+            self.acc, qd, width, level, nd, float(total), s, acc_out=self.acc if keep_sum else None, avg_out=self.avg,
+            seed=compressor.philox_key(), offset=compressor._next_call())
+        self.update_count += 1
+        self.total_samples = total
+        avg = {n: self._avg_slice(n).view(self.shapes[n]) for n in self.names}
+        got = qsgd_layers_from_arena(self.plan, q, norms_out, self.names, [self.shapes[n] for n in self.names], 2**s,
+                                     compressor.packed_wire)
+        out = []
+        for n, L in zip(self.names, got):
+            out.append(L if L is not None and int(np.prod(self.shapes[n])) > 0 else _encode_dense_layer(n, avg[n]))
+        return avg, out
 
     def apply(self, total_samples: Optional[int] = None) -> Dict[str, torch.Tensor]:
         """_apply_model_updates (global_grpc_server.py:155-171): acc / total_samples per tensor."""

@@ -10,9 +10,10 @@
 #   sq [tag]                SQ counter passes of the ResNet-18 encoders -> gpurun_out/<tag>_sq.json
 #   py <script> [args...]   any experiment script (its stdout -> gpurun_out/py.out)
 #   measure [tag]           the round's profile set: rocprofv3 kernel stats of the QSGD and the Top-K
-#                           bench lines, the two PMC passes (-> profiles/pmc_traffic.json, stamped with
-#                           the source digest; OMF_COMMIT names the commit), the bench line (reads the
-#                           fresh PMC file), the wire timings; copied into profiles/<tag>_*
+#                           bench lines, the two PMC passes at s = 4 (QSGD + Top-K) and at s = 8 (the int32
+#                           wire) (-> profiles/pmc_traffic.json, stamped with the source digest; OMF_COMMIT
+#                           names the commit), the bench lines at s = 4 and s = 8 (they read the fresh PMC
+#                           file), the wire timings; copied into profiles/<tag>_*
 set -o pipefail
 cd "$(dirname "$0")/.." && export TMPDIR=/tmp
 R=$(pwd)
@@ -98,12 +99,18 @@ case "$task" in
     T=${1:-r04}
     bash scripts/gpu.sh prof ${T} > /dev/null || exit 2
     bash scripts/gpu.sh prof ${T}_topk --codec topk > /dev/null || exit 3
+    bash scripts/gpu.sh prof ${T}_s8 --bits 8 --no-topk > /dev/null || exit 3
+    rm -f gpurun_out/${T}_pmc_traffic.json
     bash scripts/gpu.sh pmc ${T} || exit 4
+    PMC_BITS=8 bash scripts/gpu.sh pmc ${T} --bits 8 --no-topk || exit 4
     cp gpurun_out/${T}_pmc_traffic.json profiles/pmc_traffic.json
     bash scripts/gpu.sh bench ${T} || exit 5
+    bash scripts/gpu.sh bench ${T}_s8 --bits 8 --no-topk --no-cpu-baseline || exit 5
+    cp gpurun_out/${T}_s8_bench.json profiles/${T}_s8_bench.json
     bash scripts/gpu.sh wire ${T} > /dev/null || exit 6
     cp gpurun_out/${T}_kernel_stats.csv profiles/${T}_kernel_stats.csv
     cp gpurun_out/${T}_topk_kernel_stats.csv profiles/${T}_topk_kernel_stats.csv
+    cp gpurun_out/${T}_s8_kernel_stats.csv profiles/${T}_s8_kernel_stats.csv
     cp gpurun_out/${T}_bench.json profiles/${T}_bench.json
     cp gpurun_out/${T}_wire.json profiles/${T}_wire.json
     mkdir -p gpurun_out/profiles_copy && cp profiles/pmc_traffic.json profiles/${T}_* gpurun_out/profiles_copy/

@@ -2,6 +2,8 @@
 """Per-launch HBM traffic of the codec kernels from two rocprofv3 --pmc passes.
 
 Usage: python scripts/pmc_traffic.py FETCH_DIR WRITE_DIR OUT_JSON [config bits]
+The measurement goes under runs["<config>/s<bits>"] of OUT_JSON; the other runs already in it are
+kept when they were measured on the same kernel sources (source digest), dropped otherwise.
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction
 (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts 64 B per 128 B request of a wide
 coalesced stream, so it is doubled; WRITE_SIZE is exact for 16 B/lane stores.
@@ -75,14 +77,26 @@ def main():
                                     text=True).stdout.strip()
         except OSError:
             commit = ""
-    j = {"config": cfg, "bits": bits, "source_sha": source_digest(), "commit": commit or None,
+    sha = source_digest()
+    runs = {}
+    try:
+        with open(out) as fh:
+            old = json.load(fh)
+        if old.get("source_sha") == sha:
+            runs = old.get("runs", {})
+    except (OSError, ValueError):
+        pass
+    run = {"config": cfg, "bits": bits,
+           "bytes_per_launch": {k: round(v["fetch_bytes_corrected"] + v["write_bytes"]) for k, v in res.items()},
+           "detail": res}
+    runs[f"{cfg}/s{bits}"] = run
+    j = {"source_sha": sha, "commit": commit or None,
          "date": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%d"), "note": "FETCH_SIZE x2 (gfx950 wide-load correction) + WRITE_SIZE, KiB->B, "
          "average per launch; Infinity-Cache hits are counted as fetches",
-         "bytes_per_launch": {k: round(v["fetch_bytes_corrected"] + v["write_bytes"]) for k, v in res.items()},
-         "detail": res}
+         "runs": runs}
     with open(out, "w") as fh:
         json.dump(j, fh, indent=1)
-    print(json.dumps(j["bytes_per_launch"]))
+    print(json.dumps(run["bytes_per_launch"]))
 
 
 if __name__ == "__main__":
