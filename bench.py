@@ -362,10 +362,11 @@ def main():
         reps = max(args.steps, 10)
         enc_ms = event_ms(torch, st, lambda i: plan.qsgd_encode(x, s, q_out=q, norm_out=norms, alpha=weight, seed=seed,
                                                                 offset=10_000 + i), reps)
+        enc_kernel = plan.last_encoder_kernel  # what the encode launched (the plan's record)
         dec_ms = event_ms(torch, st, lambda i: plan.qsgd_decode(q, width, L, norms, y_out=y), reps)
         plan.check()
         enc_bytes = dec_bytes = (4 + w) * N
-        dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, plan.encoder_kernel_for(s)) if enc_ms >= dec_ms else \
+        dom_ms, dom_bytes, dom_name = (enc_ms, enc_bytes, enc_kernel) if enc_ms >= dec_ms else \
             (dec_ms, dec_bytes, "qsgd_decode_flat")
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(dom_name, args.config, s)

@@ -121,14 +121,20 @@ int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy);
 /* The plan's encode strategy (0-3 as above).  A new plan picks 3 (bracketed single-read) for
  * arenas of >= 2^25 elements and 2 (the ring) below: the measured crossover;
  * OMF_ENCODE_STRATEGY overrides.  Strategy 3 serves fp32 / bf16 / fp16 values with on-device
- * draws at bit_width 1-4; its int32-wire encodes (bit_width >= 7, fp32, on-device draws) take the
- * ring (2), its other encodes (caller uniforms, s = 5, 6) the two-pass encoder (1). */
+ * draws at bit_width 1-4 and fp32 values at 5-8 (omf_plan_set_wide_levels); its other int32-wire
+ * encodes take the ring (2), the rest (caller uniforms, half values at s = 5, 6) the two-pass
+ * encoder (1). */
 int32_t omf_plan_encode_strategy(const omf_plan* plan);
 /* The encoder the plan's latest encode (or fused PS step) launched: 0 register-resident +
  * two-pass, 1 two-pass, 2 ring, 3 bracketed, 4 grid, 5 levels with caller norms (norm_in);
  * -1 before the first.  Lets a test assert which path a configuration takes (e.g. the int32
  * wire of a bracketed plan: the ring). */
 int32_t omf_plan_last_encoder(const omf_plan* plan);
+/* Wide levels on a bracketed plan (strategy 3): on (the default; OMF_SPEC_WIDE=0 turns it off for
+ * new plans) the fp32 encodes at bit_width 5-8 (int8 at 5-6, the int32 wire at 7-8) take the
+ * bracketed encoder with a 32-quad undecided list per wave; off, they take the ring (7-8) or the
+ * two-pass encoder (5-6).  Identical payloads either way. */
+int omf_plan_set_wide_levels(omf_plan* plan, int32_t on);
 /* Diagnostics of the last bracketed single-read encode (strategy 3; synchronises `stream`,
  * not for the hot path): out[0] tensors requantised whole (norm outside the sampled bracket,
  * a wave's undecided-quad slot overflowed, or a degenerate sample), out[1] of those the

@@ -205,6 +205,12 @@ class Plan:
         check(lib().omf_plan_set_encode_strategy(self._h, code), "omf_plan_set_encode_strategy")
         self.strategy = strategy
 
+    def set_wide_levels(self, on: bool) -> None:
+        """Bit widths 5-8 (fp32) through the bracketed encoder (True, the default) or the ring /
+        two-pass encoders (omf_plan_set_wide_levels); identical payloads."""
+        with self._lock:
+            check(lib().omf_plan_set_wide_levels(self._h, 1 if on else 0), "omf_plan_set_wide_levels")
+
     @property
     def last_encoder(self) -> str:
         """The encoder the latest encode launched (omf_plan_last_encoder): one of STRATEGIES,
@@ -217,11 +223,19 @@ class Plan:
         """Name of the kernel one encode launch runs (profiling / roofline bookkeeping)."""
         return self.encoder_kernel_for(4)
 
+    @property
+    def last_encoder_kernel(self) -> str:
+        """The kernel name (or "qsgd_spec_all" for the bracketed encoder's three launches) of the
+        latest encode — what a profile of it shows."""
+        return {"bracket": "qsgd_spec_all", "ring": "qsgd_encode_pc", "grid": "qsgd_encode_grid",
+                "norm_in": "qsgd_quant_sub"}.get(self.last_encoder, "qsgd_encode_ordered")
+
     def encoder_kernel_for(self, bit_width: int) -> str:
-        """The kernel an fp32, on-device-draw encode at ``bit_width`` runs: the bracketed encoder
-        (three launches: "qsgd_spec_all") serves bit widths 1-4, hands int32 payloads (s >= 7) to
-        the ring and s = 5, 6 to the two-pass encoder (omf_plan_encode_strategy)."""
-        if self.strategy == "bracket" and not 1 <= int(bit_width) <= 4:
+        """The kernel an fp32, on-device-draw encode at ``bit_width`` runs by default: the bracketed
+        encoder (three launches: "qsgd_spec_all") serves bit widths 1-8 (5-8 with its wide-level
+        list, omf_plan_set_wide_levels), wider int32 payloads take the ring (omf_plan_encode_strategy).
+        ``last_encoder_kernel`` reports what a call actually launched."""
+        if self.strategy == "bracket" and not 1 <= int(bit_width) <= 8:
             return "qsgd_encode_pc" if storage_width(2 ** int(bit_width)) == 32 else "qsgd_encode_ordered"
         return {"ring": "qsgd_encode_pc", "bracket": "qsgd_spec_all", "grid": "qsgd_encode_grid"}.get(
             self.strategy, "qsgd_encode_ordered")

@@ -405,6 +405,14 @@ constexpr int kSpecV = 4;                                    // float4 rows per 
 constexpr int64_t kSpecBlk = (int64_t)kSpecV * kThreads * 4;  // 4096 elements per block
 constexpr int kSpecSlot = 32;                                 // words per block: 4 waves x 7 quads (+ 4 spare)
 constexpr int kSpecPerWave = 7;                               // listed quads per wave
+// Wide levels (bit_width 5-8, fp32: the reference's default int32 wire at 8): the undecided fraction
+// grows with L (a level step is norm / L wide), so a wave lists up to 32 quads (Llama-400M s = 8 with
+// the sampled +-2.4 % brackets: ~10 per wave on its 1 Mi-element tensors, 2.1 M quads in all) and
+// four fix threads share a wave slot.  Slots and records of this capacity are allocated at the
+// plan's first wide encode.
+constexpr int kSpecPerWaveWide = 32;
+constexpr int kSpecMaxBitsWide = 8;
+__host__ __device__ constexpr int spec_slot_words(int pw) { return pw == kSpecPerWave ? kSpecSlot : kWaves * pw; }
 constexpr int64_t kSpecExact = 16384;                         // tensors read whole by the bracket
 constexpr int kSpecRun = 64;                                  // elements per sampled run (256 B: DRAM-friendly)
 constexpr int kSpecRuns = 512;                                // sampled runs per larger tensor (at most)
@@ -447,8 +455,8 @@ struct SpecArgs {
   uint32_t* fold_cnt;      // per tensor arrival counters of the fold segments (reset by the last arriver)
   uint64_t* partials;      // fp64 bits, one per wave (kWaves per block)
   uint32_t* heads;         // per wave (dense, kWaves per block): (tensor << 8) | count of listed quads
-  uint32_t* slots;         // kSpecSlot words per block: kSpecPerWave quad indices per wave
-  float4* recs;            // per listed quad: its scaled x and its uniforms (2 float4), kWaves x kSpecPerWave per block
+  uint32_t* slots;         // spec_slot_words(PW) words per block: PW quad indices per wave
+  float4* recs;            // per listed quad: its scaled x and its uniforms (2 float4), kWaves x PW per block
   uint32_t* flags;         // per tensor: a wave's slot overflowed (set by quant, cleared by fold)
   uint32_t* status;        // per tensor: 0 = listed quads only, 1 = requantise whole
   uint64_t* ngran;         // per tensor: {epoch << 1 | bad, norm} published by the fold
@@ -740,7 +748,7 @@ __device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t 
 // One block's pass: loads issued first, the Philox draws (independent of x) computed while
 // they are in flight, then the partial, the levels and the undecided list.  FULL: a whole
 // 4 Ki block (straight-line code, no bounds checks).
-template <int WIDTH, bool FULL, bool DIV, uint32_t FMT, int AW = 0>
+template <int WIDTH, bool FULL, bool DIV, uint32_t FMT, int AW = 0, int PW = kSpecPerWave>
 __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t end, int32_t t, int64_t tb,
                                            const SpecBracket& br, uint32_t* slot, uint64_t* part, float anorm) {
   const EncArgs& e = a.e;
@@ -796,7 +804,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
   }
   uint32_t cnt = 0;  // wave-uniform
   {
-    uint32_t* list = slot + kSpecPerWave * wave;
+    uint32_t* list = slot + PW * wave;
 #pragma unroll
     for (int k = 0; k < kSpecV; ++k) {
       const int64_t el = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
@@ -809,9 +817,9 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
       const uint64_t m = __ballot(live && und);
       if (m) {  // rare: list this wave's undecided quads
         const uint32_t pos = cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
-        if (live && und && pos < (uint32_t)kSpecPerWave) {  // the quad, its x and its draws: no re-read
+        if (live && und && pos < (uint32_t)PW) {  // the quad, its x and its draws: no re-read
           list[pos] = (uint32_t)(el >> 2);
-          float4* rec = a.recs + 2 * ((blockIdx.x * kWaves + wave) * kSpecPerWave + pos);
+          float4* rec = a.recs + 2 * ((blockIdx.x * kWaves + wave) * PW + pos);
           rec[0] = v[k];
           rec[1] = uu[k];
         }
@@ -822,15 +830,15 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
   const double s = wave_sum_f64((double)acc);
   if (lane == 0) {
     *part = (uint64_t)__double_as_longlong(s);
-    a.heads[blockIdx.x * kWaves + wave] = ((uint32_t)t << 8) | min(cnt, (uint32_t)kSpecPerWave);
-    if (cnt > (uint32_t)kSpecPerWave)
+    a.heads[blockIdx.x * kWaves + wave] = ((uint32_t)t << 8) | min(cnt, (uint32_t)PW);
+    if (cnt > (uint32_t)PW)
       __hip_atomic_fetch_or(&a.flags[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 // The per-tensor tables are __restrict__ const kernel arguments so that they are read with
 // scalar loads (a vector load there is waited for before the x loads are issued).
-template <int WIDTH, bool DIV, uint32_t FMT = kFmtF32, int AW = 0>
+template <int WIDTH, bool DIV, uint32_t FMT = kFmtF32, int AW = 0, int PW = kSpecPerWave>
 __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
                                                             const int64_t* __restrict__ begins,
                                                             const float* __restrict__ anorms) {
@@ -841,7 +849,7 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const Sp
   const float anorm = AW ? anorms[it.tensor] : 0.0f;
   const int64_t b = it.begin + (blk & 3) * kSpecBlk;
   const int wave = threadIdx.x >> 6;
-  uint32_t* slot = a.slots + blk * kSpecSlot;
+  uint32_t* slot = a.slots + blk * spec_slot_words(PW);
   uint64_t* part = a.partials + blk * kWaves + wave;
   if (b >= it.end) {  // past the tensor's end: an empty block still reports (stale values otherwise)
     if ((threadIdx.x & 63) == 0) {
@@ -851,8 +859,8 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const Sp
     return;
   }
   const int64_t end = min(b + kSpecBlk, it.end);
-  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, FMT, AW>(a, b, end, it.tensor, tb, br, slot, part, anorm);
-  else spec_block<WIDTH, false, DIV, FMT, AW>(a, b, end, it.tensor, tb, br, slot, part, anorm);
+  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, FMT, AW, PW>(a, b, end, it.tensor, tb, br, slot, part, anorm);
+  else spec_block<WIDTH, false, DIV, FMT, AW, PW>(a, b, end, it.tensor, tb, br, slot, part, anorm);
 }
 
 // One fold segment (a workgroup of the finish launch); the last arriver of the tensor folds the
@@ -936,7 +944,7 @@ __device__ __forceinline__ bool spec_norm_wait(const SpecArgs& a, int32_t t, flo
 // tensor's norm granule, then per listed quad its index, recorded x and draws, the exact level
 // from the shared element math (Markstein division) and its store.  A block whose tensor the fold marked bad (norm outside the bracket, a slot
 // overflow, a deferred tensor) is requantised whole from x by its workgroup (the rare path).
-template <int WIDTH>
+template <int WIDTH, int PW = kSpecPerWave, int FT = 1>
 __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const SpecFoldItem* __restrict__ fold_items,
                                                              int32_t nfold, const Item* __restrict__ items,
                                                              const int64_t* __restrict__ begins,
@@ -947,17 +955,19 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
     if (!(a.dbg & 16u)) spec_fold(a, fold_items[blockIdx.x]);  // test hook: no fold, the fix waits expire
     return;
   }
-  // One thread per wave slot (its listed quads in turn: usually none or one), 64 blocks per
-  // workgroup: the fix is a few dependent round trips per thread, so its cost is the number of
-  // workgroup generations, not the quads (8 threads per slot took 8x the workgroups: +8-10 us).
-  constexpr int BPW = kThreads / kWaves;  // blocks per workgroup (64)
+  // FT threads per wave slot (its listed quads in turn, strided: narrow levels list none or one, so
+  // FT = 1 there — 8 threads per slot took 8x the workgroups: +8-10 us; wide levels list ~10 per
+  // slot, FT = 4), kThreads / (kWaves FT) blocks per workgroup: the fix is a few dependent round
+  // trips per thread, so its cost is the number of workgroup generations, not the quads.
+  constexpr int BPW = kThreads / (kWaves * FT);  // blocks per workgroup
   __shared__ uint32_t s_rep[BPW];
   __shared__ float s_rep_norm[BPW];  // the granule's norm (norm_out is written in this launch)
   __shared__ uint32_t s_nrep;
   const EncArgs& e = a.e;
   const int64_t fb = (int64_t)blockIdx.x - nfold;
   if (threadIdx.x == 0) s_nrep = 0u;
-  const int64_t ws = fb * kThreads + threadIdx.x;  // global wave slot
+  const int64_t ws = (fb * kThreads + threadIdx.x) / FT;  // global wave slot
+  const uint32_t sub = (uint32_t)(threadIdx.x % FT);
   const int64_t blk = ws / kWaves;
   const int w = (int)(ws % kWaves);
   bool rep = false;
@@ -966,7 +976,7 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
     const uint32_t head = heads[ws];
     const uint32_t cnt = head & 0xffu;
     const int32_t t = (int32_t)(head >> 8);
-    const bool leader = w == 0;  // one status check per block
+    const bool leader = w == 0 && sub == 0;  // one status check per block
     if ((cnt > 0u || leader) && !(a.dbg & 8u)) {
       const Item it = items[blk >> 2];
       float norm;
@@ -974,9 +984,9 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
       if (spec_norm_wait(a, t, norm, bad)) {
         const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
         const Divisor dv(norm, e.fmt);
-        for (uint32_t j = 0; j < cnt; ++j) {
-          const uint32_t q = slots[blk * kSpecSlot + kSpecPerWave * w + j];
-          const float4* rec = recs + 2 * (ws * kSpecPerWave + j);
+        for (uint32_t j = sub; j < cnt; j += FT) {
+          const uint32_t q = slots[blk * spec_slot_words(PW) + PW * w + j];
+          const float4* rec = recs + 2 * (ws * PW + j);
           int32_t qq[4];
           qsgd_quad<false>(rec[0], rec[1], dv, e.levels, false, qq);
           if (!(a.dbg & 4u)) store_quad<WIDTH>(e, 4 * (int64_t)q, end, qq);
@@ -1465,6 +1475,10 @@ struct omf_plan {
   uint32_t* d_spec_slots = nullptr;
   uint32_t* d_spec_heads = nullptr;
   float4* d_spec_recs = nullptr;  // listed quads' x and draws (32 B each)
+  uint32_t* d_spec_slots_w = nullptr;  // the wide-level capacity (kSpecPerWaveWide), made at the first
+  float4* d_spec_recs_w = nullptr;     // wide encode (bit_width 5-8)
+  int32_t spec_last_pw = kSpecPerWave;  // the list capacity of the latest bracketed encode
+  int32_t spec_wide = 1;  // wide levels (5-8 bits, fp32) through the bracket (1) or as before (0): OMF_SPEC_WIDE
   // arena-aligned decoder: per 4 Ki block, tensor id | (1 << 31 when inside it)
   int64_t n_dec_blocks = 0;
   uint32_t* d_dec_binfo = nullptr;
@@ -1986,6 +2000,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     // 0.35), the ring below (ResNet-18: 0.032 ms against 0.08 for the bracket's four launches).
     p->strategy = p->arena_end >= ((int64_t)1 << 25) ? 3 : 2;
     if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 4));
+    if (const char* sw = getenv("OMF_SPEC_WIDE")) p->spec_wide = atoi(sw) != 0 ? 1 : 0;
     {  // grid encoder: one 1024-thread workgroup per CU must fit
       int nb = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)qsgd_encode_grid<1>, 1024, 0) == hipSuccess &&
@@ -2012,6 +2027,8 @@ int omf_plan_destroy(omf_plan* plan) {
   DeviceGuard g(plan->device);
   if (plan->last_ev) (void)hipEventDestroy(plan->last_ev);
   if (plan->d_block) (void)hipFree(plan->d_block);
+  if (plan->d_spec_slots_w) (void)hipFree(plan->d_spec_slots_w);
+  if (plan->d_spec_recs_w) (void)hipFree(plan->d_spec_recs_w);
   for (auto& e : plan->topk_tables) (void)hipFree(e.dev);
   delete plan;
   return OMF_OK;
@@ -2026,6 +2043,11 @@ int64_t omf_plan_encode_items(const omf_plan* plan) {
 
 int32_t omf_plan_encode_strategy(const omf_plan* plan) { return plan ? plan->strategy : -1; }
 int32_t omf_plan_last_encoder(const omf_plan* plan) { return plan ? plan->last_encoder : -1; }
+int omf_plan_set_wide_levels(omf_plan* plan, int32_t on) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  plan->spec_wide = on != 0 ? 1 : 0;
+  return OMF_OK;
+}
 
 int omf_plan_set_encode_strategy(omf_plan* plan, int32_t strategy) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
@@ -2113,7 +2135,7 @@ int omf_plan_spec_stats(omf_plan* plan, void* stream, int64_t* out4) {
     for (int w = 0; w < kWaves; ++w) {
       const uint32_t c = heads[(size_t)blk * kWaves + w] & 0xffu;
       listed += c;
-      full += c == (uint32_t)kSpecPerWave;
+      full += c == (uint32_t)plan->spec_last_pw;
     }
   out4[0] = whole;
   out4[1] = deferred;
@@ -2178,7 +2200,7 @@ static int encode_impl(omf_plan* p, const float* x, float alpha, int32_t s, cons
 
 // Whether a fused PS step with the last client's decode takes the bracketed encoder's one pass
 // (else the caller runs decode-accumulate, then the plain fused step).
-static bool spec_serves(const omf_plan* p, int32_t s, const float* u, float divisor, uint32_t fmt);
+static bool spec_serves(const omf_plan* p, int32_t s, const float* u, float divisor, uint32_t fmt, bool wide_ok);
 
 static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, const float* u, uint64_t seed,
                          uint64_t offset, const float* norm_in, void* q, float* norm_out, bool norm_only, void* stream,
@@ -2250,7 +2272,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
   // Bracketed single-read encoder: fp32 / bf16 / fp16 values with on-device draws at s <= 4
   // (int32 payloads take the ring, caller uniforms the two-pass encoder; the fused PS step is
   // fp32).  Three launches, no host interaction.
-  if (!norm_only && spec_serves(p, s, u, divisor, fmt)) {
+  if (!norm_only && spec_serves(p, s, u, divisor, fmt, acc_in == nullptr)) {
     // (the fused PS step too: the pass divides, stores the average and quantises it)
     SpecArgs sa;
     a.items = p->d_flat;
@@ -2273,9 +2295,15 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.wait_ticks = p->wait_ticks;
     sa.br = p->d_spec_br;
     sa.partials = p->d_spec_part;
-    sa.slots = p->d_spec_slots;
+    const bool wide = s > kSpecMaxBits;
+    if (wide && !p->d_spec_slots_w) {  // once per plan: the wide-level list capacity
+      OMF_HIP(hipMalloc(&p->d_spec_slots_w, 4 * (size_t)spec_slot_words(kSpecPerWaveWide) * (size_t)p->n_spec_blocks));
+      OMF_HIP(hipMalloc(&p->d_spec_recs_w, 32 * (size_t)kWaves * kSpecPerWaveWide * (size_t)p->n_spec_blocks));
+    }
+    p->spec_last_pw = wide ? kSpecPerWaveWide : kSpecPerWave;
+    sa.slots = wide ? p->d_spec_slots_w : p->d_spec_slots;
     sa.heads = p->d_spec_heads;
-    sa.recs = p->d_spec_recs;
+    sa.recs = wide ? p->d_spec_recs_w : p->d_spec_recs;
     sa.flags = p->d_spec_flags;
     sa.status = p->d_spec_status;
     sa.nblocks = p->n_spec_blocks;
@@ -2293,7 +2321,13 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     const bool div = divisor != 0.0f;
     const float* an = sa.anorm;
     const int aw = acc_in ? (acc_in->width == 32 ? 4 : 1) : 0;
-    if (fmt == kFmtBF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtBF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    constexpr int PWW = kSpecPerWaveWide;
+    if (wide) {  // fp32, no fused last client (spec_serves)
+      if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+      else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+      else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+      else hipLaunchKernelGGL((qsgd_spec_quant<4, true, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    } else if (fmt == kFmtBF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtBF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
     else if (fmt == kFmtF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
     else if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
     else if (width == 1 && aw == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 1>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
@@ -2306,6 +2340,20 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
       return OMF_OK;
     }
     const int32_t nfold = (int32_t)p->n_spec_fold;
+    if (wide) {
+      constexpr int FT = 4, BPW = kThreads / (kWaves * FT);  // fix: 16 blocks per workgroup
+      const dim3 gw((unsigned)(nfold + (p->n_spec_blocks + BPW - 1) / BPW));
+      if (width == 1)
+        hipLaunchKernelGGL((qsgd_spec_finish<1, PWW, FT>), gw, blk, 0, st, sa, (const SpecFoldItem*)sa.fold_items, nfold,
+                           (const Item*)a.items, (const int64_t*)sa.begins, (const uint32_t*)sa.slots,
+                           (const float4*)sa.recs, (const uint32_t*)sa.heads);
+      else
+        hipLaunchKernelGGL((qsgd_spec_finish<4, PWW, FT>), gw, blk, 0, st, sa, (const SpecFoldItem*)sa.fold_items, nfold,
+                           (const Item*)a.items, (const int64_t*)sa.begins, (const uint32_t*)sa.slots,
+                           (const float4*)sa.recs, (const uint32_t*)sa.heads);
+      OMF_HIP(hipGetLastError());
+      return OMF_OK;
+    }
     const dim3 gfin((unsigned)(nfold + (p->n_spec_blocks + kThreads / kWaves - 1) / (kThreads / kWaves)));  // fix: 64 blocks per workgroup
     if (width == 1)
       hipLaunchKernelGGL(qsgd_spec_finish<1>, gfin, blk, 0, st, sa, (const SpecFoldItem*)sa.fold_items, nfold,
@@ -2380,8 +2428,10 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
   return OMF_OK;
 }
 
-static bool spec_serves(const omf_plan* p, int32_t s, const float* u, float divisor, uint32_t fmt) {
-  return p->strategy == 3 && !u && (fmt == 0 || divisor == 0.0f) && s >= kSpecMinBits && s <= kSpecMaxBits;
+static bool spec_serves(const omf_plan* p, int32_t s, const float* u, float divisor, uint32_t fmt, bool wide_ok) {
+  if (p->strategy != 3 || u || s < kSpecMinBits) return false;
+  if (s <= kSpecMaxBits) return fmt == 0 || divisor == 0.0f;
+  return wide_ok && p->spec_wide && s <= kSpecMaxBitsWide && fmt == 0;  // fp32 wide levels
 }
 
 int omf_qsgd_encode(omf_plan* plan, const float* x, float alpha, int32_t bit_width, const float* u, uint64_t seed,
@@ -2453,7 +2503,7 @@ int omf_ps_accumulate_apply_encode(omf_plan* p, const float* acc, const void* q_
   DeviceGuard g(p->device);
   if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
   hipStream_t st = (hipStream_t)stream;
-  if (spec_serves(p, bit_width, u, divisor, 0u)) {  // one pass: acc and the last payload read once
+  if (spec_serves(p, bit_width, u, divisor, 0u, false)) {  // one pass: acc and the last payload read once
     const AccIn ai{q_in, width_in, levels_in, norm_in, acc_out};
     return encode_impl(p, acc, 1.0f, bit_width, u, seed, offset, nullptr, q_out, norm_out, false, stream, divisor,
                        avg_out, 0, &ai);

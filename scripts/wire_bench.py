@@ -64,7 +64,10 @@ def leg(comp, tag):
     r["encode_updates_dict_ms"] = tm(lambda: encode_updates_dict(upd, comp))
     r["decode_updates_dict_gpu_ms"] = tm(lambda: decode_updates_dict(layers, device=dev))
     r["decode_updates_into_ms"] = tm(lambda: decode_updates_into(layers, targets))
-    r["decode_updates_dict_cpu_ms"] = tm(lambda: decode_updates_dict(layers), reps=3, warm=1)
+    r["decode_updates_dict_cpu_ms"] = tm(lambda: decode_updates_dict(layers), reps=3, warm=1)  # pageable pool
+    hostio.set_pinned_arenas(4 << 30)  # the opt-in page-locked result arenas (OMF_PIN_HOST_ARENAS)
+    r["decode_updates_dict_cpu_pinned_ms"] = tm(lambda: decode_updates_dict(layers), reps=3, warm=1)
+    hostio.set_pinned_arenas(0)
     agg = DeviceAggregator(named, device=dev)
     r["agg_accumulate_layers_ms"] = tm(lambda: agg.accumulate_layers(layers, number_samples=1))
     # GetUpdatedModel: the server's compressor re-encodes the average (apply_and_encode).  A dense
@@ -160,6 +163,34 @@ def separate():
 res["ps_fused_apply_encode_ms"] = round(tm(lambda: plan.ps_apply_encode(acc, 40.0, 4, avg_out=avg, q_out=q,
                                                                          norm_out=nr, seed=1), reps=10), 4)
 res["ps_divide_then_encode_ms"] = round(tm(separate, reps=10), 4)
+# the last client's SendUpdate + the first GetUpdatedModel (global_grpc_server.py:108-125, 147-171,
+# 213-234): its decode-accumulate fused into the PS step (omf_ps_accumulate_apply_encode) against
+# decode-accumulate then the fused PS step; device-resident, then through the drop-in's messages
+q_last, n_last = plan.qsgd_encode(torch.randn(plan.arena_end, device=dev, generator=g), 4, seed=2)
+acc_keep = acc.clone()
+
+
+def last_two_calls():
+    acc_keep.copy_(acc)
+    plan.qsgd_decode(q_last, 8, 16, n_last, y_out=acc_keep, accumulate=True)
+    plan.ps_apply_encode(acc_keep, 40.0, 4, avg_out=avg, q_out=q, norm_out=nr, seed=1)
+
+
+def last_fused():
+    plan.ps_accumulate_apply_encode(acc, q_last, 8, 16, n_last, 40.0, 4, avg_out=avg, q_out=q, norm_out=nr, seed=1)
+
+
+res["ps_last_client_fused_ms"] = round(tm(last_fused, reps=10), 4)
+res["ps_last_client_two_calls_ms"] = round(tm(last_two_calls, reps=10) - tm(lambda: acc_keep.copy_(acc), reps=10), 4)
+del acc_keep
+agg_f = DeviceAggregator(named, device=dev)
+agg_s = DeviceAggregator(named, device=dev)
+srv_f = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev)
+srv_s = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev)
+res["ps_last_update_and_get_model_fused_ms"] = tm(lambda: agg_f.accumulate_apply_encode(layers, 1, srv_f), reps=5)
+res["ps_last_update_and_get_model_two_calls_ms"] = tm(
+    lambda: (agg_s.accumulate_layers(layers, 1), agg_s.apply_and_encode(srv_s)), reps=5)
+del agg_f, agg_s
 # opt-in bit-packed wire (s = 4: 6 bits per element instead of 8)
 pcomp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev, packed_wire=True)
 players = encode_updates_dict(upd, pcomp)

@@ -9,9 +9,10 @@ equal, and the decode equal to ``oracle.qsgd_dequantize``.  The bracketed encode
 pass (the undecided quads it lists and fixes) must have run: spec_stats()["listed"] > 0.
 
 Round 5 adds the int32 wire (``bit_width: 8``, the reference's default, conf/base.yaml:200;
-qsgd.py:18-21 stores levels > 127 as int32): on these bracketed plans an s = 8 encode takes the
-ring encoder (omf_qsgd.hip encode_impl, ``wide_ring``), asserted through the plan's record of
-the encoder it launched; Llama-400M (alpha 1) and Llama-150M (alpha 2), every tensor.
+qsgd.py:18-21 stores levels > 127 as int32): on these plans an s = 8 encode takes the bracketed
+encoder with its wide-level undecided list (asserted through the plan's record of the encoder it
+launched; the fix pass must have run), Llama-400M (alpha 1) and Llama-150M (alpha 2), every tensor;
+and test_wide_levels_bracket_equals_ring pins the wide path against the ring at s = 5-8.
 """
 
 from concurrent.futures import ThreadPoolExecutor
@@ -48,13 +49,12 @@ def test_headline_arena_every_tensor_equals_oracle(gpu, cfg, s, alpha):
     seed, off = 0x5EED, 7
     q, norms = plan.qsgd_encode(x, s, alpha=alpha, seed=seed, offset=off)
     width = codec.storage_width(2**s)
-    if s <= 4:
-        assert plan.last_encoder == "bracket"
-        stats = plan.spec_stats()
-        assert stats["listed"] > 0, stats  # the finish pass fixed undecided quads
-    else:
-        assert width == 32 and q.dtype == torch.int32
-        assert plan.last_encoder == "ring"  # the int32 wire of a bracketed plan
+    assert plan.last_encoder == "bracket"
+    stats = plan.spec_stats()
+    assert stats["listed"] > 0, stats  # the finish pass fixed undecided quads
+    assert stats["whole"] == 0, stats  # no tensor needed the whole-tensor requantisation
+    if s >= 7:
+        assert width == 32 and q.dtype == torch.int32  # the int32 wire
     plan.check()
     L = 2**s
     y = plan.qsgd_decode(q, width, L, norms)
@@ -80,6 +80,55 @@ def test_headline_arena_every_tensor_equals_oracle(gpu, cfg, s, alpha):
             return f"tensor {t}: decode differs"
         return None
 
+    with ThreadPoolExecutor(_threads()) as ex:
+        errors = [e for e in ex.map(check, range(len(sizes))) if e]
+    assert not errors, errors[:5]
+
+
+@pytest.mark.parametrize("s", [5, 6, 7, 8])
+def test_wide_levels_against_the_oracle(gpu, s):
+    """Bit widths 5-8 through the bracketed encoder's wide-level list, weighted, and the fused PS
+    step at the same widths: every tensor's levels equal the oracle's given the GPU norm and draws
+    (the fix pass ran: listed > 0), and the average is numpy's fp32 division."""
+    sizes = [5, 16384, 70001] + [1 << 20] * 4 + [4 << 20] * 4 + [3000, 2_000_000, 8 << 20]
+    plan = codec.Plan(sizes, device=gpu)
+    plan.set_encode_strategy("bracket")  # 30 M elements: below the default crossover
+    g = torch.Generator(device=gpu)
+    g.manual_seed(77 + s)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    L = 2**s
+    seed, off = 9, 4
+    q, norms = plan.qsgd_encode(x, s, alpha=2.0, seed=seed, offset=off)
+    assert plan.last_encoder == "bracket"
+    stats = plan.spec_stats()
+    # the fix pass ran; a mid-size tensor (70 001 elements) may overflow its wave lists at s = 8 and be
+    # requantised whole (exact, and cheap at that size) — the large ones never are
+    assert stats["listed"] > 0 and stats["whole"] <= 1, stats
+    avg, qa, na = plan.ps_apply_encode(x, 3.0, s, seed=seed, offset=off + 1)
+    assert plan.last_encoder == "bracket"
+    plan.check()
+    xh = x.cpu().numpy()
+    xs_all = (xh * np.float32(2.0)).astype(np.float32)
+    av_all = xh / np.float32(3.0)
+    qh, nh, qah, nah, ah = q.cpu().numpy(), norms.cpu().numpy(), qa.cpu().numpy(), na.cpu().numpy(), avg.cpu().numpy()
+
+    def check(t):
+        o, n = plan.offsets[t], sizes[t]
+        for src, qq, nn, off_ in ((xs_all, qh, nh, off), (av_all, qah, nah, off + 1)):
+            xs = src[o:o + n]
+            ref = float(np.sqrt(np.sum(xs.astype(np.float64) ** 2)))
+            if abs(float(nn[t]) - ref) > 2e-6 * ref:
+                return f"tensor {t}: norm {nn[t]} vs fp64 {ref}"
+            u = torch.from_numpy(oracle.philox_uniforms(seed, off_, t, n))
+            want, _, _, _ = oracle.qsgd_quantize(torch.from_numpy(xs), s, norm=float(nn[t]), u=u)
+            if qq[o:o + n].tobytes() != want.numpy().tobytes():
+                bad = np.flatnonzero(qq[o:o + n] != want.numpy())
+                return f"tensor {t}: {bad.size} levels differ, first at {bad[:4].tolist()}"
+        if ah[o:o + n].tobytes() != av_all[o:o + n].tobytes():
+            return f"tensor {t}: average differs"
+        return None
+
+    assert L > 16
     with ThreadPoolExecutor(_threads()) as ex:
         errors = [e for e in ex.map(check, range(len(sizes))) if e]
     assert not errors, errors[:5]

@@ -184,7 +184,7 @@ def test_device_to_host_ring_equals_cpu(gpu, dtype):
     """hostio.device_to_host (the CPU placement's D2H): same bytes as .cpu() for empty, odd-sized
     and many-chunk tensors — through the D2HRing into pageable memory (the ring wrapping several
     times: small chunks, 3 slots; from the main thread and from concurrent threads, each call
-    leasing its own ring) and into the pooled page-locked arenas."""
+    leasing its own ring), into the pooled pageable arenas and, with a budget, the page-locked ones."""
     from omnifed_amd import hostio
 
     g = torch.Generator(device=gpu).manual_seed(5)
@@ -196,9 +196,15 @@ def test_device_to_host_ring_equals_cpu(gpu, dtype):
         out = hostio.device_to_host(s, limit=1 << 16, slots=3, pool_memory=False)  # the D2HRing
         assert out.device.type == "cpu" and out.dtype == dtype and not out.is_pinned()
         assert torch.equal(out, s.cpu())
-        pooled = hostio.device_to_host(s)  # a pooled page-locked arena from 1 MiB up
-        assert pooled.dtype == dtype and torch.equal(pooled, s.cpu())
-        assert pooled.is_pinned() == (s.numel() * s.element_size() >= hostio.HostArenaPool.MIN_BYTES)
+        pooled = hostio.device_to_host(s)  # a pooled pageable arena from 1 MiB up (page-locked: opt-in)
+        assert pooled.dtype == dtype and torch.equal(pooled, s.cpu()) and not pooled.is_pinned()
+        hostio.set_pinned_arenas(64 << 20)
+        try:
+            pinned = hostio.device_to_host(s)  # with a budget: a page-locked arena from 1 MiB up
+        finally:
+            hostio.set_pinned_arenas(0)
+        assert pinned.dtype == dtype and torch.equal(pinned, s.cpu())
+        assert pinned.is_pinned() == (s.numel() * s.element_size() >= hostio.HostArenaPool.MIN_BYTES)
     with ThreadPoolExecutor(4) as ex:
         outs = list(ex.map(lambda s: hostio.device_to_host(s, limit=1 << 16, slots=3, pool_memory=False), srcs * 2))
     for o, s in zip(outs, srcs * 2):
