@@ -416,6 +416,12 @@ __host__ __device__ constexpr int spec_slot_words(int pw) { return pw == kSpecPe
 constexpr int64_t kSpecExact = 16384;                         // tensors read whole by the bracket
 constexpr int kSpecRun = 64;                                  // elements per sampled run (256 B: DRAM-friendly)
 constexpr int kSpecRuns = 512;                                // sampled runs per larger tensor (at most)
+// wide levels: 4x the sampled elements (half the bracket width: the undecided quads, the fix pass's
+// work, grow with L and with the bracket's width) in runs of 256 elements (1 KiB: four times fewer
+// random DRAM accesses than 2 Ki runs of 64), kBrParts workgroups per tensor, 128 runs each
+constexpr int kSpecRunWide = 256;
+constexpr int kSpecRunsWide = 512;
+constexpr int kBrParts = 2;  // (4 parts of one round each: 732 workgroups of 1024 threads, three generations)
 constexpr int kSpecSeg = 4096;                                // wave partials per fold workgroup (16 loads per thread
                                                               // in flight: a 4 Mi-element tensor is one segment)
 // Widest level count the bracket serves: the undecided fraction grows with L (a level step is
@@ -436,7 +442,7 @@ struct SpecBrItem {
   int64_t begin, n;  // the tensor's arena range
   int64_t base;      // stratum length n / R (R = runs of the tensor); rem = n % R strata are one longer
   int32_t R, rem;
-  int32_t tensor, pad;
+  int32_t tensor, Rw;  // Rw: the runs of kSpecRunWide sampled for wide levels (strata n / Rw)
 };
 // Fold work item: wave partials [p_begin, p_end) of tensor `tensor`, segment `seg` of `nsegs`.
 struct SpecFoldItem {
@@ -466,6 +472,9 @@ struct SpecArgs {
   float zsig;              // bracket half-width in standard deviations of the sample estimate (6)
   float* xout;
   uint32_t epoch;          // per-launch tag (never 0)
+  uint32_t wide;           // wide levels: the bracket samples Rw runs (SpecBrItem), kBrParts workgroups per tensor
+  double* br_part;         // wide: per (tensor, part) the partial {S1, S2}
+  uint32_t* br_cnt;        // wide: per tensor arrival counter (reset by the last arriver)
   int64_t nblocks;
   // Fused last-client decode-accumulate (omf_ps_accumulate_apply_encode; aq == NULL: none): before
   // the divide, x := fl32(x + fl32(fl32(anorm[t] * q) / alevels)) — the decoder's accumulate, bit
@@ -576,16 +585,62 @@ __device__ __forceinline__ double br_sum(double v, double* lds) {
   return s;
 }
 
+// The bracket's sample of one tensor: runs of RUN elements at a hashed position inside each of R
+// balanced strata (of >= 2 RUN elements); a run is RUN / 4 float4 loaded by consecutive lanes, 8
+// passes per round (their loads in flight together); this workgroup takes the rounds part, part +
+// parts, ...  Per run: s1 += its sum of squares, s2 += its square (in lane 0 of the run).
+template <int RUN>
+__device__ __forceinline__ void bracket_sample(const SpecArgs& a, const float* __restrict__ x, int32_t t, int64_t tb,
+                                               int64_t n, int64_t R, int part, int parts, double& s1, double& s2) {
+  constexpr int LPR = RUN / 4, RPP = kBrThreads / LPR, PASSES = 8, PER_ROUND = RPP * PASSES;
+  const int64_t base = n / R, rem = n % R;
+  const int j = threadIdx.x & (LPR - 1);
+  const float alpha = a.e.alpha;
+  for (int64_t rb = (int64_t)part * PER_ROUND; rb < R; rb += (int64_t)parts * PER_ROUND) {
+    float4 v[PASSES];
+    bool live[PASSES];
+    int64_t pos[PASSES];
+#pragma unroll
+    for (int i = 0; i < PASSES; ++i) {
+      const int64_t r0 = rb + (int64_t)i * RPP + (threadIdx.x / LPR);
+      live[i] = r0 < R;
+      const int64_t r = live[i] ? r0 : 0;  // a dead lane re-reads run 0 (masked below)
+      const int64_t lo = r * base + min(r, rem), len = base + (r < rem ? 1 : 0);
+      pos[i] = ((lo + (int64_t)(spec_hash((uint32_t)r, (uint32_t)t) % (uint32_t)(len - (RUN - 1)))) & ~(int64_t)3) +
+               4 * j;
+      v[i] = *reinterpret_cast<const float4*>(x + pos[i]);
+    }
+    if (a.aq) {  // the fused PS step's last client (after every x load is issued)
+#pragma unroll
+      for (int i = 0; i < PASSES; ++i) v[i] = br_value(a, v[i], tb + pos[i], tb + n, t);
+    }
+#pragma unroll
+    for (int i = 0; i < PASSES; ++i) {
+      float sr = live[i] ? sq4(spec_prologue(v[i], alpha, a.divisor, a.e.fmt), 0.0f) : 0.0f;
+#pragma unroll
+      for (int o = LPR / 2; o > 0; o >>= 1) sr += __shfl_xor(sr, o, LPR);  // the run's sum in every lane
+      if (live[i] && j == 0) {
+        s1 += (double)sr;
+        s2 += (double)sr * (double)sr;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, const SpecBrItem* __restrict__ items) {
   __shared__ double red[kBrWaves];
-  const SpecBrItem bi = items[blockIdx.x];  // one scalar load: the tensor's range and strata
+  __shared__ uint32_t s_last;
+  // wide levels: kBrParts workgroups per tensor, part g sampling runs [g kSpecRuns, (g + 1) kSpecRuns)
+  const int parts = a.wide ? kBrParts : 1;
+  const int part = (int)(blockIdx.x % (unsigned)parts);
+  const SpecBrItem bi = items[blockIdx.x / (unsigned)parts];  // one scalar load: the tensor's range and strata
   const int32_t t = bi.tensor;
   const int64_t tb = bi.begin, n = bi.n;
   const float* __restrict__ x = a.e.x + tb;
   const float alpha = a.e.alpha;
   double s1 = 0.0, s2 = 0.0;
   const bool exact = n <= kSpecExact;
-  const int64_t R = bi.R;
+  const int64_t R = a.wide ? (int64_t)bi.Rw : (int64_t)bi.R;
   // Loads are unconditional (a clamped address, the value masked after): a load under a
   // branch is waited for at the branch's end, which would serialise the round trips.
   if (exact) {  // 4 float4 per thread, all loads in flight
@@ -621,37 +676,31 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     for (int i = 0; i < PER; ++i) acc = sq4(spec_prologue(v[i], alpha, a.divisor, a.e.fmt), acc);
     s1 = acc;
   } else {
-    // runs of 64 elements at a hashed position inside each of R <= 512 balanced strata (of
-    // >= 128 elements); a run is 16 float4 loaded by 16 consecutive lanes, 64 runs per pass
-    constexpr int LPR = kSpecRun / 4, RPP = kBrThreads / LPR, PASSES = kSpecRuns / RPP;
-    const int64_t base = bi.base, rem = bi.rem;
-    const int j = threadIdx.x & (LPR - 1);
-    float4 v[PASSES];
-    bool live[PASSES];
-#pragma unroll
-    for (int i = 0; i < PASSES; ++i) {
-      const int64_t r0 = (int64_t)i * RPP + (threadIdx.x / LPR);
-      live[i] = r0 < R;
-      const int64_t r = live[i] ? r0 : 0;  // a dead lane re-reads run 0 (masked below)
-      const int64_t lo = r * base + min(r, rem), len = base + (r < rem ? 1 : 0);
-      const int64_t pos = (lo + (int64_t)(spec_hash((uint32_t)r, (uint32_t)t) % (uint32_t)(len - (kSpecRun - 1)))) &
-                          ~(int64_t)3;
-      v[i] = *reinterpret_cast<const float4*>(x + pos + 4 * j);
-      if (a.aq) v[i] = br_value(a, v[i], tb + pos + 4 * j, tb + n, t);  // the fused PS step's last client
+    if (a.wide) bracket_sample<kSpecRunWide>(a, x, t, tb, n, R, part, parts, s1, s2);
+    else bracket_sample<kSpecRun>(a, x, t, tb, n, R, part, parts, s1, s2);
+  }
+  if (exact && part != 0) return;  // an exact tensor is one workgroup's
+  double S1 = br_sum(s1, red);
+  double S2 = br_sum(s2, red);
+  if (!exact && parts > 1) {  // the last part to arrive combines the partials in part order
+    if (threadIdx.x == 0) {
+      double* bp = a.br_part + 2 * ((int64_t)t * parts + part);
+      st_agent(reinterpret_cast<uint64_t*>(bp), (uint64_t)__double_as_longlong(S1));
+      st_agent(reinterpret_cast<uint64_t*>(bp + 1), (uint64_t)__double_as_longlong(S2));
+      drain_vmem();
+      const uint32_t last = add_agent(&a.br_cnt[t], 1u) == (uint32_t)(parts - 1) ? 1u : 0u;
+      if (last) __hip_atomic_store(&a.br_cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
     }
-#pragma unroll
-    for (int i = 0; i < PASSES; ++i) {
-      float sr = live[i] ? sq4(spec_prologue(v[i], alpha, a.divisor, a.e.fmt), 0.0f) : 0.0f;
-#pragma unroll
-      for (int o = LPR / 2; o > 0; o >>= 1) sr += __shfl_xor(sr, o, LPR);  // the run's sum in every lane
-      if (live[i] && j == 0) {
-        s1 += (double)sr;
-        s2 += (double)sr * (double)sr;
-      }
+    __syncthreads();
+    if (!s_last || threadIdx.x != 0) return;
+    S1 = S2 = 0.0;
+    for (int g = 0; g < parts; ++g) {
+      const uint64_t* bp = reinterpret_cast<const uint64_t*>(a.br_part + 2 * ((int64_t)t * parts + g));
+      S1 += __longlong_as_double((long long)ld_agent(bp));
+      S2 += __longlong_as_double((long long)ld_agent(bp + 1));
     }
   }
-  const double S1 = br_sum(s1, red);
-  const double S2 = br_sum(s2, red);
   if (threadIdx.x != 0) return;
   double ss, k;
   if (exact) {
@@ -660,7 +709,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
   } else {
     const double Rd = (double)R, m = S1 / Rd;
     const double var = fmax(0.0, (S2 - Rd * m * m) / (Rd - 1.0));
-    ss = S1 * ((double)n / ((double)kSpecRun * Rd));
+    ss = S1 * ((double)n / ((double)(a.wide ? kSpecRunWide : kSpecRun) * Rd));
     k = (double)a.zsig * sqrt(var / Rd) / m + 0x1p-10;  // 6 sigma of the run-sum estimate + 0.1 %
   }
   // bf16 / fp16 values: the norm is rounded to the format (at most half an ulp: 2^-8 / 2^-11
@@ -978,13 +1027,34 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
     const int32_t t = (int32_t)(head >> 8);
     const bool leader = w == 0 && sub == 0;  // one status check per block
     if ((cnt > 0u || leader) && !(a.dbg & 8u)) {
+      // this thread's first PRE listed quads (index, recorded x and draws) are loaded before the
+      // norm wait, so their round trip overlaps it (clamped to the last listed quad: no load
+      // under a branch); the rest, if any (narrow lists only), in the loop after
+      constexpr int PRE = FT > 1 ? PW / FT : 2;
+      uint32_t qv[PRE];
+      float4 rx[PRE], ru[PRE];
+      const uint32_t jl = cnt > 0u ? cnt - 1u : 0u;
+#pragma unroll
+      for (int k = 0; k < PRE; ++k) {
+        const uint32_t j = min(sub + (uint32_t)(k * FT), jl);
+        qv[k] = slots[blk * spec_slot_words(PW) + PW * w + j];
+        rx[k] = recs[2 * (ws * PW + j)];
+        ru[k] = recs[2 * (ws * PW + j) + 1];
+      }
       const Item it = items[blk >> 2];
       float norm;
       bool bad;
       if (spec_norm_wait(a, t, norm, bad)) {
         const int64_t b = it.begin + (blk & 3) * kSpecBlk, end = min(b + kSpecBlk, it.end);
         const Divisor dv(norm, e.fmt);
-        for (uint32_t j = sub; j < cnt; j += FT) {
+#pragma unroll
+        for (int k = 0; k < PRE; ++k) {
+          if (sub + (uint32_t)(k * FT) >= cnt) break;
+          int32_t qq[4];
+          qsgd_quad<false>(rx[k], ru[k], dv, e.levels, false, qq);
+          if (!(a.dbg & 4u)) store_quad<WIDTH>(e, 4 * (int64_t)qv[k], end, qq);
+        }
+        for (uint32_t j = sub + (uint32_t)(PRE * FT); j < cnt; j += FT) {
           const uint32_t q = slots[blk * spec_slot_words(PW) + PW * w + j];
           const float4* rec = recs + 2 * (ws * PW + j);
           int32_t qq[4];
@@ -1477,6 +1547,8 @@ struct omf_plan {
   float4* d_spec_recs = nullptr;  // listed quads' x and draws (32 B each)
   uint32_t* d_spec_slots_w = nullptr;  // the wide-level capacity (kSpecPerWaveWide), made at the first
   float4* d_spec_recs_w = nullptr;     // wide encode (bit_width 5-8)
+  double* d_spec_br_part = nullptr;    // wide: the bracket parts' partial sums and arrival counters
+  uint32_t* d_spec_br_cnt = nullptr;
   int32_t spec_last_pw = kSpecPerWave;  // the list capacity of the latest bracketed encode
   int32_t spec_wide = 1;  // wide levels (5-8 bits, fp32) through the bracket (1) or as before (0): OMF_SPEC_WIDE
   // arena-aligned decoder: per 4 Ki block, tensor id | (1 << 31 when inside it)
@@ -1800,7 +1872,8 @@ static int upload_plan(omf_plan* p) {
     gpbeg[(size_t)t] = (uint32_t)(p_begin / (kWaves * 4));  // the grid encoder: one partial per item
     gpcnt[(size_t)t] = (uint32_t)((p_end - p_begin) / (kWaves * 4));
     const int64_t R = std::max<int64_t>(1, std::min<int64_t>(kSpecRuns, n / (2 * kSpecRun)));
-    br_items.push_back(SpecBrItem{b, n, n / R, (int32_t)R, (int32_t)(n % R), t});
+    const int64_t Rw = std::max<int64_t>(1, std::min<int64_t>(kSpecRunsWide, n / (2 * kSpecRunWide)));
+    br_items.push_back(SpecBrItem{b, n, n / R, (int32_t)R, (int32_t)(n % R), t, (int32_t)Rw});
     const int32_t nsegs = (int32_t)((p_end - p_begin + kSpecSeg - 1) / kSpecSeg);
     for (int32_t q = 0; q < nsegs; ++q)
       fold_items.push_back(SpecFoldItem{p_begin + (int64_t)q * kSpecSeg, std::min(p_end, p_begin + (int64_t)(q + 1) * kSpecSeg),
@@ -2029,6 +2102,8 @@ int omf_plan_destroy(omf_plan* plan) {
   if (plan->d_block) (void)hipFree(plan->d_block);
   if (plan->d_spec_slots_w) (void)hipFree(plan->d_spec_slots_w);
   if (plan->d_spec_recs_w) (void)hipFree(plan->d_spec_recs_w);
+  if (plan->d_spec_br_part) (void)hipFree(plan->d_spec_br_part);
+  if (plan->d_spec_br_cnt) (void)hipFree(plan->d_spec_br_cnt);
   for (auto& e : plan->topk_tables) (void)hipFree(e.dev);
   delete plan;
   return OMF_OK;
@@ -2287,6 +2362,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.fold_cnt = p->d_spec_cnt;
     if (++p->spec_epoch >= 0x80000000u) p->spec_epoch = 1;  // 31-bit tags (the norm granule keeps a status bit)
     sa.epoch = p->spec_epoch;
+    sa.wide = s > kSpecMaxBits ? 1u : 0u;
     sa.ngran = p->d_spec_ngran;
     sa.dbg = p->spec_skip;
     sa.zsig = p->spec_zsig;
@@ -2299,7 +2375,12 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     if (wide && !p->d_spec_slots_w) {  // once per plan: the wide-level list capacity
       OMF_HIP(hipMalloc(&p->d_spec_slots_w, 4 * (size_t)spec_slot_words(kSpecPerWaveWide) * (size_t)p->n_spec_blocks));
       OMF_HIP(hipMalloc(&p->d_spec_recs_w, 32 * (size_t)kWaves * kSpecPerWaveWide * (size_t)p->n_spec_blocks));
+      OMF_HIP(hipMalloc(&p->d_spec_br_part, 16 * (size_t)kBrParts * (size_t)p->nt));
+      OMF_HIP(hipMalloc(&p->d_spec_br_cnt, 4 * (size_t)p->nt));
+      OMF_HIP(hipMemsetAsync(p->d_spec_br_cnt, 0, 4 * (size_t)p->nt, st));  // left zero by every launch
     }
+    sa.br_part = p->d_spec_br_part;
+    sa.br_cnt = p->d_spec_br_cnt;
     p->spec_last_pw = wide ? kSpecPerWaveWide : kSpecPerWave;
     sa.slots = wide ? p->d_spec_slots_w : p->d_spec_slots;
     sa.heads = p->d_spec_heads;
@@ -2313,7 +2394,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.awidth = acc_in ? acc_in->width : 0;
     sa.alevels = acc_in ? (float)acc_in->levels : 0.0f;
     sa.ainv = acc_in && (acc_in->levels & (acc_in->levels - 1)) == 0 ? 1.0f / (float)acc_in->levels : 0.0f;
-    const dim3 gbr((unsigned)p->n_spec_br), gb((unsigned)p->n_spec_blocks);
+    const dim3 gbr((unsigned)(p->n_spec_br * (s > kSpecMaxBits ? kBrParts : 1))), gb((unsigned)p->n_spec_blocks);
     // p->spec_skip: test / experiment switches (omf_plan_set_debug; 0 in production): bit 0
     // skips the bracket launch (the previous brackets stay), bit 1 the finish launch, bits 2/3
     // the fix stores / the fix, bit 4 the fold — the payload is then not the encoder's.

@@ -90,8 +90,9 @@ def leg(comp, tag):
             agg2 = DeviceAggregator(named, device=dev)
             for c in range(2):
                 cc = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
-                if noise is None and c:
-                    u = {n: torch.randn(t.shape, device=dev, generator=g) * 1e-3 for n, t in upd.items()}
+                if noise is None:  # disjoint: independent gradients
+                    u = upd if c == 0 else {n: torch.randn(t.shape, device=dev, generator=g) * 1e-3
+                                            for n, t in upd.items()}
                 else:
                     u = {n: t + (noise * c) * torch.randn(t.shape, device=dev, generator=g) * 1e-3
                          for n, t in upd.items()}
