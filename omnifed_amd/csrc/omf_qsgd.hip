@@ -421,7 +421,10 @@ constexpr int kSpecRuns = 512;                                // sampled runs pe
 // random DRAM accesses than 2 Ki runs of 64), kBrParts workgroups per tensor, 128 runs each
 constexpr int kSpecRunWide = 256;
 constexpr int kSpecRunsWide = 512;
-constexpr int kBrParts = 2;  // (4 parts of one round each: 732 workgroups of 1024 threads, three generations)
+#ifndef OMF_BR_PARTS  // experiment builds may override it (scripts/exp/s8_variants.sh)
+#define OMF_BR_PARTS 2
+#endif
+constexpr int kBrParts = OMF_BR_PARTS;
 constexpr int kSpecSeg = 4096;                                // wave partials per fold workgroup (16 loads per thread
                                                               // in flight: a 4 Mi-element tensor is one segment)
 // Widest level count the bracket serves: the undecided fraction grows with L (a level step is
@@ -589,7 +592,7 @@ __device__ __forceinline__ double br_sum(double v, double* lds) {
 // balanced strata (of >= 2 RUN elements); a run is RUN / 4 float4 loaded by consecutive lanes, 8
 // passes per round (their loads in flight together); this workgroup takes the rounds part, part +
 // parts, ...  Per run: s1 += its sum of squares, s2 += its square (in lane 0 of the run).
-template <int RUN>
+template <int RUN, bool AQ>
 __device__ __forceinline__ void bracket_sample(const SpecArgs& a, const float* __restrict__ x, int32_t t, int64_t tb,
                                                int64_t n, int64_t R, int part, int parts, double& s1, double& s2) {
   constexpr int LPR = RUN / 4, RPP = kBrThreads / LPR, PASSES = 8, PER_ROUND = RPP * PASSES;
@@ -599,20 +602,20 @@ __device__ __forceinline__ void bracket_sample(const SpecArgs& a, const float* _
   for (int64_t rb = (int64_t)part * PER_ROUND; rb < R; rb += (int64_t)parts * PER_ROUND) {
     float4 v[PASSES];
     bool live[PASSES];
-    int64_t pos[PASSES];
+    auto run_pos = [&](int i) {  // element of this lane's float4 in pass i (recomputed: no VGPRs held)
+      const int64_t r0 = rb + (int64_t)i * RPP + (threadIdx.x / LPR);
+      const int64_t r = r0 < R ? r0 : 0;  // a dead lane re-reads run 0 (masked below)
+      const int64_t lo = r * base + min(r, rem), len = base + (r < rem ? 1 : 0);
+      return ((lo + (int64_t)(spec_hash((uint32_t)r, (uint32_t)t) % (uint32_t)(len - (RUN - 1)))) & ~(int64_t)3) + 4 * j;
+    };
 #pragma unroll
     for (int i = 0; i < PASSES; ++i) {
-      const int64_t r0 = rb + (int64_t)i * RPP + (threadIdx.x / LPR);
-      live[i] = r0 < R;
-      const int64_t r = live[i] ? r0 : 0;  // a dead lane re-reads run 0 (masked below)
-      const int64_t lo = r * base + min(r, rem), len = base + (r < rem ? 1 : 0);
-      pos[i] = ((lo + (int64_t)(spec_hash((uint32_t)r, (uint32_t)t) % (uint32_t)(len - (RUN - 1)))) & ~(int64_t)3) +
-               4 * j;
-      v[i] = *reinterpret_cast<const float4*>(x + pos[i]);
+      live[i] = rb + (int64_t)i * RPP + (threadIdx.x / LPR) < R;
+      v[i] = *reinterpret_cast<const float4*>(x + run_pos(i));
     }
-    if (a.aq) {  // the fused PS step's last client (after every x load is issued)
+    if (AQ) {  // the fused PS step's last client (after every x load is issued)
 #pragma unroll
-      for (int i = 0; i < PASSES; ++i) v[i] = br_value(a, v[i], tb + pos[i], tb + n, t);
+      for (int i = 0; i < PASSES; ++i) v[i] = br_value(a, v[i], tb + run_pos(i), tb + n, t);
     }
 #pragma unroll
     for (int i = 0; i < PASSES; ++i) {
@@ -627,11 +630,14 @@ __device__ __forceinline__ void bracket_sample(const SpecArgs& a, const float* _
   }
 }
 
-__global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, const SpecBrItem* __restrict__ items) {
-  __shared__ double red[kBrWaves];
-  __shared__ uint32_t s_last;
+// WIDE: kBrParts workgroups per tensor, runs of kSpecRunWide (bit widths 5-8); AQ: the fused PS
+// step's last client is added to the sample (narrow only).  One instance per case keeps each small
+// enough for two 1024-thread workgroups per CU (one kernel for all three took 94 VGPRs).
+template <bool WIDE, bool AQ>
+__device__ __forceinline__ void spec_bracket_body(const SpecArgs& a, const SpecBrItem* __restrict__ items,
+                                                  double* red, uint32_t& s_last) {
   // wide levels: kBrParts workgroups per tensor, part g sampling runs [g kSpecRuns, (g + 1) kSpecRuns)
-  const int parts = a.wide ? kBrParts : 1;
+  const int parts = WIDE ? kBrParts : 1;
   const int part = (int)(blockIdx.x % (unsigned)parts);
   const SpecBrItem bi = items[blockIdx.x / (unsigned)parts];  // one scalar load: the tensor's range and strata
   const int32_t t = bi.tensor;
@@ -640,7 +646,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
   const float alpha = a.e.alpha;
   double s1 = 0.0, s2 = 0.0;
   const bool exact = n <= kSpecExact;
-  const int64_t R = a.wide ? (int64_t)bi.Rw : (int64_t)bi.R;
+  const int64_t R = WIDE ? (int64_t)bi.Rw : (int64_t)bi.R;
   // Loads are unconditional (a clamped address, the value masked after): a load under a
   // branch is waited for at the branch's end, which would serialise the round trips.
   if (exact) {  // 4 float4 per thread, all loads in flight
@@ -664,7 +670,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
         }
       }
     }
-    if (a.aq) {  // the fused PS step's last client, added before the divide
+    if (AQ) {  // the fused PS step's last client, added before the divide
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
         const int64_t e = 4 * ((int64_t)i * kBrThreads + threadIdx.x);
@@ -676,8 +682,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     for (int i = 0; i < PER; ++i) acc = sq4(spec_prologue(v[i], alpha, a.divisor, a.e.fmt), acc);
     s1 = acc;
   } else {
-    if (a.wide) bracket_sample<kSpecRunWide>(a, x, t, tb, n, R, part, parts, s1, s2);
-    else bracket_sample<kSpecRun>(a, x, t, tb, n, R, part, parts, s1, s2);
+    bracket_sample<WIDE ? kSpecRunWide : kSpecRun, AQ>(a, x, t, tb, n, R, part, parts, s1, s2);
   }
   if (exact && part != 0) return;  // an exact tensor is one workgroup's
   double S1 = br_sum(s1, red);
@@ -709,7 +714,7 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
   } else {
     const double Rd = (double)R, m = S1 / Rd;
     const double var = fmax(0.0, (S2 - Rd * m * m) / (Rd - 1.0));
-    ss = S1 * ((double)n / ((double)(a.wide ? kSpecRunWide : kSpecRun) * Rd));
+    ss = S1 * ((double)n / ((double)(WIDE ? kSpecRunWide : kSpecRun) * Rd));
     k = (double)a.zsig * sqrt(var / Rd) / m + 0x1p-10;  // 6 sigma of the run-sum estimate + 0.1 %
   }
   // bf16 / fp16 values: the norm is rounded to the format (at most half an ulp: 2^-8 / 2^-11
@@ -733,6 +738,21 @@ __global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, cons
     }
   }
   a.br[t] = o;
+}
+
+template <bool WIDE, bool AQ>
+__global__ __launch_bounds__(kBrThreads) void qsgd_spec_bracket(SpecArgs a, const SpecBrItem* __restrict__ items) {
+  __shared__ double red[kBrWaves];
+  __shared__ uint32_t s_last;
+  spec_bracket_body<WIDE, AQ>(a, items, red, s_last);
+}
+// wide levels: two 1024-thread workgroups per CU (<= 64 VGPRs), so the kBrParts workgroups per
+// tensor run in one generation
+__global__ __launch_bounds__(kBrThreads) __attribute__((amdgpu_waves_per_eu(8))) void qsgd_spec_bracket_wide(
+    SpecArgs a, const SpecBrItem* __restrict__ items) {
+  __shared__ double red[kBrWaves];
+  __shared__ uint32_t s_last;
+  spec_bracket_body<true, false>(a, items, red, s_last);
 }
 
 // Levels of a quad for every norm of the bracket; und: some element is undecided.  u == 0 is
@@ -1030,9 +1050,9 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_finish(SpecArgs a, const S
       // this thread's first PRE listed quads (index, recorded x and draws) are loaded before the
       // norm wait, so their round trip overlaps it (clamped to the last listed quad: no load
       // under a branch); the rest, if any (narrow lists only), in the loop after
-      constexpr int PRE = FT > 1 ? PW / FT : 2;
-      uint32_t qv[PRE];
-      float4 rx[PRE], ru[PRE];
+      constexpr int PRE = FT > 1 ? PW / FT : 0;  // (narrow lists: usually empty, the loop below)
+      uint32_t qv[PRE > 0 ? PRE : 1];
+      float4 rx[PRE > 0 ? PRE : 1], ru[PRE > 0 ? PRE : 1];
       const uint32_t jl = cnt > 0u ? cnt - 1u : 0u;
 #pragma unroll
       for (int k = 0; k < PRE; ++k) {
@@ -1539,6 +1559,10 @@ struct omf_plan {
   uint32_t spec_epoch = 0;
   uint32_t spec_skip = 0;  // test / experiment switches (omf_plan_set_debug), 0 in production
   float spec_zsig = 6.0f;  // experiment switch (OMF_SPEC_ZSIG): the bracket's width in sigmas
+  // wide levels: 5 sigmas (a tensor whose norm falls outside is requantised whole, exactly; the
+  // narrower bracket lists fewer undecided quads: Llama-400M s = 8 encode 0.601-0.611 ms against
+  // 0.616-0.622 at 6, profiles/r05_s8_variants.txt)
+  float spec_zsig_wide = 5.0f;
   SpecBracket* d_spec_br = nullptr;
   uint64_t* d_spec_ngran = nullptr;  // per tensor {epoch << 1 | bad, norm} granules of the fold
   uint64_t* d_spec_part = nullptr;
@@ -2067,7 +2091,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     if (const char* dg = getenv("OMF_RING_DBG")) p->ring_dbg = (uint32_t)atoi(dg);
     if (const char* sk = getenv("OMF_SPEC_SKIP")) p->spec_skip = (uint32_t)atoi(sk);
 #endif
-    if (const char* zs = getenv("OMF_SPEC_ZSIG")) p->spec_zsig = std::max(1.0f, (float)atof(zs));
+    if (const char* zs = getenv("OMF_SPEC_ZSIG")) p->spec_zsig = p->spec_zsig_wide = std::max(1.0f, (float)atof(zs));
     // Default strategy by arena size: the bracketed single-read encoder from 2^25 elements
     // (Llama-400M 0.386 ms against the two-pass 0.59 and the ring 0.63; Llama-150M 0.25 against
     // 0.35), the ring below (ResNet-18: 0.032 ms against 0.08 for the bracket's four launches).
@@ -2365,7 +2389,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     sa.wide = s > kSpecMaxBits ? 1u : 0u;
     sa.ngran = p->d_spec_ngran;
     sa.dbg = p->spec_skip;
-    sa.zsig = p->spec_zsig;
+    sa.zsig = s > kSpecMaxBits ? p->spec_zsig_wide : p->spec_zsig;
     sa.divisor = divisor;
     sa.xout = xout;
     sa.wait_ticks = p->wait_ticks;
@@ -2398,7 +2422,11 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     // p->spec_skip: test / experiment switches (omf_plan_set_debug; 0 in production): bit 0
     // skips the bracket launch (the previous brackets stay), bit 1 the finish launch, bits 2/3
     // the fix stores / the fix, bit 4 the fold — the payload is then not the encoder's.
-    if (!(p->spec_skip & 1u)) hipLaunchKernelGGL(qsgd_spec_bracket, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
+    if (!(p->spec_skip & 1u)) {
+      if (wide) hipLaunchKernelGGL(qsgd_spec_bracket_wide, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
+      else if (sa.aq) hipLaunchKernelGGL((qsgd_spec_bracket<false, true>), gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
+      else hipLaunchKernelGGL((qsgd_spec_bracket<false, false>), gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
+    }
     const bool div = divisor != 0.0f;
     const float* an = sa.anorm;
     const int aw = acc_in ? (acc_in->width == 32 ? 4 : 1) : 0;
@@ -2422,7 +2450,10 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     }
     const int32_t nfold = (int32_t)p->n_spec_fold;
     if (wide) {
-      constexpr int FT = 4, BPW = kThreads / (kWaves * FT);  // fix: 16 blocks per workgroup
+#ifndef OMF_FIX_FT  // experiment builds may override it (scripts/exp/s8_variants.sh)
+#define OMF_FIX_FT 4
+#endif
+      constexpr int FT = OMF_FIX_FT, BPW = kThreads / (kWaves * FT);  // fix: 16 blocks per workgroup
       const dim3 gw((unsigned)(nfold + (p->n_spec_blocks + BPW - 1) / BPW));
       if (width == 1)
         hipLaunchKernelGGL((qsgd_spec_finish<1, PWW, FT>), gw, blk, 0, st, sa, (const SpecFoldItem*)sa.fold_items, nfold,
