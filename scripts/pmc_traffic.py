@@ -34,6 +34,8 @@ TOPK_DECODE = ("topk_dec_place", "topk_dec_tiles", "topk_dec_overflow")
 
 
 def short(name):
+    if "qsgd_spec_bracket_wide(" in name:  # the wide-level bracket kernel (bit widths 5-8)
+        return "qsgd_spec_bracket"
     for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_encode_grid", "qsgd_decode_flat",
               "qsgd_decode_arena", "qsgd_quant_sub",
               "qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_finish",
