@@ -41,6 +41,7 @@ SIGNATURES = {
     "omf_plan_encode_strategy": (_c_i32, [_c_p]),
     "omf_plan_last_encoder": (_c_i32, [_c_p]),
     "omf_plan_set_wide_levels": (ctypes.c_int, [_c_p, _c_i32]),
+    "omf_plan_set_fused_bracket": (ctypes.c_int, [_c_p, _c_i32]),
     "omf_plan_resident_capacity": (_c_i64, [_c_p]),
     "omf_plan_set_resident_capacity": (ctypes.c_int, [_c_p, _c_i64, _c_i64]),
     "omf_plan_set_ring": (ctypes.c_int, [_c_p, _c_i32, _c_i32, _c_i64, _c_i64]),

@@ -211,6 +211,12 @@ class Plan:
         with self._lock:
             check(lib().omf_plan_set_wide_levels(self._h, 1 if on else 0), "omf_plan_set_wide_levels")
 
+    def set_fused_bracket(self, on: bool) -> None:
+        """The bracketed encoder's bracket folded into its pass (omf_plan_set_fused_bracket);
+        identical payloads."""
+        with self._lock:
+            check(lib().omf_plan_set_fused_bracket(self._h, 1 if on else 0), "omf_plan_set_fused_bracket")
+
     @property
     def last_encoder(self) -> str:
         """The encoder the latest encode launched (omf_plan_last_encoder): one of STRATEGIES,

@@ -476,7 +476,8 @@ struct SpecArgs {
   float* xout;
   uint32_t epoch;          // per-launch tag (never 0)
   uint32_t wide;           // wide levels: the bracket samples Rw runs (SpecBrItem), kBrParts workgroups per tensor
-  double* br_part;         // wide: per (tensor, part) the partial {S1, S2}
+  double* br_part;         // wide / fused bracket: per (tensor, part) the partial {S1, S2}
+  uint64_t* brgran;        // fused bracket: per tensor {epoch, c_lo} and {epoch, c_hi}
   uint32_t* br_cnt;        // wide: per tensor arrival counter (reset by the last arriver)
   int64_t nblocks;
   // Fused last-client decode-accumulate (omf_ps_accumulate_apply_encode; aq == NULL: none): before
@@ -592,10 +593,10 @@ __device__ __forceinline__ double br_sum(double v, double* lds) {
 // balanced strata (of >= 2 RUN elements); a run is RUN / 4 float4 loaded by consecutive lanes, 8
 // passes per round (their loads in flight together); this workgroup takes the rounds part, part +
 // parts, ...  Per run: s1 += its sum of squares, s2 += its square (in lane 0 of the run).
-template <int RUN, bool AQ>
+template <int RUN, bool AQ, int NT = kBrThreads, int PASSES = 8>
 __device__ __forceinline__ void bracket_sample(const SpecArgs& a, const float* __restrict__ x, int32_t t, int64_t tb,
                                                int64_t n, int64_t R, int part, int parts, double& s1, double& s2) {
-  constexpr int LPR = RUN / 4, RPP = kBrThreads / LPR, PASSES = 8, PER_ROUND = RPP * PASSES;
+  constexpr int LPR = RUN / 4, RPP = NT / LPR, PER_ROUND = RPP * PASSES;
   const int64_t base = n / R, rem = n % R;
   const int j = threadIdx.x & (LPR - 1);
   const float alpha = a.e.alpha;
@@ -633,6 +634,9 @@ __device__ __forceinline__ void bracket_sample(const SpecArgs& a, const float* _
 // WIDE: kBrParts workgroups per tensor, runs of kSpecRunWide (bit widths 5-8); AQ: the fused PS
 // step's last client is added to the sample (narrow only).  One instance per case keeps each small
 // enough for two 1024-thread workgroups per CU (one kernel for all three took 94 VGPRs).
+__device__ SpecBracket bracket_from_sums(const SpecArgs& a, bool exact, int64_t n, int64_t R, int run, double S1,
+                                         double S2);
+
 template <bool WIDE, bool AQ>
 __device__ __forceinline__ void spec_bracket_body(const SpecArgs& a, const SpecBrItem* __restrict__ items,
                                                   double* red, uint32_t& s_last) {
@@ -707,6 +711,12 @@ __device__ __forceinline__ void spec_bracket_body(const SpecArgs& a, const SpecB
     }
   }
   if (threadIdx.x != 0) return;
+  a.br[t] = bracket_from_sums(a, exact, n, R, WIDE ? kSpecRunWide : kSpecRun, S1, S2);
+}
+
+// The bracket of a tensor from its sample's sums (exact: S1 is the whole tensor's sum of squares).
+__device__ SpecBracket bracket_from_sums(const SpecArgs& a, bool exact, int64_t n, int64_t R, int run, double S1,
+                                         double S2) {
   double ss, k;
   if (exact) {
     ss = S1;
@@ -714,7 +724,7 @@ __device__ __forceinline__ void spec_bracket_body(const SpecArgs& a, const SpecB
   } else {
     const double Rd = (double)R, m = S1 / Rd;
     const double var = fmax(0.0, (S2 - Rd * m * m) / (Rd - 1.0));
-    ss = S1 * ((double)n / ((double)(WIDE ? kSpecRunWide : kSpecRun) * Rd));
+    ss = S1 * ((double)n / ((double)run * Rd));
     k = (double)a.zsig * sqrt(var / Rd) / m + 0x1p-10;  // 6 sigma of the run-sum estimate + 0.1 %
   }
   // bf16 / fp16 values: the norm is rounded to the format (at most half an ulp: 2^-8 / 2^-11
@@ -737,7 +747,7 @@ __device__ __forceinline__ void spec_bracket_body(const SpecArgs& a, const SpecB
       o.mode = 0u;
     }
   }
-  a.br[t] = o;
+  return o;
 }
 
 template <bool WIDE, bool AQ>
@@ -817,9 +827,9 @@ __device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t 
 // One block's pass: loads issued first, the Philox draws (independent of x) computed while
 // they are in flight, then the partial, the levels and the undecided list.  FULL: a whole
 // 4 Ki block (straight-line code, no bounds checks).
-template <int WIDTH, bool FULL, bool DIV, uint32_t FMT, int AW = 0, int PW = kSpecPerWave>
-__device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t end, int32_t t, int64_t tb,
-                                           const SpecBracket& br, uint32_t* slot, uint64_t* part, float anorm) {
+template <int WIDTH, bool FULL, bool DIV, uint32_t FMT, int AW = 0, int PW = kSpecPerWave, class GetBr>
+__device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t blk, int64_t b, int64_t end, int32_t t,
+                                           int64_t tb, GetBr get_br, uint32_t* slot, uint64_t* part, float anorm) {
   const EncArgs& e = a.e;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float4 v[kSpecV];
@@ -871,6 +881,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
     }
     acc = sq4(v[k], acc);
   }
+  const SpecBracket br = get_br();  // (the fused-bracket pass polls for it here, its loads in flight)
   uint32_t cnt = 0;  // wave-uniform
   {
     uint32_t* list = slot + PW * wave;
@@ -888,7 +899,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
         const uint32_t pos = cnt + (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
         if (live && und && pos < (uint32_t)PW) {  // the quad, its x and its draws: no re-read
           list[pos] = (uint32_t)(el >> 2);
-          float4* rec = a.recs + 2 * ((blockIdx.x * kWaves + wave) * PW + pos);
+          float4* rec = a.recs + 2 * ((blk * kWaves + wave) * PW + pos);
           rec[0] = v[k];
           rec[1] = uu[k];
         }
@@ -899,7 +910,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t b, int64_t
   const double s = wave_sum_f64((double)acc);
   if (lane == 0) {
     *part = (uint64_t)__double_as_longlong(s);
-    a.heads[blockIdx.x * kWaves + wave] = ((uint32_t)t << 8) | min(cnt, (uint32_t)PW);
+    a.heads[blk * kWaves + wave] = ((uint32_t)t << 8) | min(cnt, (uint32_t)PW);
     if (cnt > (uint32_t)PW)
       __hip_atomic_fetch_or(&a.flags[t], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -928,8 +939,128 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const Sp
     return;
   }
   const int64_t end = min(b + kSpecBlk, it.end);
-  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, FMT, AW, PW>(a, b, end, it.tensor, tb, br, slot, part, anorm);
-  else spec_block<WIDTH, false, DIV, FMT, AW, PW>(a, b, end, it.tensor, tb, br, slot, part, anorm);
+  auto get_br = [&]() { return br; };
+  if (end - b == kSpecBlk)
+    spec_block<WIDTH, true, DIV, FMT, AW, PW>(a, blk, b, end, it.tensor, tb, get_br, slot, part, anorm);
+  else
+    spec_block<WIDTH, false, DIV, FMT, AW, PW>(a, blk, b, end, it.tensor, tb, get_br, slot, part, anorm);
+}
+
+// Fused bracket (OMF_SPEC_FB / omf_plan_set_fused_bracket): the bracket launch folded into the pass.
+// Its first kFbParts x (bracket items) workgroups sample the tensors (256 threads each, an eighth of
+// a tensor's runs; the last part to arrive combines the sums and publishes the multipliers as two
+// {epoch, value} granules); the rest are the pass's blocks, which issue their loads and draws and
+// then poll their tensor's granules.  The bracket workgroups have the lowest ids, so they are
+// dispatched before any pass block and never wait; a pass block's poll is bounded anyway (20 ms and a
+// minimum of polls): on expiry the tensor is flagged and requantised whole by the finish — exact.
+constexpr int kFbParts = 8;  // 64 runs each: four float4 per thread (the pass's blocks' register budget)
+
+__device__ __forceinline__ void spec_bracket_part(const SpecArgs& a, const SpecBrItem* __restrict__ items, int64_t wg) {
+  __shared__ double red[kWaves];
+  __shared__ uint32_t s_last;
+  const int part = (int)(wg % kFbParts);
+  const SpecBrItem bi = items[wg / kFbParts];
+  const int32_t t = bi.tensor;
+  const int64_t tb = bi.begin, n = bi.n, R = bi.R;
+  const float* __restrict__ x = a.e.x + tb;
+  const bool exact = n <= kSpecExact;
+  if (exact && part != 0) return;
+  double s1 = 0.0, s2 = 0.0;
+  if (exact) {  // 16 Ki elements at most: up to four rounds of four float4 per thread
+    for (int64_t r0 = 0; r0 < n; r0 += 16 * kThreads) {
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t e = r0 + 4 * ((int64_t)i * kThreads + threadIdx.x);
+        v[i] = e + 4 <= n ? *reinterpret_cast<const float4*>(x + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < n && e + 4 > n) {  // the tensor's partial last quad
+          v[i].x = x[e];
+          if (e + 1 < n) v[i].y = x[e + 1];
+          if (e + 2 < n) v[i].z = x[e + 2];
+        }
+      }
+      float acc = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc = sq4(spec_prologue(v[i], a.e.alpha, a.divisor, a.e.fmt), acc);
+      s1 += (double)acc;
+    }
+  } else {
+    bracket_sample<kSpecRun, false, kThreads, 4>(a, x, t, tb, n, R, part, kFbParts, s1, s2);
+  }
+  double S1 = block_sum_f64(s1, red), S2 = block_sum_f64(s2, red);
+  if (!exact) {  // the last part to arrive combines the partials in part order
+    if (threadIdx.x == 0) {
+      double* bp = a.br_part + 2 * ((int64_t)t * kFbParts + part);
+      st_agent(reinterpret_cast<uint64_t*>(bp), (uint64_t)__double_as_longlong(S1));
+      st_agent(reinterpret_cast<uint64_t*>(bp + 1), (uint64_t)__double_as_longlong(S2));
+      drain_vmem();
+      const uint32_t last = add_agent(&a.br_cnt[t], 1u) == (uint32_t)(kFbParts - 1) ? 1u : 0u;
+      if (last) __hip_atomic_store(&a.br_cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    S1 = S2 = 0.0;
+    for (int g = 0; g < kFbParts; ++g) {
+      const uint64_t* bp = reinterpret_cast<const uint64_t*>(a.br_part + 2 * ((int64_t)t * kFbParts + g));
+      S1 += __longlong_as_double((long long)ld_agent(bp));
+      S2 += __longlong_as_double((long long)ld_agent(bp + 1));
+    }
+  }
+  if (threadIdx.x != 0) return;
+  const SpecBracket o = bracket_from_sums(a, exact, n, R, kSpecRun, S1, S2);
+  a.br[t] = o;  // the finish launch reads it (a later launch)
+  const uint64_t ep = (uint64_t)a.epoch << 32;
+  st_agent(&a.brgran[2 * t], ep | __float_as_uint(o.c_lo));
+  st_agent(&a.brgran[2 * t + 1], ep | __float_as_uint(o.c_hi));
+}
+
+template <int WIDTH, bool DIV>
+__global__ __launch_bounds__(kThreads) void qsgd_spec_quant_fb(SpecArgs a, const SpecBrItem* __restrict__ bitems,
+                                                               int64_t nbrw, const int64_t* __restrict__ begins) {
+  if ((int64_t)blockIdx.x < nbrw) {
+    spec_bracket_part(a, bitems, blockIdx.x);
+    return;
+  }
+  const int64_t blk = (int64_t)blockIdx.x - nbrw;
+  const Item it = a.e.items[blk >> 2];
+  const int32_t t = it.tensor;
+  const int64_t tb = begins[t];
+  const int64_t b = it.begin + (blk & 3) * kSpecBlk;
+  const int wave = threadIdx.x >> 6;
+  uint32_t* slot = a.slots + blk * kSpecSlot;
+  uint64_t* part = a.partials + blk * kWaves + wave;
+  if (b >= it.end) {
+    if ((threadIdx.x & 63) == 0) {
+      *part = 0ull;
+      a.heads[blk * kWaves + wave] = (uint32_t)t << 8;
+    }
+    return;
+  }
+  auto get_br = [&]() {
+    uint64_t g0 = ld_agent(&a.brgran[2 * t]), g1 = ld_agent(&a.brgran[2 * t + 1]);
+    if ((uint32_t)(g0 >> 32) != a.epoch || (uint32_t)(g1 >> 32) != a.epoch) {
+      const uint64_t t0 = wall_clock64(), min_polls = a.wait_ticks >> 10;
+      uint64_t polls = 0;
+      for (int k = 0;; k = min(k + 1, 6)) {
+        if (k < 2) __builtin_amdgcn_s_sleep(2);
+        else __builtin_amdgcn_s_sleep(8);
+        g0 = ld_agent(&a.brgran[2 * t]);
+        g1 = ld_agent(&a.brgran[2 * t + 1]);
+        if ((uint32_t)(g0 >> 32) == a.epoch && (uint32_t)(g1 >> 32) == a.epoch) break;
+        if (++polls > min_polls && wall_clock64() - t0 > a.wait_ticks) {  // never expected: requantise whole
+          __hip_atomic_fetch_or(&a.flags[t], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          g0 = g1 = 0;
+          break;
+        }
+      }
+    }
+    SpecBracket o{__uint_as_float((uint32_t)g0), __uint_as_float((uint32_t)g1), 0.f, 0.f, 0u, {0u, 0u, 0u}};
+    return o;
+  };
+  const int64_t end = min(b + kSpecBlk, it.end);
+  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, kFmtF32>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f);
+  else spec_block<WIDTH, false, DIV, kFmtF32>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f);
 }
 
 // One fold segment (a workgroup of the finish launch); the last arriver of the tensor folds the
@@ -1573,6 +1704,13 @@ struct omf_plan {
   float4* d_spec_recs_w = nullptr;     // wide encode (bit_width 5-8)
   double* d_spec_br_part = nullptr;    // wide: the bracket parts' partial sums and arrival counters
   uint32_t* d_spec_br_cnt = nullptr;
+  // the fused-bracket pass (OMF_SPEC_FB=0 / omf_plan_set_fused_bracket turn it off): Llama-400M s = 4
+  // step 0.6977-0.7021 ms against 0.7009-0.7067 with the bracket's own launch (three interleaved
+  // pairs), the encode alone unchanged (0.348-0.360 both); profiles/r05_fused_bracket_ab.txt
+  int32_t spec_fb = 1;
+  double* d_spec_fb_part = nullptr;    // its parts' partial sums, arrival counters and granules
+  uint32_t* d_spec_fb_cnt = nullptr;
+  uint64_t* d_spec_brgran = nullptr;
   int32_t spec_last_pw = kSpecPerWave;  // the list capacity of the latest bracketed encode
   int32_t spec_wide = 1;  // wide levels (5-8 bits, fp32) through the bracket (1) or as before (0): OMF_SPEC_WIDE
   // arena-aligned decoder: per 4 Ki block, tensor id | (1 << 31 when inside it)
@@ -2098,6 +2236,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     p->strategy = p->arena_end >= ((int64_t)1 << 25) ? 3 : 2;
     if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 4));
     if (const char* sw = getenv("OMF_SPEC_WIDE")) p->spec_wide = atoi(sw) != 0 ? 1 : 0;
+    if (const char* fb = getenv("OMF_SPEC_FB")) p->spec_fb = atoi(fb) != 0 ? 1 : 0;
     {  // grid encoder: one 1024-thread workgroup per CU must fit
       int nb = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)qsgd_encode_grid<1>, 1024, 0) == hipSuccess &&
@@ -2128,6 +2267,9 @@ int omf_plan_destroy(omf_plan* plan) {
   if (plan->d_spec_recs_w) (void)hipFree(plan->d_spec_recs_w);
   if (plan->d_spec_br_part) (void)hipFree(plan->d_spec_br_part);
   if (plan->d_spec_br_cnt) (void)hipFree(plan->d_spec_br_cnt);
+  if (plan->d_spec_fb_part) (void)hipFree(plan->d_spec_fb_part);
+  if (plan->d_spec_fb_cnt) (void)hipFree(plan->d_spec_fb_cnt);
+  if (plan->d_spec_brgran) (void)hipFree(plan->d_spec_brgran);
   for (auto& e : plan->topk_tables) (void)hipFree(e.dev);
   delete plan;
   return OMF_OK;
@@ -2142,6 +2284,11 @@ int64_t omf_plan_encode_items(const omf_plan* plan) {
 
 int32_t omf_plan_encode_strategy(const omf_plan* plan) { return plan ? plan->strategy : -1; }
 int32_t omf_plan_last_encoder(const omf_plan* plan) { return plan ? plan->last_encoder : -1; }
+int omf_plan_set_fused_bracket(omf_plan* plan, int32_t on) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  plan->spec_fb = on != 0 ? 1 : 0;
+  return OMF_OK;
+}
 int omf_plan_set_wide_levels(omf_plan* plan, int32_t on) {
   if (!plan) return fail(OMF_EINVAL, "plan is NULL");
   plan->spec_wide = on != 0 ? 1 : 0;
@@ -2403,8 +2550,17 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
       OMF_HIP(hipMalloc(&p->d_spec_br_cnt, 4 * (size_t)p->nt));
       OMF_HIP(hipMemsetAsync(p->d_spec_br_cnt, 0, 4 * (size_t)p->nt, st));  // left zero by every launch
     }
-    sa.br_part = p->d_spec_br_part;
-    sa.br_cnt = p->d_spec_br_cnt;
+    const bool fb = p->spec_fb && !wide && !acc_in && fmt == 0 && width == 1 && !(p->spec_skip & 1u);
+    if (fb && !p->d_spec_fb_part) {  // once per plan: the fused bracket's sums, counters and granules
+      OMF_HIP(hipMalloc(&p->d_spec_fb_part, 16 * (size_t)kFbParts * (size_t)p->nt));
+      OMF_HIP(hipMalloc(&p->d_spec_fb_cnt, 4 * (size_t)p->nt));
+      OMF_HIP(hipMalloc(&p->d_spec_brgran, 16 * (size_t)p->nt));
+      OMF_HIP(hipMemsetAsync(p->d_spec_fb_cnt, 0, 4 * (size_t)p->nt, st));  // left zero by every launch
+      OMF_HIP(hipMemsetAsync(p->d_spec_brgran, 0, 16 * (size_t)p->nt, st));  // epoch 0 is never a launch's
+    }
+    sa.br_part = fb ? p->d_spec_fb_part : p->d_spec_br_part;
+    sa.br_cnt = fb ? p->d_spec_fb_cnt : p->d_spec_br_cnt;
+    sa.brgran = p->d_spec_brgran;
     p->spec_last_pw = wide ? kSpecPerWaveWide : kSpecPerWave;
     sa.slots = wide ? p->d_spec_slots_w : p->d_spec_slots;
     sa.heads = p->d_spec_heads;
@@ -2422,16 +2578,23 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     // p->spec_skip: test / experiment switches (omf_plan_set_debug; 0 in production): bit 0
     // skips the bracket launch (the previous brackets stay), bit 1 the finish launch, bits 2/3
     // the fix stores / the fix, bit 4 the fold — the payload is then not the encoder's.
-    if (!(p->spec_skip & 1u)) {
+    const bool div = divisor != 0.0f;
+    if (fb) {  // the bracket folded into the pass (its first workgroups)
+      const int64_t nbrw = (int64_t)kFbParts * p->n_spec_br;
+      const dim3 gfb((unsigned)(nbrw + p->n_spec_blocks));
+      if (div) hipLaunchKernelGGL((qsgd_spec_quant_fb<1, true>), gfb, blk, 0, st, sa, sa.br_items, nbrw, sa.begins);
+      else hipLaunchKernelGGL((qsgd_spec_quant_fb<1, false>), gfb, blk, 0, st, sa, sa.br_items, nbrw, sa.begins);
+    } else if (!(p->spec_skip & 1u)) {
       if (wide) hipLaunchKernelGGL(qsgd_spec_bracket_wide, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
       else if (sa.aq) hipLaunchKernelGGL((qsgd_spec_bracket<false, true>), gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
       else hipLaunchKernelGGL((qsgd_spec_bracket<false, false>), gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
     }
-    const bool div = divisor != 0.0f;
     const float* an = sa.anorm;
     const int aw = acc_in ? (acc_in->width == 32 ? 4 : 1) : 0;
     constexpr int PWW = kSpecPerWaveWide;
-    if (wide) {  // fp32, no fused last client (spec_serves)
+    if (fb) {
+      // (the pass ran above)
+    } else if (wide) {  // fp32, no fused last client (spec_serves)
       if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
       else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
       else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);

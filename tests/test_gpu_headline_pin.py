@@ -132,3 +132,33 @@ def test_wide_levels_against_the_oracle(gpu, s):
     with ThreadPoolExecutor(_threads()) as ex:
         errors = [e for e in ex.map(check, range(len(sizes))) if e]
     assert not errors, errors[:5]
+
+
+@pytest.mark.parametrize("cfg", ["llama400m", "llama150m"])
+def test_fused_bracket_equals_bracket_launch(gpu, cfg):
+    """The bracket folded into the pass (omf_plan_set_fused_bracket: its first workgroups sample, the
+    pass's blocks poll for their tensor's bracket) writes the payload, norms and — for the fused PS
+    step — the average of the separate bracket launch, bit for bit (weighted, s = 3 and 4)."""
+    named = shapes.model_shapes(cfg)
+    sizes = [shapes.numel(sh) for _, sh in named]
+    plan = codec.Plan(sizes, device=gpu)
+    assert plan.strategy == "bracket"
+    g = torch.Generator(device=gpu)
+    g.manual_seed(5)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    for s in (3, 4):
+        outs = []
+        for fb in (False, True):
+            plan.set_fused_bracket(fb)
+            q, n = plan.qsgd_encode(x, s, alpha=2.0, seed=3, offset=s)
+            st = plan.spec_stats()
+            avg, qa, na = plan.ps_apply_encode(x, 7.0, s, seed=3, offset=10 + s)
+            plan.check()
+            outs.append((q, n, avg, qa, na, st))
+        plan.set_fused_bracket(False)
+        (q1, n1, a1, qa1, na1, st1), (q2, n2, a2, qa2, na2, st2) = outs
+        assert st2["whole"] == 0 and st2["listed"] > 0, st2
+        assert torch.equal(n1, n2) and torch.equal(na1, na2)
+        for o, k in zip(plan.offsets, sizes):
+            assert torch.equal(q1[o:o + k], q2[o:o + k]) and torch.equal(qa1[o:o + k], qa2[o:o + k])
+            assert torch.equal(a1[o:o + k], a2[o:o + k])
