@@ -371,7 +371,8 @@ def main():
         achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
         traffic, tsrc = pmc_traffic(dom_name, args.config, s)
         if dom_name == "qsgd_spec_all":  # the whole bracketed encode call, timed as one unit
-            dom_name = "omf_qsgd_encode = qsgd_spec_bracket + qsgd_spec_quant + qsgd_spec_finish"
+            dom_name = ("omf_qsgd_encode = qsgd_spec_bracket + qsgd_spec_quant + qsgd_spec_finish"
+                        " (at widths <= 4 the bracket runs as qsgd_spec_quant_fb's first workgroups)")
         qsgd = {
             "value": world * alg_bytes_step * args.steps / dt / 1e9, "ms_per_step": dt / args.steps * 1e3,
             "alg_bytes_step": alg_bytes_step,
@@ -409,6 +410,7 @@ def main():
 
         for i in range(args.warmup):
             t_step(i)
+        plan.topk_stats(reset=True)
         steps_t = args.steps if args.codec == "topk" else max(5, args.steps // 2)
         dtt = timed(t_step, args.warmup, steps_t)
         alg_t = 16 * N + 24 * K
@@ -425,7 +427,8 @@ def main():
                              "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": t_traffic, "traffic_source": t_tsrc,
                              "kernel": "omf_topk_encode (all launches of one call, host sync included)",
                              "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(tenc, 4),
-                             "decode_ms": round(tdec, 4)}}
+                             "decode_ms": round(tdec, 4)},
+                "encoder_paths": plan.topk_stats()}  # timed calls: bucket-sort fast path vs fallbacks
         del res, yt, xs
 
     extras = {}

@@ -979,6 +979,9 @@ __global__ __launch_bounds__(kThreads) void topk_restore(const uint64_t* __restr
 
 // Fast path, pass H: the exact fine-bin histogram of every tensor's candidates (LDS counts per
 // super-item, flushed with one global atomic per touched bin).
+#ifndef OMF_FHIST_U  // 4: measured against 8 (30.9 us, more VGPRs) on Llama-400M
+#define OMF_FHIST_U 4
+#endif
 __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restrict__ cand,
                                                        const Item* __restrict__ items,
                                                        const uint32_t* __restrict__ sub_cnt,
@@ -996,7 +999,7 @@ __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restric
   v.init(supinfo, items, sub_cnt, fmap, s_map, s_part, sup0 + blockIdx.x);
   const uint32_t lo = tlo[v.t], F = fcount[v.t];
   const uint32_t* map_t = s_map;
-  constexpr int U = 4;
+  constexpr int U = OMF_FHIST_U;  // key loads in flight per thread
   for (uint32_t e0 = threadIdx.x; e0 < v.total; e0 += U * 1024) {
     uint64_t key[U];
 #pragma unroll
@@ -1157,7 +1160,15 @@ __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const ui
 // region kb2[t] of the bucket buffer).  Per super-item: LDS counts per bucket, one global
 // reservation per touched bucket, then LDS ranks.  Order inside a bucket is arbitrary (the
 // bucket sort orders by the full key).
-__global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __restrict__ cand,
+// SMALL (every tensor of the launch has <= kScatterSmallB bucket slots): the tensor's bucket
+// table is staged in LDS as 16-bit entries, so the per-key bucket lookup is an LDS read instead
+// of a global load that waits on the key load (two such round trips per key otherwise).
+constexpr uint32_t kScatterSmallB = 4096;
+#ifndef OMF_SCATTER_CACHE  // key loads per thread (x4) kept in registers between the two phases
+#define OMF_SCATTER_CACHE 3
+#endif
+template <bool SMALL>
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void topk_bucket_scatter(const uint64_t* __restrict__ cand,
                                                             const Item* __restrict__ items,
                                                             const uint32_t* __restrict__ sub_cnt,
                                                             const uint4* __restrict__ supinfo,
@@ -1174,7 +1185,8 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
                                                             const uint32_t* __restrict__ status,
                                                             const uint32_t* __restrict__ thi, uint32_t sup0) {
   if (status[1] | status[2]) return;  // the plan's verdict is a fallback: nothing to do
-  __shared__ uint32_t s_b[kPlanMaxBuckets];
+  __shared__ uint32_t s_b[SMALL ? kScatterSmallB : kPlanMaxBuckets];
+  __shared__ int16_t s_fb[SMALL ? kFineMax : 1];
   __shared__ uint32_t s_spre[1025], s_part[1024];
   __shared__ int64_t s_ibeg[kSupItems];
   __shared__ uint32_t s_map[kCoarse];
@@ -1184,37 +1196,59 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
   const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nb = bbase[t + 1] - b0, hi = thi[t];
   const int64_t base = tbegin[t];
   for (uint32_t j = threadIdx.x; j < nb; j += 1024) s_b[j] = 0;
-  __syncthreads();
   const uint32_t* map_t = s_map;
   const int32_t* fb = fbucket + (size_t)t * kFineMax;
+  if (SMALL)
+    for (uint32_t j = threadIdx.x; j < F; j += 1024) s_fb[j] = (int16_t)fb[j];
+  __syncthreads();
   constexpr int U = 4;
+  // SMALL: the first CI x U keys of each thread (and their buckets) stay in registers from the
+  // count phase to the place phase, so most keys are read from memory once, not twice
+  constexpr int CI = SMALL ? OMF_SCATTER_CACHE : 0;
+  uint64_t* dst = bkeys + kb2[t];
+  const auto load = [&](uint32_t e0, uint64_t (&key)[U], int32_t (&j)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e = min(e0 + (uint32_t)u * 1024, v.total - 1);
+      key[u] = cand[v.pos(e)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t f = fine_bin((uint32_t)key[u] & 0x7fffffffu, lo, map_t, F);
+      j[u] = SMALL ? (int32_t)s_fb[f] : fb[f];
+    }
+  };
+  const auto visit = [&](int phase, uint32_t e0, const uint64_t (&key)[U], const int32_t (&j)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (e0 + (uint32_t)u * 1024 >= v.total) continue;
+      if (j[u] < 0) {  // below the k-th key's bin: not selected (a "sure" key gets its t' back)
+        if (phase == 1 && r && ((uint32_t)key[u] & 0x7fffffffu) >= hi)
+          r[base + (key[u] >> 32)] = __uint_as_float((uint32_t)key[u]);
+        continue;
+      }
+      if (phase == 0) {
+        atomicAdd(&s_b[j[u]], 1u);
+      } else {
+        const uint32_t p = atomicAdd(&s_b[j[u]], 1u);
+        dst[p] = key[u];
+      }
+    }
+  };
+  uint64_t ck[CI > 0 ? CI : 1][U];
+  int32_t cj[CI > 0 ? CI : 1][U];
+#pragma unroll
+  for (int i = 0; i < CI; ++i)
+    if (threadIdx.x + (uint32_t)i * U * 1024 < v.total) load(threadIdx.x + (uint32_t)i * U * 1024, ck[i], cj[i]);
   for (int phase = 0; phase < 2; ++phase) {  // 0: count per bucket; 1: place
-    uint64_t* dst = bkeys + kb2[t];
-    for (uint32_t e0 = threadIdx.x; e0 < v.total; e0 += U * 1024) {
+#pragma unroll
+    for (int i = 0; i < CI; ++i)
+      if (threadIdx.x + (uint32_t)i * U * 1024 < v.total) visit(phase, threadIdx.x + (uint32_t)i * U * 1024, ck[i], cj[i]);
+    for (uint32_t e0 = threadIdx.x + (uint32_t)CI * U * 1024; e0 < v.total; e0 += U * 1024) {
       uint64_t key[U];
       int32_t j[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const uint32_t e = min(e0 + (uint32_t)u * 1024, v.total - 1);
-        key[u] = cand[v.pos(e)];
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) j[u] = fb[fine_bin((uint32_t)key[u] & 0x7fffffffu, lo, map_t, F)];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (e0 + (uint32_t)u * 1024 >= v.total) continue;
-        if (j[u] < 0) {  // below the k-th key's bin: not selected (a "sure" key gets its t' back)
-          if (phase == 1 && r && ((uint32_t)key[u] & 0x7fffffffu) >= hi)
-            r[base + (key[u] >> 32)] = __uint_as_float((uint32_t)key[u]);
-          continue;
-        }
-        if (phase == 0) {
-          atomicAdd(&s_b[j[u]], 1u);
-        } else {
-          const uint32_t p = atomicAdd(&s_b[j[u]], 1u);
-          dst[p] = key[u];
-        }
-      }
+      load(e0, key, j);
+      visit(phase, e0, key, j);
     }
     __syncthreads();
     if (phase == 0) {  // reserve each touched bucket's range; s_b := this block's first slot
@@ -1233,6 +1267,9 @@ __global__ __launch_bounds__(1024) void topk_bucket_scatter(const uint64_t* __re
 // sorted instead.  Sort key: (2^31-1-|t'|bits) << 33 | index << 1 | sign.
 constexpr int kSubBins = kBT * kBI;  // 4096
 constexpr uint32_t kMaxRun = 32;
+#ifndef OMF_SORT_LOCAL  // 1: sub-bins from an LDS histogram of the bucket's keys; 0: from the fine bins
+#define OMF_SORT_LOCAL 1
+#endif
 #ifndef OMF_SORT_WAVES  // waves per SIMD the bucket sort is compiled for (experiment builds may override)
 #define OMF_SORT_WAVES 6
 #endif
@@ -1261,6 +1298,10 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(OMF_SORT_WA
       uint64_t out[kSubBins];
       uint32_t start2[kSubBins / 2];
     } cs;
+    struct {  // OMF_SORT_LOCAL: the level-1 histogram, and the wave min / max (then scan totals)
+      uint32_t h1[kBT];
+      uint32_t mm[2 * (kBT / 64)];
+    } lv;
   } s_u;
   const BucketRec rec = brec[b0 + blockIdx.x];
   const uint32_t cnt = rec.count_tensor & 0xffffu;
@@ -1269,6 +1310,70 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(OMF_SORT_WA
   const uint32_t st = rec.start;
   const uint64_t* src = bkeys + rec.key_off;
   const int64_t k = kk[t], o = koff[t], base = tbegin[t], n = tsize[t];  // issued with the key loads
+  uint64_t keys[kBI];
+  uint32_t meta[kBI];  // sub-bin << 16 | slot in it (0xffffffff: no key)
+#if OMF_SORT_LOCAL
+  // Sub-bin of a key from the bucket's own keys, in LDS (no memory round after the key loads):
+  // the bucket's |t'| range [mmin, mmax] is cut into kBT equal level-1 bins, counted and scanned;
+  // a key's sub-bin = its level-1 bin's first rank plus its linear position inside that bin times
+  // the bin's count — about one key per sub-bin, monotone in |t'| (descending), so the counting
+  // sort below plus an insertion sort per sub-bin orders the bucket exactly.
+  const uint32_t hi = thi[t];
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) keys[j] = src[min(threadIdx.x + (uint32_t)j * kBT, cnt - 1u)];  // striped
+  uint32_t mn = 0xffffffffu, mx = 0u;
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {  // past the count: the last key again (no effect on the range)
+    const uint32_t mag = (uint32_t)keys[j] & 0x7fffffffu;
+    mn = min(mn, mag);
+    mx = max(mx, mag);
+  }
+#pragma unroll
+  for (int d = 32; d > 0; d >>= 1) {
+    mn = min(mn, (uint32_t)__shfl_xor(mn, d, 64));
+    mx = max(mx, (uint32_t)__shfl_xor(mx, d, 64));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    s_u.lv.mm[wave] = mn;
+    s_u.lv.mm[kBT / 64 + wave] = mx;
+  }
+  s_u.lv.h1[threadIdx.x] = 0;
+  for (int i = threadIdx.x; i < kSubBins / 2; i += kBT) s_u.cs.start2[i] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int w = 0; w < kBT / 64; ++w) {
+    mn = min(mn, s_u.lv.mm[w]);
+    mx = max(mx, s_u.lv.mm[kBT / 64 + w]);
+  }
+  // y = (mmax - |t'|) * kBT / range: one rounding of a monotone product, so monotone in |t'|
+  const float sc = (float)kBT / (float)((uint64_t)mx - mn + 1u);
+  float y[kBI];
+  uint32_t b1[kBI];
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {
+    y[j] = (float)(mx - ((uint32_t)keys[j] & 0x7fffffffu)) * sc;
+    b1[j] = min((uint32_t)y[j], (uint32_t)kBT - 1u);
+    if (threadIdx.x + (uint32_t)j * kBT < cnt) atomicAdd(&s_u.lv.h1[b1[j]], 1u);
+  }
+  __syncthreads();
+  {
+    const uint32_t c1 = s_u.lv.h1[threadIdx.x];
+    uint32_t tot;
+    const uint32_t inc = block_scan_incl<kBT>(c1, s_u.lv.mm, tot);  // begins with a barrier
+    s_u.lv.h1[threadIdx.x] = (inc - c1) | (c1 << 16);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kBI; ++j) {
+    const uint32_t e = threadIdx.x + (uint32_t)j * kBT;
+    const uint32_t w = s_u.lv.h1[b1[j]], c = w >> 16;
+    const uint32_t in = min((uint32_t)((y[j] - (float)b1[j]) * (float)c), c - 1u);
+    const uint32_t bits = (uint32_t)keys[j], mag = bits & 0x7fffffffu;
+    meta[j] = e < cnt ? min((w & 0xffffu) + in, cnt - 1u) : 0xffffffffu;
+    keys[j] = e < cnt ? ((uint64_t)(0x7fffffffu - mag) << 33) | ((keys[j] >> 32) << 1) | (uint64_t)(bits >> 31) : ~0ull;
+  }
+#else
   const uint32_t lo = tlo[t], F = fcount[t], hi = thi[t];
   const uint32_t* map_t = fmap + (size_t)t * kCoarse;
   const uint32_t* h_t = fhist + (size_t)t * kFineMax;
@@ -1278,8 +1383,6 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(OMF_SORT_WA
   // c keys, descending |t'|.  Sub-bins = the bucket's key count, about one key each.
   // Three rounds of loads, each issued whole before any is used (no load under a branch): the
   // keys (past the count: the last key again), their fine bins' maps, the bins' counts and ranks.
-  uint64_t keys[kBI];
-  uint32_t meta[kBI];  // sub-bin << 16 | slot in it (0xffffffff: no key)
   uint32_t mv[kBI];  // each key's coarse-bin map entry (its fine bin and low bits follow from it)
 #pragma unroll
   for (int j = 0; j < kBI; ++j) keys[j] = src[min(threadIdx.x + (uint32_t)j * kBT, cnt - 1u)];  // striped
@@ -1312,6 +1415,7 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(OMF_SORT_WA
   }
   for (int i = threadIdx.x; i < kSubBins / 2; i += kBT) s_u.cs.start2[i] = 0;
   __syncthreads();
+#endif
 #pragma unroll
   for (int j = 0; j < kBI; ++j) {
     if (meta[j] == 0xffffffffu) continue;
@@ -1922,6 +2026,7 @@ struct Group {
   int32_t t0 = 0, t1 = 0;                           // tensors [t0, t1)
   uint32_t sb0 = 0, nsb = 0, sub0 = 0, nsub = 0;    // sample blocks, fused-pass blocks
   uint32_t sup0 = 0, nsup = 0, bk0 = 0, nbk = 0;    // super-items, bucket slots
+  uint32_t nb_max = 0;                              // most bucket slots of one tensor
 };
 
 int topk_group_count(const omf_plan* p, const TopkKnobs& kn) {
@@ -1952,6 +2057,7 @@ std::vector<Group> make_groups(const std::vector<int64_t>& sizes, double ratio, 
     cur.nsub += (uint32_t)(ni * kSubsPerItem);
     cur.nsup += ns;
     cur.nbk += nb;
+    cur.nb_max = std::max(cur.nb_max, nb);
     sb += nsb;
     sub += (uint32_t)(ni * kSubsPerItem);
     sup += ns;
@@ -1973,7 +2079,8 @@ std::vector<Group> make_groups(const std::vector<int64_t>& sizes, double ratio, 
 }
 
 // The plan's Top-K settings: the OMF_TOPK_* environment read once, at its first Top-K call
-// (OMF_TOPK_GROUPS, OMF_TOPK_DBG, OMF_TOPK_FALLBACK, OMF_TOPK_SAMPLE_RUNS, OMF_TOPK_SURE="z,c"),
+// (OMF_TOPK_GROUPS, OMF_TOPK_DBG, OMF_TOPK_FALLBACK, OMF_TOPK_SAMPLE_RUNS, OMF_TOPK_SURE="z,c",
+// OMF_TOPK_SCATTER_SMALL),
 // unless omf_plan_set_topk set them first.
 const TopkKnobs& knobs(omf_plan* p) {
   TopkKnobs& k = omf_plan_access::topk_knobs(p);
@@ -1991,6 +2098,7 @@ const TopkKnobs& knobs(omf_plan* p) {
 #endif
   }
   if (const char* e = std::getenv("OMF_TOPK_FALLBACK")) k.force_fallback = e[0] == '1';
+  if (const char* e = std::getenv("OMF_TOPK_SCATTER_SMALL")) k.scatter_small = e[0] != '0';
   if (const char* e = std::getenv("OMF_TOPK_SAMPLE_RUNS")) {
     const long long v = std::atoll(e);
     if (v >= 64 && v <= (1 << 20)) k.sample_runs = v;
@@ -2395,9 +2503,14 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
                          bstart, brec, bfill, kb2, flag, status, fse, tkey, zcnt, dbg, tb.done, hsync->dev, seq, G.t0,
                          (uint32_t)nt);
       if (!forced) {
-        hipLaunchKernelGGL(topk_bucket_scatter, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo,
-                           fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins, rz, sorted, status, thi,
-                           G.sup0);
+        if (G.nb_max <= kScatterSmallB && kn.scatter_small)
+          hipLaunchKernelGGL(topk_bucket_scatter<true>, supgrid, supblk, 0, s, cand, items, sub_cnt,
+                             (const uint4*)tb.supinfo, fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins,
+                             rz, sorted, status, thi, G.sup0);
+        else
+          hipLaunchKernelGGL(topk_bucket_scatter<false>, supgrid, supblk, 0, s, cand, items, sub_cnt,
+                             (const uint4*)tb.supinfo, fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins,
+                             rz, sorted, status, thi, G.sup0);
         hipLaunchKernelGGL(topk_bucket_sort, dim3(G.nbk), dim3(kBT), 0, s, sorted, brec, kk, koff, d_begins, d_sizes,
                            rz, values, indices, status, fmap, tlo, fcount, fhist, fse, thi, dbg, G.bk0);
       }

@@ -54,7 +54,7 @@ case "$task" in
     [ -n "$s" ] && cp "$s" gpurun_out/${T}_kernel_stats.csv && cat gpurun_out/${T}_kernel_stats.csv
     ;;
   pmc)
-    T=${1:-r04}
+    T=${1:-r04}_s${PMC_BITS:-4}
     shift || true
     for c in FETCH_SIZE WRITE_SIZE; do
       rm -rf gpurun_out/${T}_pmc_$c
@@ -100,10 +100,11 @@ case "$task" in
     bash scripts/gpu.sh prof ${T} > /dev/null || exit 2
     bash scripts/gpu.sh prof ${T}_topk --codec topk > /dev/null || exit 3
     bash scripts/gpu.sh prof ${T}_s8 --bits 8 --no-topk > /dev/null || exit 3
-    rm -f gpurun_out/${T}_pmc_traffic.json
+    rm -f gpurun_out/${T}_s4_pmc_traffic.json gpurun_out/${T}_s8_pmc_traffic.json
     bash scripts/gpu.sh pmc ${T} || exit 4
+    cp gpurun_out/${T}_s4_pmc_traffic.json gpurun_out/${T}_s8_pmc_traffic.json
     PMC_BITS=8 bash scripts/gpu.sh pmc ${T} --bits 8 --no-topk || exit 4
-    cp gpurun_out/${T}_pmc_traffic.json profiles/pmc_traffic.json
+    cp gpurun_out/${T}_s8_pmc_traffic.json profiles/pmc_traffic.json
     bash scripts/gpu.sh bench ${T} || exit 5
     bash scripts/gpu.sh bench ${T}_s8 --bits 8 --no-topk --no-cpu-baseline || exit 5
     cp gpurun_out/${T}_s8_bench.json profiles/${T}_s8_bench.json
