@@ -38,6 +38,7 @@ struct TopkKnobs {
   int64_t sample_runs = 0;     // sampled runs per tensor at most (0: the default, 2 Ki)
   float sure_z = 1.5f, sure_c = 2.0f;  // the "sure" bin's margin below the expected rank-k count
   bool scatter_small = true;   // the bucket scatter's LDS-staged bucket table (OMF_TOPK_SCATTER_SMALL=0 off)
+  bool planned_scatter = true; // the bucket plan inside the scatter launch (OMF_TOPK_PLANNED_SCATTER=0 off)
 };
 
 // Thread-local error string behind omf_last_error().

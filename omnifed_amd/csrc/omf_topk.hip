@@ -931,13 +931,15 @@ struct SupView {
   int64_t* s_ibeg;    // [kSupItems] arena offsets of the items
   int t;
   uint32_t total;
-  // supinfo[sup] = {tensor, first item, items} (a plan-owned table: no search), and the
+  bool first;  // the tensor's first super-item
+  // supinfo[sup] = {tensor, first item, items, first} (a plan-owned table: no search), and the
   // tensor's fine-bin map staged into s_map[kCoarse] (read per key by the callers).
   __device__ __forceinline__ void init(const uint4* __restrict__ supinfo, const Item* __restrict__ items,
                                        const uint32_t* __restrict__ sub_cnt, const uint32_t* __restrict__ fmap,
                                        uint32_t* s_map, uint32_t* s_part, uint32_t sup) {
     const uint4 si = supinfo[sup];
     t = (int)si.x;
+    first = si.w != 0u;
     const uint32_t i0 = si.y, ni = si.z;
     s_map[threadIdx.x] = fmap[(size_t)t * kCoarse + threadIdx.x];  // 1024 threads = kCoarse
     const uint32_t run = threadIdx.x;  // run j of item j / 16
@@ -989,15 +991,19 @@ __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restric
                                                        const uint32_t* __restrict__ fmap,
                                                        const uint32_t* __restrict__ tlo,
                                                        const uint32_t* __restrict__ fcount,
-                                                       uint32_t* __restrict__ fhist, uint32_t sup0) {
+                                                       uint32_t* __restrict__ fhist,
+                                                       const uint32_t* __restrict__ bbase,
+                                                       uint32_t* __restrict__ bfill, uint32_t sup0) {
   __shared__ uint32_t s_h[kFineMax];
   __shared__ uint32_t s_spre[1025], s_part[1024];
   __shared__ int64_t s_ibeg[kSupItems];
   __shared__ uint32_t s_map[kCoarse];
-  SupView v{s_spre, s_ibeg, 0, 0};
+  SupView v{s_spre, s_ibeg, 0, 0, false};
   for (int i = threadIdx.x; i < kFineMax; i += 1024) s_h[i] = 0;
   v.init(supinfo, items, sub_cnt, fmap, s_map, s_part, sup0 + blockIdx.x);
   const uint32_t lo = tlo[v.t], F = fcount[v.t];
+  if (v.first)  // the tensor's bucket reservation counters, for topk_scatter_planned (topk_plan also clears them)
+    for (uint32_t j = bbase[v.t] + threadIdx.x; j < bbase[v.t + 1]; j += 1024) bfill[j] = 0;
   const uint32_t* map_t = s_map;
   constexpr int U = OMF_FHIST_U;  // key loads in flight per thread
   for (uint32_t e0 = threadIdx.x; e0 < v.total; e0 += U * 1024) {
@@ -1190,7 +1196,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   __shared__ uint32_t s_spre[1025], s_part[1024];
   __shared__ int64_t s_ibeg[kSupItems];
   __shared__ uint32_t s_map[kCoarse];
-  SupView v{s_spre, s_ibeg, 0, 0};
+  SupView v{s_spre, s_ibeg, 0, 0, false};
   v.init(supinfo, items, sub_cnt, fmap, s_map, s_part, sup0 + blockIdx.x);
   const int t = v.t;
   const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nb = bbase[t + 1] - b0, hi = thi[t];
@@ -1508,6 +1514,177 @@ __global__ __launch_bounds__(kBT) __attribute__((amdgpu_waves_per_eu(OMF_SORT_WA
       if (r && !sure && !(dbg & 2)) r[base + idx] = __fsub_rn(v, v);  // selected below the sure bin
     } else if (r && sure && !(dbg & 2)) {
       r[base + idx] = v;  // a "sure" key that was not selected after all: t' back
+    }
+  }
+}
+
+// Fast path, plan + scatter in one launch (every tensor of the launch with <= kScatterSmallB bucket
+// slots; the LDS sort, which needs no fine-bin ranks): each super-item block plans its own tensor's
+// buckets in LDS from the exact fine-bin histogram — the counts (16 per thread), one block scan, the
+// bucket of every kept bin and each bucket's first rank — exactly as topk_plan_tensor, so the bucket
+// table and the buckets' first ranks never go through global memory and no launch (with its drain)
+// separates the plan from the scatter.  The tensor's first super-item block also writes the bucket
+// records, the zero-fill count and the redo flag, sets the verdict bits, and arrives on the call's
+// counter (one arrival per tensor, as topk_plan's blocks): the last tensor to arrive publishes the
+// verdict to mapped host memory early in the launch.  A block whose own tensor is flagged (redo, or a
+// fine bin over kBucketHalf keys, whose keys could run past the tensor's bucket region) places
+// nothing: the call takes the fallback, which restores every candidate's residual.  Blocks of
+// unflagged tensors proceed whatever the others' verdicts (their bucket writes are then unused).
+static_assert(OMF_SORT_LOCAL, "topk_scatter_planned needs the sort that does not read the fine-bin ranks");
+#ifndef OMF_PLANNED_CACHE  // key loads per thread (x4) kept in registers between the scatter's phases
+#define OMF_PLANNED_CACHE 2
+#endif
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void topk_scatter_planned(
+    const uint64_t* __restrict__ cand, const Item* __restrict__ items, const uint32_t* __restrict__ sub_cnt,
+    const uint4* __restrict__ supinfo, const uint32_t* __restrict__ fmap, const uint32_t* __restrict__ tlo,
+    const uint32_t* __restrict__ fcount, const uint32_t* __restrict__ fhist, const int64_t* __restrict__ kk,
+    const uint32_t* __restrict__ tkey, const uint32_t* __restrict__ bbase, BucketRec* __restrict__ brec,
+    uint32_t* __restrict__ bfill, const int64_t* __restrict__ kb2, const int64_t* __restrict__ tbegin,
+    float* __restrict__ r, uint64_t* __restrict__ bkeys, uint32_t* __restrict__ flag, uint32_t* __restrict__ zcnt,
+    uint32_t* __restrict__ status, const uint32_t* __restrict__ thi, uint32_t* __restrict__ done, uint32_t* host,
+    uint32_t seq, uint32_t total_arrivals, uint32_t sup0) {
+  __shared__ uint32_t s_b[kScatterSmallB];   // per bucket: this block's count, then its first slot
+  __shared__ uint32_t s_bs[kScatterSmallB];  // per bucket: its first rank in the tensor
+  __shared__ int16_t s_fb[kFineMax];         // per fine bin: its bucket (-1: below the k-th key's bin)
+  __shared__ uint32_t s_spre[1025], s_part[1024];
+  __shared__ int64_t s_ibeg[kSupItems];
+  __shared__ uint32_t s_map[kCoarse];
+  __shared__ uint32_t s_kend, s_nb, s_over;
+  SupView v{s_spre, s_ibeg, 0, 0, false};
+  v.init(supinfo, items, sub_cnt, fmap, s_map, s_part, sup0 + blockIdx.x);
+  const int t = v.t;
+  const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nbmax = bbase[t + 1] - b0, hi = thi[t];
+  const int64_t base = tbegin[t];
+  // ---- the plan (topk_plan_tensor's rule)
+  constexpr int PER = kFineMax / 1024;
+  const uint32_t* ht = fhist + (size_t)t * kFineMax;
+  uint32_t h[PER], loc = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const uint32_t i = PER * threadIdx.x + j;
+    h[j] = i < F ? ht[i] : 0u;
+    loc += h[j];
+  }
+  if (threadIdx.x == 0) {
+    s_kend = 0;
+    s_nb = 0;
+    s_over = 0;
+  }
+  for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) {
+    s_bs[j] = 0xffffffffu;
+    s_b[j] = 0;
+  }
+  uint32_t tot32;
+  const uint32_t inc = block_scan_incl<1024>(loc, s_part, tot32);  // begins with a barrier
+  const bool zero_mode = tkey[t] == 1u;
+  uint64_t k = (uint64_t)kk[t];
+  const bool redo = tot32 < k && !zero_mode;  // the sampled threshold was too high: exact redo
+  const bool zero_fill = tot32 < k && zero_mode;  // every candidate selected, then zeros
+  if (zero_fill) k = tot32;
+  if (!redo) {
+    uint64_t se = tot32 - inc;  // keys in the bins of higher threads
+#pragma unroll
+    for (int j = PER - 1; j >= 0; --j) {
+      const uint32_t i = PER * threadIdx.x + j;
+      int32_t bucket = -1;
+      if (h[j] && se < k) {
+        bucket = (int32_t)(se / kBucketHalf);
+        atomicMin(&s_bs[bucket], (uint32_t)se);
+        if (h[j] > (uint32_t)kBucketHalf) s_over = 1u;  // (OMF_TOPK_PLANNED_SCATTER=0 with OMF_TOPK_DBG=8 names it)
+        if (se + h[j] >= k) {  // the bin of the k-th key (exactly one)
+          s_kend = (uint32_t)(se + h[j]);
+          s_nb = (uint32_t)bucket + 1u;
+        }
+      }
+      if (i < F) s_fb[i] = (int16_t)bucket;
+      se += h[j];
+    }
+  }
+  __syncthreads();
+  const bool skip = redo || s_over != 0u;  // block-uniform
+  if (v.first) {  // the tensor's records, flags and verdict bits; its arrival
+    const uint32_t nb = s_nb;
+    for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) {
+      uint32_t st = 0, c = 0;
+      if (!redo && j < nb && s_bs[j] != 0xffffffffu) {
+        st = s_bs[j];
+        const uint32_t en = j + 1 < nb ? s_bs[j + 1] : s_kend;
+        c = en > st ? en - st : 0u;
+      }
+      brec[b0 + j] = BucketRec{(uint64_t)kb2[t] + st, st, min(c, 0xffffu) | ((uint32_t)t << 16)};
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      flag[t] = redo ? 1u : 0u;
+      zcnt[t] = zero_fill ? tot32 : kNoZeroFill;
+      if (redo) atomicOr(&status[1], 1u);
+      if (!redo && s_over) atomicOr(&status[2], 1u);
+      if (zero_fill) atomicOr(&status[0], 1u);
+      // the arrival (as topk_plan): this thread's status atomics performed, then one agent-scope add;
+      // the last of the call's tensors publishes the verdict, the sequence number last (release)
+      drain_vmem();
+      if (add_agent(done, 1u) == total_arrivals - 1) {
+        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t w0 = atomicOr(&status[0], 0u), w1 = atomicOr(&status[1], 0u), w2 = atomicOr(&status[2], 0u);
+        __hip_atomic_store(&host[0], w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host[1], w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host[2], w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+  }
+  if (skip) return;
+  // ---- the scatter (topk_bucket_scatter<true> with the LDS plan)
+  const uint32_t* map_t = s_map;
+  uint64_t* dst = bkeys + kb2[t];
+  constexpr int U = 4;
+  constexpr int CI = OMF_PLANNED_CACHE;
+  const auto load = [&](uint32_t e0, uint64_t (&key)[U], int32_t (&j)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint32_t e = min(e0 + (uint32_t)u * 1024, v.total - 1);
+      key[u] = cand[v.pos(e)];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) j[u] = (int32_t)s_fb[fine_bin((uint32_t)key[u] & 0x7fffffffu, lo, map_t, F)];
+  };
+  const auto visit = [&](int phase, uint32_t e0, const uint64_t (&key)[U], const int32_t (&j)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (e0 + (uint32_t)u * 1024 >= v.total) continue;
+      if (j[u] < 0) {  // below the k-th key's bin: not selected (a "sure" key gets its t' back)
+        if (phase == 1 && r && ((uint32_t)key[u] & 0x7fffffffu) >= hi)
+          r[base + (key[u] >> 32)] = __uint_as_float((uint32_t)key[u]);
+        continue;
+      }
+      if (phase == 0) {
+        atomicAdd(&s_b[j[u]], 1u);
+      } else {
+        const uint32_t p = atomicAdd(&s_b[j[u]], 1u);
+        dst[p] = key[u];
+      }
+    }
+  };
+  uint64_t ck[CI > 0 ? CI : 1][U];
+  int32_t cj[CI > 0 ? CI : 1][U];
+#pragma unroll
+  for (int i = 0; i < CI; ++i)
+    if (threadIdx.x + (uint32_t)i * U * 1024 < v.total) load(threadIdx.x + (uint32_t)i * U * 1024, ck[i], cj[i]);
+  for (int phase = 0; phase < 2; ++phase) {  // 0: count per bucket; 1: place
+#pragma unroll
+    for (int i = 0; i < CI; ++i)
+      if (threadIdx.x + (uint32_t)i * U * 1024 < v.total) visit(phase, threadIdx.x + (uint32_t)i * U * 1024, ck[i], cj[i]);
+    for (uint32_t e0 = threadIdx.x + (uint32_t)CI * U * 1024; e0 < v.total; e0 += U * 1024) {
+      uint64_t key[U];
+      int32_t j[U];
+      load(e0, key, j);
+      visit(phase, e0, key, j);
+    }
+    __syncthreads();
+    if (phase == 0) {  // reserve each touched bucket's range; s_b := this block's first slot
+      for (uint32_t q = threadIdx.x; q < nbmax; q += 1024)
+        if (s_b[q]) s_b[q] = s_bs[q] + atomicAdd(&bfill[b0 + q], s_b[q]);
+      __syncthreads();
     }
   }
 }
@@ -2080,7 +2257,7 @@ std::vector<Group> make_groups(const std::vector<int64_t>& sizes, double ratio, 
 
 // The plan's Top-K settings: the OMF_TOPK_* environment read once, at its first Top-K call
 // (OMF_TOPK_GROUPS, OMF_TOPK_DBG, OMF_TOPK_FALLBACK, OMF_TOPK_SAMPLE_RUNS, OMF_TOPK_SURE="z,c",
-// OMF_TOPK_SCATTER_SMALL),
+// OMF_TOPK_SCATTER_SMALL, OMF_TOPK_PLANNED_SCATTER),
 // unless omf_plan_set_topk set them first.
 const TopkKnobs& knobs(omf_plan* p) {
   TopkKnobs& k = omf_plan_access::topk_knobs(p);
@@ -2099,6 +2276,7 @@ const TopkKnobs& knobs(omf_plan* p) {
   }
   if (const char* e = std::getenv("OMF_TOPK_FALLBACK")) k.force_fallback = e[0] == '1';
   if (const char* e = std::getenv("OMF_TOPK_SCATTER_SMALL")) k.scatter_small = e[0] != '0';
+  if (const char* e = std::getenv("OMF_TOPK_PLANNED_SCATTER")) k.planned_scatter = e[0] != '0';
   if (const char* e = std::getenv("OMF_TOPK_SAMPLE_RUNS")) {
     const long long v = std::atoll(e);
     if (v >= 64 && v <= (1 << 20)) k.sample_runs = v;
@@ -2226,7 +2404,7 @@ WsLayout layout_uncached(const omf_plan* p) {
 struct SetupTable {
   int64_t *kk, *koff, *kb2;
   uint32_t *tfirst, *tlast, *bbase, *sbase, *smap, *gh, *gz, *done, *arrive;
-  uint32_t* supinfo;  // per super-item {tensor, first item, items, 0}
+  uint32_t* supinfo;  // per super-item {tensor, first item, items, first super-item of its tensor}
   uint32_t* zmap;     // per zero-fill block {tensor, sub-chunk}: the sub-chunks below index k_t
   int32_t nsb, nzb;
 };
@@ -2265,7 +2443,7 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
       supinfo.push_back((uint32_t)t);
       supinfo.push_back(item0 + i);
       supinfo.push_back(std::min<uint32_t>(kSupItems, ni - i));
-      supinfo.push_back(0u);
+      supinfo.push_back(i == 0 ? 1u : 0u);
     }
     item0 += ni;
   }
@@ -2495,22 +2673,30 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       // fast path: exact fine-bin histograms, bucket plan
       const dim3 supgrid(G.nsup), supblk(1024);
       hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo, fmap,
-                         tlo, fcount, fhist, G.sup0);
+                         tlo, fcount, fhist, bbase, bfill, G.sup0);
       // the call's last plan block (over every group) publishes the verdict to mapped host
       // memory; the bucket kernels are enqueued before the host waits for it (they do nothing
       // when the verdict is a fallback), so the GPU does not idle while the host reads it
-      hipLaunchKernelGGL(topk_plan, dim3((unsigned)(G.t1 - G.t0)), sblk, 0, s, kk, fcount, fhist, bbase, fbucket,
-                         bstart, brec, bfill, kb2, flag, status, fse, tkey, zcnt, dbg, tb.done, hsync->dev, seq, G.t0,
-                         (uint32_t)nt);
+      const bool small = G.nb_max <= kScatterSmallB && kn.scatter_small;
+      if (!forced && small && kn.planned_scatter)  // the plan inside the scatter launch
+        hipLaunchKernelGGL(topk_scatter_planned, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo,
+                           fmap, tlo, fcount, fhist, kk, tkey, bbase, brec, bfill, kb2, d_begins, rz, sorted, flag, zcnt,
+                           status, thi, tb.done, hsync->dev, seq, (uint32_t)nt, G.sup0);
+      else
+        hipLaunchKernelGGL(topk_plan, dim3((unsigned)(G.t1 - G.t0)), sblk, 0, s, kk, fcount, fhist, bbase, fbucket,
+                           bstart, brec, bfill, kb2, flag, status, fse, tkey, zcnt, dbg, tb.done, hsync->dev, seq, G.t0,
+                           (uint32_t)nt);
       if (!forced) {
-        if (G.nb_max <= kScatterSmallB && kn.scatter_small)
-          hipLaunchKernelGGL(topk_bucket_scatter<true>, supgrid, supblk, 0, s, cand, items, sub_cnt,
-                             (const uint4*)tb.supinfo, fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins,
-                             rz, sorted, status, thi, G.sup0);
-        else
-          hipLaunchKernelGGL(topk_bucket_scatter<false>, supgrid, supblk, 0, s, cand, items, sub_cnt,
-                             (const uint4*)tb.supinfo, fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2, d_begins,
-                             rz, sorted, status, thi, G.sup0);
+        if (!(small && kn.planned_scatter)) {  // (the planned scatter has run above)
+          if (small)
+            hipLaunchKernelGGL(topk_bucket_scatter<true>, supgrid, supblk, 0, s, cand, items, sub_cnt,
+                               (const uint4*)tb.supinfo, fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2,
+                               d_begins, rz, sorted, status, thi, G.sup0);
+          else
+            hipLaunchKernelGGL(topk_bucket_scatter<false>, supgrid, supblk, 0, s, cand, items, sub_cnt,
+                               (const uint4*)tb.supinfo, fmap, tlo, fcount, fbucket, bbase, bstart, bfill, kb2,
+                               d_begins, rz, sorted, status, thi, G.sup0);
+        }
         hipLaunchKernelGGL(topk_bucket_sort, dim3(G.nbk), dim3(kBT), 0, s, sorted, brec, kk, koff, d_begins, d_sizes,
                            rz, values, indices, status, fmap, tlo, fcount, fhist, fse, thi, dbg, G.bk0);
       }
