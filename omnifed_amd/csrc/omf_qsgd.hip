@@ -1529,14 +1529,18 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_flat(DecArgs a) {
   }
 }
 
-// Decoder over arena-aligned 4 Ki-element blocks: the payload loads depend on blockIdx only,
-// so they go out at once; the block's tensor (binfo: tensor id, bit 31 = the block lies inside
-// it) and its norm are scalar loads in flight with them.  A block that crosses a tensor
-// boundary or padding (at most nt + 1 of them) finds each quad's tensor and writes only its
-// elements.  The streaming shape of scripts/exp/dec_probe.hip (4 rows of 1 Ki elements per
-// block); the item-indexed decoder waited for its item and norm loads before its payload loads.
-constexpr int kDecV = 4;
-constexpr int64_t kDecBlk = (int64_t)kDecV * kThreads * 4;  // 4096 elements
+// Decoder over arena-aligned blocks: the payload loads depend on blockIdx only, so they go out
+// at once; the block's tensor (binfo, one entry per 4 Ki-element table block: tensor id, bit 31 =
+// the table block lies inside it) and its norm are scalar loads in flight with them.  A block in
+// a table block that crosses a tensor boundary or padding (at most nt + 1 of them) finds each
+// quad's tensor and writes only its elements.  Round 5: the decode block is narrower than the
+// table block — kDecQuads(W, ACC) quads per thread: 2 for an int8 payload, 1 for an int32 payload
+// or an accumulate — measured on Llama-400M (scripts/exp/dec_shapes.hip, interleaved): int8
+// 0.298-0.304 ms against 0.331 with 4 quads, int32 0.492 against 0.550, accumulate 0.556 / 0.748
+// against 0.612 / 0.807 (fewer bytes per thread, more workgroups in flight per CU).
+constexpr int64_t kDecBlk = (int64_t)4 * kThreads * 4;  // 4096 elements per binfo table block
+template <int WIDTH, bool ACC>
+constexpr int kDecQuads = (WIDTH == 1 && !ACC) ? 2 : 1;
 
 template <int WIDTH, bool ACC, bool POW2>
 __device__ __forceinline__ void dec_quad(const DecArgs& a, int32_t raw[4], float norm, float (&yv)[4]) {
@@ -1562,25 +1566,26 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_arena(DecArgs a, const u
                                                               const int64_t* __restrict__ begins,
                                                               const int64_t* __restrict__ sizes, int32_t nt,
                                                               int64_t qlast, uint32_t blk0) {
+  constexpr int V = kDecQuads<WIDTH, ACC>;
   const uint32_t bid = blk0 + blockIdx.x;  // a range launch starts at block blk0
-  const int64_t base = (int64_t)bid * kDecBlk;
-  int32_t raw[kDecV][WIDTH == 1 ? 1 : 4];
+  const int64_t base = (int64_t)bid * (V * kThreads * 4);
+  int32_t raw[V][WIDTH == 1 ? 1 : 4];
 #pragma unroll
-  for (int k = 0; k < kDecV; ++k) {  // unconditional (clamped) nontemporal loads
+  for (int k = 0; k < V; ++k) {  // unconditional (clamped) loads
     const int64_t e = min(base + 4 * ((int64_t)k * kThreads + threadIdx.x), qlast);
-    if (WIDTH == 1) {
-      raw[k][0] = __builtin_nontemporal_load(reinterpret_cast<const int32_t*>(reinterpret_cast<const int8_t*>(a.q) + e));
+    if (WIDTH == 1) {  // default policy: 0.298 against 0.304 ms non-temporal (dec_shapes.hip)
+      raw[k][0] = *reinterpret_cast<const int32_t*>(reinterpret_cast<const int8_t*>(a.q) + e);
     } else {
       const i32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const i32x4_t*>(reinterpret_cast<const int32_t*>(a.q) + e));
       raw[k][0] = t[0]; raw[k][1] = t[1]; raw[k][2] = t[2]; raw[k][3] = t[3];
     }
   }
-  const uint32_t info = binfo[bid];
+  const uint32_t info = binfo[base / kDecBlk];
   const int32_t t0 = (int32_t)(info & 0x7fffffffu);
-  if (info >> 31) {  // the whole block lies inside tensor t0
+  if (info >> 31) {  // the whole table block lies inside tensor t0
     const float norm = norms[t0];
 #pragma unroll
-    for (int k = 0; k < kDecV; ++k) {
+    for (int k = 0; k < V; ++k) {
       const int64_t e = base + 4 * ((int64_t)k * kThreads + threadIdx.x);
       float yv[4];
       dec_quad<WIDTH, ACC, POW2>(a, raw[k], norm, yv);
@@ -1596,7 +1601,7 @@ __global__ __launch_bounds__(kThreads) void qsgd_decode_arena(DecArgs a, const u
   }
   // boundary block: each quad's tensor, element by element
 #pragma unroll
-  for (int k = 0; k < kDecV; ++k) {
+  for (int k = 0; k < V; ++k) {
     const int64_t e = base + 4 * ((int64_t)k * kThreads + threadIdx.x);
     int32_t t = t0;
     while (t + 1 < nt && e >= begins[t + 1]) ++t;
@@ -2812,17 +2817,19 @@ static int decode_blocks(omf_plan* p, const void* q, int32_t width, int32_t leve
   b0 = std::max<int64_t>(b0, 0);
   b1 = std::min<int64_t>(b1, p->n_dec_blocks);
   if (b1 <= b0) return OMF_OK;
-  const dim3 grid((unsigned)(b1 - b0)), blk(kThreads);
+  const dim3 blk(kThreads);
   hipStream_t st = (hipStream_t)stream;
   // the last whole quad of the payload the caller holds (width 8: round_up(arena_end, 4) bytes
   // are not promised, so a clamped load never passes the last full quad)
   const int64_t qlast = (p->arena_end & ~(int64_t)3) - 4;  // < 0 only for arenas of < 4 elements
 #define OMF_DEC(W, A, P)                                                                                         \
   do {                                                                                                           \
-    if (qlast >= 0)                                                                                              \
-      hipLaunchKernelGGL((qsgd_decode_arena<W, A, P>), grid, blk, 0, st, a, (const uint32_t*)p->d_dec_binfo,     \
-                         norm, (const int64_t*)p->d_begins, (const int64_t*)p->d_sizes, p->nt, qlast, (uint32_t)b0);           \
-    else /* a payload of < 4 elements: the item decoder's byte loads */                                          \
+    if (qlast >= 0) {                                                                                            \
+      const int64_t per = kDecBlk / (kDecQuads<W, A> * kThreads * 4); /* decode blocks per table block */       \
+      hipLaunchKernelGGL((qsgd_decode_arena<W, A, P>), dim3((unsigned)((b1 - b0) * per)), blk, 0, st, a,         \
+                         (const uint32_t*)p->d_dec_binfo, norm, (const int64_t*)p->d_begins,                    \
+                         (const int64_t*)p->d_sizes, p->nt, qlast, (uint32_t)(b0 * per));                       \
+    } else /* a payload of < 4 elements: the item decoder's byte loads */                                          \
       hipLaunchKernelGGL((qsgd_decode_flat<W, A, P>), dim3((unsigned)p->n_flat), blk, 0, st, a);                \
   } while (0)
   if (width == 8) {
