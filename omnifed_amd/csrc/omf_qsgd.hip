@@ -84,10 +84,11 @@ struct DecArgs {
 };
 
 template <int V, bool FULL, bool NT = false>
-__device__ __forceinline__ void load_f4(const float* __restrict__ p, int64_t b, int64_t end, float4 (&v)[V]) {
+__device__ __forceinline__ void load_f4(const float* __restrict__ p, int64_t b, int64_t end, float4 (&v)[V],
+                                        int tid) {
 #pragma unroll
   for (int k = 0; k < V; ++k) {
-    const int64_t e = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+    const int64_t e = b + 4 * ((int64_t)k * kThreads + tid);
     if (FULL || e + 4 <= end) {
       if (NT) {  // a last read (the second pass of a two-pass tensor)
         const f32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p + e));
@@ -103,6 +104,10 @@ __device__ __forceinline__ void load_f4(const float* __restrict__ p, int64_t b, 
       v[k] = t;
     }
   }
+}
+template <int V, bool FULL, bool NT = false>
+__device__ __forceinline__ void load_f4(const float* __restrict__ p, int64_t b, int64_t end, float4 (&v)[V]) {
+  load_f4<V, FULL, NT>(p, b, end, v, (int)threadIdx.x);
 }
 
 // x * alpha (the client weighting), rounded to the value format for bf16/fp16 tensors
@@ -136,8 +141,8 @@ __device__ __forceinline__ float sumsq_f4(const float4 (&v)[V], float acc) {
 // Uniforms of rows k = 4g .. 4g+3 of this thread in a sub-chunk starting at b:
 // 3 Philox calls per 16 elements (oracle/philox.py: group G, 96-bit slots).
 __device__ __forceinline__ void philox_rows(const EncArgs& a, int64_t b, int64_t tbegin, int32_t tensor, int g,
-                                            float4 (&uu)[4]) {
-  const uint64_t G = ((uint64_t)((b - tbegin) >> 12) + (uint64_t)g) * (uint64_t)kThreads + threadIdx.x;
+                                            float4 (&uu)[4], int tid) {
+  const uint64_t G = ((uint64_t)((b - tbegin) >> 12) + (uint64_t)g) * (uint64_t)kThreads + (uint32_t)tid;
   uint32_t w[12];
 #pragma unroll
   for (int c = 0; c < 3; ++c) {
@@ -148,6 +153,10 @@ __device__ __forceinline__ void philox_rows(const EncArgs& a, int64_t b, int64_t
   }
 #pragma unroll
   for (int sl = 0; sl < 4; ++sl) uu[sl] = u24x4(w[3 * sl], w[3 * sl + 1], w[3 * sl + 2]);
+}
+__device__ __forceinline__ void philox_rows(const EncArgs& a, int64_t b, int64_t tbegin, int32_t tensor, int g,
+                                            float4 (&uu)[4]) {
+  philox_rows(a, b, tbegin, tensor, g, uu, (int)threadIdx.x);
 }
 
 // Quantise V float4 of one sub-chunk starting at b (tensor t begins at tbegin) and store.
@@ -829,19 +838,20 @@ __device__ __forceinline__ void store_quad(const EncArgs& a, int64_t e, int64_t 
 // 4 Ki block (straight-line code, no bounds checks).
 template <int WIDTH, bool FULL, bool DIV, uint32_t FMT, int AW = 0, int PW = kSpecPerWave, class GetBr>
 __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t blk, int64_t b, int64_t end, int32_t t,
-                                           int64_t tb, GetBr get_br, uint32_t* slot, uint64_t* part, float anorm) {
+                                           int64_t tb, GetBr get_br, uint32_t* slot, uint64_t* part, float anorm,
+                                           int tid) {
   const EncArgs& e = a.e;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = tid & 63, wave = tid >> 6;
   float4 v[kSpecV];
-  load_f4<kSpecV, FULL, true>(e.x, b, end, v);  // x is read once: nontemporal (the fix uses the records)
+  load_f4<kSpecV, FULL, true>(e.x, b, end, v, tid);  // x is read once: nontemporal (the fix uses the records)
   int4 araw[AW ? kSpecV : 1];
   if (AW) {  // the fused PS step's last client: its payload loaded beside x
 #pragma unroll
     for (int k = 0; k < kSpecV; ++k)
-      araw[k] = acc_load<AW ? AW : 1, FULL>(a.aq, b + 4 * ((int64_t)k * kThreads + threadIdx.x), end);
+      araw[k] = acc_load<AW ? AW : 1, FULL>(a.aq, b + 4 * ((int64_t)k * kThreads + tid), end);
   }
   float4 uu[4];
-  philox_rows(e, b, tb, t, 0, uu);
+  philox_rows(e, b, tb, t, 0, uu, tid);
   // Branch-free from the loads to the stores, so that the scheduler can place the Philox
   // arithmetic under the load latency: x * alpha unconditionally (x * 1 = x; fp32 only, the
   // product is not rounded further), and levels computed for a deferred tensor too (its
@@ -856,7 +866,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t blk, int64
     if (AW) {  // acc + decode(last client), stored when the caller keeps the accumulator
       v[k] = acc_add4<AW ? AW : 1>(v[k], araw[k], anorm, a.alevels, a.ainv);
       if (a.aout) {
-        const int64_t el = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+        const int64_t el = b + 4 * ((int64_t)k * kThreads + tid);
         if (FULL || el + 4 <= end) {
           store_nt(a.aout + el, v[k]);
         } else if (el < end) {
@@ -870,7 +880,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t blk, int64
       const float d = a.divisor;
       v[k].x = __fdiv_rn(v[k].x, d); v[k].y = __fdiv_rn(v[k].y, d);
       v[k].z = __fdiv_rn(v[k].z, d); v[k].w = __fdiv_rn(v[k].w, d);
-      const int64_t el = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+      const int64_t el = b + 4 * ((int64_t)k * kThreads + tid);
       if (FULL || el + 4 <= end) {
         store_nt(a.xout + el, v[k]);
       } else if (el < end) {
@@ -887,7 +897,7 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t blk, int64
     uint32_t* list = slot + PW * wave;
 #pragma unroll
     for (int k = 0; k < kSpecV; ++k) {
-      const int64_t el = b + 4 * ((int64_t)k * kThreads + threadIdx.x);
+      const int64_t el = b + 4 * ((int64_t)k * kThreads + tid);
       const bool live = FULL || el < end;
       int32_t qq[4];
       bool und = false;
@@ -918,21 +928,28 @@ __device__ __forceinline__ void spec_block(const SpecArgs& a, int64_t blk, int64
 
 // The per-tensor tables are __restrict__ const kernel arguments so that they are read with
 // scalar loads (a vector load there is waited for before the x loads are issued).
-template <int WIDTH, bool DIV, uint32_t FMT = kFmtF32, int AW = 0, int PW = kSpecPerWave>
-__global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
+// WPB: waves per workgroup.  A 4 Ki-element block's waves keep their element map (thread t of the
+// block owns rows b + 4 (k 256 + t)), partials, heads and lists whatever the workgroup size; wide
+// levels run one wave per workgroup (scripts/exp/dec_shapes.hip, the int32 pass's shape: 0.508
+// against 0.534 ms for four waves).
+template <int WIDTH, bool DIV, uint32_t FMT = kFmtF32, int AW = 0, int PW = kSpecPerWave, int WPB = kWaves>
+__global__ __launch_bounds__(64 * WPB) void qsgd_spec_quant(SpecArgs a, const SpecBracket* __restrict__ brs,
                                                             const int64_t* __restrict__ begins,
                                                             const float* __restrict__ anorms) {
-  const int64_t blk = blockIdx.x;
+  static_assert(kWaves % WPB == 0, "a block's waves split evenly");
+  constexpr int kPer = kWaves / WPB;  // workgroups per 4 Ki block
+  const int64_t blk = blockIdx.x / kPer;
+  const int tid = (int)(blockIdx.x % kPer) * 64 * WPB + (int)threadIdx.x;
   const Item it = a.e.items[blk >> 2];
   const SpecBracket br = brs[it.tensor];
   const int64_t tb = begins[it.tensor];
   const float anorm = AW ? anorms[it.tensor] : 0.0f;
   const int64_t b = it.begin + (blk & 3) * kSpecBlk;
-  const int wave = threadIdx.x >> 6;
+  const int wave = tid >> 6;
   uint32_t* slot = a.slots + blk * spec_slot_words(PW);
   uint64_t* part = a.partials + blk * kWaves + wave;
   if (b >= it.end) {  // past the tensor's end: an empty block still reports (stale values otherwise)
-    if ((threadIdx.x & 63) == 0) {
+    if ((tid & 63) == 0) {
       *part = 0ull;
       a.heads[blk * kWaves + wave] = (uint32_t)it.tensor << 8;
     }
@@ -941,9 +958,9 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant(SpecArgs a, const Sp
   const int64_t end = min(b + kSpecBlk, it.end);
   auto get_br = [&]() { return br; };
   if (end - b == kSpecBlk)
-    spec_block<WIDTH, true, DIV, FMT, AW, PW>(a, blk, b, end, it.tensor, tb, get_br, slot, part, anorm);
+    spec_block<WIDTH, true, DIV, FMT, AW, PW>(a, blk, b, end, it.tensor, tb, get_br, slot, part, anorm, tid);
   else
-    spec_block<WIDTH, false, DIV, FMT, AW, PW>(a, blk, b, end, it.tensor, tb, get_br, slot, part, anorm);
+    spec_block<WIDTH, false, DIV, FMT, AW, PW>(a, blk, b, end, it.tensor, tb, get_br, slot, part, anorm, tid);
 }
 
 // Fused bracket (OMF_SPEC_FB / omf_plan_set_fused_bracket): the bracket launch folded into the pass.
@@ -1059,8 +1076,8 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant_fb(SpecArgs a, const
     return o;
   };
   const int64_t end = min(b + kSpecBlk, it.end);
-  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, kFmtF32>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f);
-  else spec_block<WIDTH, false, DIV, kFmtF32>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f);
+  if (end - b == kSpecBlk) spec_block<WIDTH, true, DIV, kFmtF32>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f, (int)threadIdx.x);
+  else spec_block<WIDTH, false, DIV, kFmtF32>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f, (int)threadIdx.x);
 }
 
 // One fold segment (a workgroup of the finish launch); the last arriver of the tensor folds the
@@ -2599,11 +2616,20 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     constexpr int PWW = kSpecPerWaveWide;
     if (fb) {
       // (the pass ran above)
-    } else if (wide) {  // fp32, no fused last client (spec_serves)
-      if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
-      else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
-      else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
-      else hipLaunchKernelGGL((qsgd_spec_quant<4, true, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+    } else if (wide) {  // fp32, no fused last client (spec_serves); one wave per workgroup unless OMF_SPEC_WPB=4
+      static const bool wpb4 = [] { const char* v = getenv("OMF_SPEC_WPB"); return v && atoi(v) == 4; }();
+      const dim3 g1((unsigned)(p->n_spec_blocks * kWaves)), b1(64);
+      if (wpb4) {
+        if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+        else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+        else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+        else hipLaunchKernelGGL((qsgd_spec_quant<4, true, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
+      } else {
+        if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF32, 0, PWW, 1>), g1, b1, 0, st, sa, sa.br, sa.begins, an);
+        else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 0, PWW, 1>), g1, b1, 0, st, sa, sa.br, sa.begins, an);
+        else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, kFmtF32, 0, PWW, 1>), g1, b1, 0, st, sa, sa.br, sa.begins, an);
+        else hipLaunchKernelGGL((qsgd_spec_quant<4, true, kFmtF32, 0, PWW, 1>), g1, b1, 0, st, sa, sa.br, sa.begins, an);
+      }
     } else if (fmt == kFmtBF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtBF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
     else if (fmt == kFmtF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
     else if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
