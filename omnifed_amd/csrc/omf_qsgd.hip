@@ -2601,6 +2601,11 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     // skips the bracket launch (the previous brackets stay), bit 1 the finish launch, bits 2/3
     // the fix stores / the fix, bit 4 the fold — the payload is then not the encoder's.
     const bool div = divisor != 0.0f;
+    // The wide pass's one-wave workgroups reserve 10 KiB of LDS each (unused): 16 per CU, i.e. four
+    // waves per SIMD — 0.556-0.559 ms per Llama-400M s = 8 encode against 0.589 uncapped, 0.565 at 12
+    // KiB, 0.635 at 16 KiB (scripts/exp/occ_ab.sh, two interleaved rounds); OMF_SPEC_LDS_W overrides.
+    // The s <= 4 pass is co-bound by its VALU and keeps every wave (24 KiB: 0.367 against 0.360 ms).
+    static const size_t plds_w = [] { const char* v = getenv("OMF_SPEC_LDS_W"); return v ? (size_t)atoi(v) : (size_t)10240; }();
     if (fb) {  // the bracket folded into the pass (its first workgroups)
       const int64_t nbrw = (int64_t)kFbParts * p->n_spec_br;
       const dim3 gfb((unsigned)(nbrw + p->n_spec_blocks));
@@ -2625,10 +2630,10 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
         else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
         else hipLaunchKernelGGL((qsgd_spec_quant<4, true, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
       } else {
-        if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF32, 0, PWW, 1>), g1, b1, 0, st, sa, sa.br, sa.begins, an);
-        else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 0, PWW, 1>), g1, b1, 0, st, sa, sa.br, sa.begins, an);
-        else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, kFmtF32, 0, PWW, 1>), g1, b1, 0, st, sa, sa.br, sa.begins, an);
-        else hipLaunchKernelGGL((qsgd_spec_quant<4, true, kFmtF32, 0, PWW, 1>), g1, b1, 0, st, sa, sa.br, sa.begins, an);
+        if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF32, 0, PWW, 1>), g1, b1, plds_w, st, sa, sa.br, sa.begins, an);
+        else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant<1, true, kFmtF32, 0, PWW, 1>), g1, b1, plds_w, st, sa, sa.br, sa.begins, an);
+        else if (!div) hipLaunchKernelGGL((qsgd_spec_quant<4, false, kFmtF32, 0, PWW, 1>), g1, b1, plds_w, st, sa, sa.br, sa.begins, an);
+        else hipLaunchKernelGGL((qsgd_spec_quant<4, true, kFmtF32, 0, PWW, 1>), g1, b1, plds_w, st, sa, sa.br, sa.begins, an);
       }
     } else if (fmt == kFmtBF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtBF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
     else if (fmt == kFmtF16) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF16>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
@@ -2845,6 +2850,10 @@ static int decode_blocks(omf_plan* p, const void* q, int32_t width, int32_t leve
   if (b1 <= b0) return OMF_OK;
   const dim3 blk(kThreads);
   hipStream_t st = (hipStream_t)stream;
+  // A plain decode's workgroups reserve 24 KiB of LDS each (unused): six per CU — Llama-400M 0.294-
+  // 0.296 ms at s = 4 and 0.482-0.484 at s = 8 against 0.301 / 0.490 uncapped, 0.308 / 0.489 at 28 KiB
+  // (scripts/exp/occ_ab.sh); OMF_DEC_LDS overrides.  Accumulating decodes keep every wave.
+  static const size_t dlds = [] { const char* v = getenv("OMF_DEC_LDS"); return v ? (size_t)atoi(v) : (size_t)24576; }();
   // the last whole quad of the payload the caller holds (width 8: round_up(arena_end, 4) bytes
   // are not promised, so a clamped load never passes the last full quad)
   const int64_t qlast = (p->arena_end & ~(int64_t)3) - 4;  // < 0 only for arenas of < 4 elements
@@ -2852,7 +2861,7 @@ static int decode_blocks(omf_plan* p, const void* q, int32_t width, int32_t leve
   do {                                                                                                           \
     if (qlast >= 0) {                                                                                            \
       const int64_t per = kDecBlk / (kDecQuads<W, A> * kThreads * 4); /* decode blocks per table block */       \
-      hipLaunchKernelGGL((qsgd_decode_arena<W, A, P>), dim3((unsigned)((b1 - b0) * per)), blk, 0, st, a,         \
+      hipLaunchKernelGGL((qsgd_decode_arena<W, A, P>), dim3((unsigned)((b1 - b0) * per)), blk, A ? 0 : dlds, st, a, \
                          (const uint32_t*)p->d_dec_binfo, norm, (const int64_t*)p->d_begins,                    \
                          (const int64_t*)p->d_sizes, p->nt, qlast, (uint32_t)(b0 * per));                       \
     } else /* a payload of < 4 elements: the item decoder's byte loads */                                          \

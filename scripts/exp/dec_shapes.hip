@@ -122,6 +122,7 @@ struct Shape {
   void (*fn)(const void*, float*, float, float, int64_t);
   int blk_elems, threads;
   bool acc;
+  int lds = 0;  // dynamic LDS bytes per workgroup: caps workgroups per CU (160 KiB / lds)
 };
 
 #define SH(W, V, T, L, S, X) Shape{"W" #W " V" #V " T" #T " ntl" #L " nts" #S " xcd" #X, \
@@ -137,7 +138,12 @@ int main(int argc, char** argv) {
   const int64_t n = 401122304;
   const int W = argc > 1 ? atoi(argv[1]) : 1;
   std::vector<Shape> shapes;
-  if (W == 1) {
+  if (argc > 2) {  // occupancy sweep of the encoder shapes
+    for (int lds : {0, 16384, 24576, 32768, 40960}) {
+      Shape a = W == 1 ? SHE(1, 4, 256) : SHE(4, 4, 256); a.lds = lds; shapes.push_back(a);
+      Shape b = W == 1 ? SHE(1, 2, 256) : SHE(4, 1, 256); b.lds = lds; shapes.push_back(b);
+    }
+  } else if (W == 1) {
     shapes = {SH(1, 4, 256, 1, 1, 0), SH(1, 2, 256, 1, 1, 0), SH(1, 2, 128, 1, 1, 0), SH(1, 4, 128, 1, 1, 0),
               SH(1, 1, 512, 1, 1, 0), SH(1, 1, 1024, 1, 1, 0), SH(1, 2, 512, 1, 1, 0), SH(1, 2, 256, 0, 1, 0),
               SHA(1, 4, 256), SHA(1, 2, 256), SHA(1, 1, 256), SHA(1, 1, 512),
@@ -160,9 +166,9 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < shapes.size(); ++i) {
       const Shape& s = shapes[i];
       const int grid = (int)((n + s.blk_elems - 1) / s.blk_elems);
-      hipLaunchKernelGGL(s.fn, dim3(grid), dim3(s.threads), 0, 0, q, y, 1.5f, 0.125f, n);
+      hipLaunchKernelGGL(s.fn, dim3(grid), dim3(s.threads), s.lds, 0, q, y, 1.5f, 0.125f, n);
       CK(hipEventRecord(a));
-      for (int k = 0; k < reps; ++k) hipLaunchKernelGGL(s.fn, dim3(grid), dim3(s.threads), 0, 0, q, y, 1.5f, 0.125f, n);
+      for (int k = 0; k < reps; ++k) hipLaunchKernelGGL(s.fn, dim3(grid), dim3(s.threads), s.lds, 0, q, y, 1.5f, 0.125f, n);
       CK(hipEventRecord(b));
       CK(hipEventSynchronize(b));
       float t;
@@ -174,7 +180,9 @@ int main(int argc, char** argv) {
     std::sort(ms[i].begin(), ms[i].end());
     const double med = ms[i][rounds / 2];
     const double bytes = (double)n * (W + (shapes[i].acc ? 8 : 4));
-    printf("%-36s median %.4f ms  min %.4f  %.2f TB/s\n", shapes[i].name, med, ms[i][0], bytes / med / 1e9);
+    char nm[96];
+    snprintf(nm, sizeof nm, "%s%s", shapes[i].name, shapes[i].lds ? (shapes[i].lds == 16384 ? " lds16K" : shapes[i].lds == 24576 ? " lds24K" : shapes[i].lds == 32768 ? " lds32K" : " lds40K") : "");
+    printf("%-36s median %.4f ms  min %.4f  %.2f TB/s\n", nm, med, ms[i][0], bytes / med / 1e9);
   }
   return 0;
 }
