@@ -18,7 +18,7 @@
 //                       magnitude (about the k-th, 1.5 sigma above) and the fine-bin map.
 //   2. topk_fused       ONE streaming pass: read x (+ residual), write the residual, append
 //                       every |t'| at or above the threshold as index << 32 | bits(t') to the
-//                       1 Ki-element sub-chunk's own range (one block scan, no atomics).
+//                       512-element sub-chunk's own range (one block scan, no atomics).
 //   3. topk_fine_hist   exact fine-bin histogram of the candidates (LDS per super-item).
 //   4. topk_plan        per tensor: the fine bins above rank k -> buckets of <= 4096 keys with
 //                       known first ranks; the last block publishes the verdict to host memory.
@@ -91,7 +91,14 @@ constexpr int kBucketHalf = 2048;
 constexpr int kBT = 512;              // bucket-sort block: 512 threads x 8 keys = 2 kBucketHalf
 constexpr int kBI = 8;
 constexpr int kPlanMaxBuckets = (1 << 25) / kBucketHalf + 2;
-constexpr int kSupItems = 64;         // items per super-item (x 16 sub-chunks = 1024 runs)
+#ifndef OMF_TK_SUBPER  // experiment builds may override it
+#define OMF_TK_SUBPER 512
+#endif
+constexpr int kSubPer = OMF_TK_SUBPER;        // elements per block of the fused pass
+constexpr int kSubThreads = kSubPer / 4;      // one float4 per thread: 128 threads, two waves
+constexpr int kSubWaves = kSubThreads / 64;
+constexpr int kSubsPerItem = (int)(kSub / kSubPer);  // 32
+constexpr int kSupItems = 1024 / kSubsPerItem;  // items per super-item (x 32 sub-chunks = 1024 runs)
 
 // One bucket of the fast path: its keys at bkeys[key_off, + count), its first rank `start`
 // within the tensor; count | tensor << 16 (a bucket holds <= 2 kBucketHalf keys).
@@ -262,7 +269,6 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, uin
   constexpr int PER = kSBins / 1024;
   __shared__ uint32_t s_w[16];
   for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;  // this call's redo histogram
-  for (uint32_t i = tfirst[t] + threadIdx.x; i <= tlast[t]; i += 1024) item_cnt[i] = 0;  // the fused pass adds to them
   uint32_t c[PER], loc = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -556,23 +562,22 @@ struct PassCollector {
 };
 
 // Pass 3: t' (written to the residual in the EF modes) and the candidates above the
-// sampled threshold.  One 256-thread block per 1 Ki-element sub-chunk of an item (sub j of
-// item i is block 16 i + j), one float4 of x (and r) per thread: the shape that streams
+// sampled threshold.  One 128-thread block per 512-element sub-chunk of an item (sub j of
+// item i is block 32 i + j), one float4 of x (and r) per thread: the shape that streams
 // fastest here (scripts/exp/ef_probe.py: r += x at 5.6 TB/s with one float4 per thread vs
-// 5.1 with 8 per thread or a persistent grid).  The sub's candidates go to its own element
+// 5.1 with 8 per thread or a persistent grid; round 5, scripts/exp/dec_shapes.hip: 0.733 ms
+// for Llama-400M's 12 N with 128-thread blocks against 0.763 with 256, 0.793 with 512).  The sub's candidates go to its own element
 // range of `cand` in index order (one wave scan + one barrier), its count to sub_cnt.
 // MODE 0: t' = alpha x (not stored); 1: r := r + alpha x; 2: r := alpha x.
-constexpr int kSubPer = 1024;                 // elements per block of the fused pass
-constexpr int kSubsPerItem = (int)(kSub / kSubPer);  // 16
 template <int MODE>
-__global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__ x, float* __restrict__ r, float alpha,
+__global__ __launch_bounds__(kSubThreads) void topk_fused(const float* __restrict__ x, float* __restrict__ r, float alpha,
                                                        const Item* __restrict__ items,
                                                        const int64_t* __restrict__ tbegin,
                                                        const uint32_t* __restrict__ tkey,
                                                        const uint32_t* __restrict__ thi,
                                                        uint32_t* __restrict__ sub_cnt, uint32_t* __restrict__ item_cnt,
                                                        uint64_t* __restrict__ cand, uint32_t sub0) {
-  __shared__ uint32_t s_w[kWaves];
+  __shared__ uint32_t s_w[kSubWaves];
   const uint32_t bid = sub0 + blockIdx.x;
   const Item it = items[bid / kSubsPerItem];
   const int64_t b = it.begin + (int64_t)(bid % kSubsPerItem) * kSubPer;
@@ -630,7 +635,7 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
   __syncthreads();
   uint32_t pos = inc - mine, total = 0;
 #pragma unroll
-  for (int w2 = 0; w2 < kWaves; ++w2) {
+  for (int w2 = 0; w2 < kSubWaves; ++w2) {
     const uint32_t ws = s_w[w2];
     if (w2 < wave) pos += ws;
     total += ws;
@@ -642,10 +647,22 @@ __global__ __launch_bounds__(kThreads) void topk_fused(const float* __restrict__
     for (int c = 0; c < 4; ++c)
       if ((selm >> c) & 1u) dst[pos++] = ((uint64_t)(idx0 + c) << 32) | (uint64_t)__float_as_uint(vv[c]);
   }
-  if (threadIdx.x == 0) {
-    sub_cnt[bid] = total;
-    if (total) atomicAdd(&item_cnt[bid / kSubsPerItem], total);
+  if (threadIdx.x == 0) sub_cnt[bid] = total;  // (the fallback sums an item's subs: topk_item_counts)
+}
+
+// Fallback path: each item's candidate count, the sum of its sub-chunks' (one thread per item).
+__global__ __launch_bounds__(kThreads) void topk_item_counts(const uint32_t* __restrict__ sub_cnt, int64_t n_items,
+                                                             uint32_t* __restrict__ item_cnt) {
+  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n_items) return;
+  const uint4* p = reinterpret_cast<const uint4*>(sub_cnt + i * kSubsPerItem);
+  uint32_t c = 0;
+#pragma unroll
+  for (int j = 0; j < kSubsPerItem / 4; ++j) {
+    const uint4 v = p[j];
+    c += v.x + v.y + v.z + v.w;
   }
+  item_cnt[i] = c;
 }
 
 // One block: exclusive scan of the per-item candidate counts (items in tensor order) in
@@ -875,7 +892,7 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
   if (GLOBAL && threadIdx.x == 0) item_cnt[blockIdx.x] = item_total;
 }
 
-// The 16 sub-chunk candidate counts of item `item` -> s_pre[0..16] (exclusive prefix, s_pre[16]
+// The kSubsPerItem sub-chunk candidate counts of item `item` -> s_pre[0..32] (exclusive prefix, s_pre[32]
 // = the item's total).  Wave 0 scans; ends with a block barrier.
 __device__ __forceinline__ void item_prefix(const uint32_t* __restrict__ sub_cnt, int64_t item, uint32_t* s_pre) {
   if (threadIdx.x < 64) {
@@ -942,7 +959,7 @@ struct SupView {
     first = si.w != 0u;
     const uint32_t i0 = si.y, ni = si.z;
     s_map[threadIdx.x] = fmap[(size_t)t * kCoarse + threadIdx.x];  // 1024 threads = kCoarse
-    const uint32_t run = threadIdx.x;  // run j of item j / 16
+    const uint32_t run = threadIdx.x;  // run j of item j / kSubsPerItem
     const uint32_t c = run < ni * kSubsPerItem ? sub_cnt[(size_t)i0 * kSubsPerItem + run] : 0u;
     if (threadIdx.x < ni) s_ibeg[threadIdx.x] = items[i0 + threadIdx.x].begin;
     uint32_t tot;
@@ -957,7 +974,7 @@ struct SupView {
 #pragma unroll
     for (int h = 512; h > 0; h >>= 1)
       if (s_spre[j + h] <= e) j += h;
-    return s_ibeg[j >> 4] + (int64_t)(j & 15) * kSubPer + (e - s_spre[j]);
+    return s_ibeg[j / kSubsPerItem] + (int64_t)(j % kSubsPerItem) * kSubPer + (e - s_spre[j]);
   }
 };
 
@@ -1699,7 +1716,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 // sub's non-zeros from their candidate keys in an LDS bitmap, and ranks its zeros with a block
 // scan; value = t' (the sign of the zero), residual := t' - t' (+0).  Launched only when the
 // plan's verdict reports a zero fill.
-__global__ __launch_bounds__(kThreads) void topk_zero_fill(const uint2* __restrict__ zmap,
+__global__ __launch_bounds__(kSubThreads) void topk_zero_fill(const uint2* __restrict__ zmap,
                                                            const uint32_t* __restrict__ zcnt,
                                                            const int64_t* __restrict__ kk,
                                                            const int64_t* __restrict__ koff,
@@ -1713,8 +1730,8 @@ __global__ __launch_bounds__(kThreads) void topk_zero_fill(const uint2* __restri
                                                            float* __restrict__ r, float* __restrict__ values,
                                                            int64_t* __restrict__ indices) {
   __shared__ uint32_t s_bm[kSubPer / 32];
-  __shared__ uint32_t s_w[kWaves];
-  __shared__ uint32_t s_sum[kWaves];
+  __shared__ uint32_t s_w[kSubWaves];
+  __shared__ uint32_t s_sum[kSubWaves];
   const uint2 zm = zmap[blockIdx.x];
   const int t = (int)zm.x;
   const uint32_t x = zm.y;
@@ -1725,7 +1742,7 @@ __global__ __launch_bounds__(kThreads) void topk_zero_fill(const uint2* __restri
   const uint32_t s0 = tfirst[t] * (uint32_t)kSubsPerItem;
   // non-zeros before this sub
   uint32_t nz = 0;
-  for (uint32_t j = threadIdx.x; j < x; j += kThreads) nz += sub_cnt[s0 + j];
+  for (uint32_t j = threadIdx.x; j < x; j += kSubThreads) nz += sub_cnt[s0 + j];
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) nz += __shfl_xor(nz, o, 64);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1734,14 +1751,14 @@ __global__ __launch_bounds__(kThreads) void topk_zero_fill(const uint2* __restri
   __syncthreads();
   uint32_t nzb = 0;
 #pragma unroll
-  for (int w2 = 0; w2 < kWaves; ++w2) nzb += s_sum[w2];
+  for (int w2 = 0; w2 < kSubWaves; ++w2) nzb += s_sum[w2];
   const int64_t z = k - (int64_t)c;                 // zeros to select
   const int64_t zr0 = rel0 - (int64_t)nzb;          // zeros before this sub
   if (zr0 >= z) return;                             // block-uniform
   const uint32_t g = s0 + x;
   const int64_t b = items[g / kSubsPerItem].begin + (int64_t)(g % kSubsPerItem) * kSubPer;
   const uint32_t cx = sub_cnt[g];
-  for (uint32_t e = threadIdx.x; e < cx; e += kThreads) {
+  for (uint32_t e = threadIdx.x; e < cx; e += kSubThreads) {
     const uint32_t rel = (uint32_t)(cand[b + e] >> 32) - (uint32_t)rel0;  // < kSubPer
     atomicOr(&s_bm[rel >> 5], 1u << (rel & 31));
   }
@@ -1763,7 +1780,7 @@ __global__ __launch_bounds__(kThreads) void topk_zero_fill(const uint2* __restri
   __syncthreads();
   uint32_t pos = inc - mine;
 #pragma unroll
-  for (int w2 = 0; w2 < kWaves; ++w2)
+  for (int w2 = 0; w2 < kSubWaves; ++w2)
     if (w2 < wave) pos += s_w[w2];
   const int64_t out0 = koff[t] + (int64_t)c;
 #pragma unroll
@@ -2661,13 +2678,13 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       if (gi > 0) OMF_HIP(hipStreamWaitEvent(s, hsync->fused[(gi - 1) & 1], 0));
       const dim3 fgrid(G.nsub);
       if (residual_mode == 1)
-        hipLaunchKernelGGL((topk_fused<1>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
+        hipLaunchKernelGGL((topk_fused<1>), fgrid, dim3(kSubThreads), 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
                            item_cnt, cand, G.sub0);
       else if (residual_mode == 2)
-        hipLaunchKernelGGL((topk_fused<2>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
+        hipLaunchKernelGGL((topk_fused<2>), fgrid, dim3(kSubThreads), 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
                            item_cnt, cand, G.sub0);
       else
-        hipLaunchKernelGGL((topk_fused<0>), fgrid, blk, 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
+        hipLaunchKernelGGL((topk_fused<0>), fgrid, dim3(kSubThreads), 0, s, x, residual, alpha, items, d_begins, tkey, thi, sub_cnt,
                            item_cnt, cand, G.sub0);
       if (groups.size() > 1) OMF_HIP(hipEventRecord(hsync->fused[gi & 1], s));
       // fast path: exact fine-bin histograms, bucket plan
@@ -2716,7 +2733,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       ++stats.fast;
       if (host_status[0]) {  // zero mode: complete the short tensors with their lowest-index zeros
         ++stats.zero_fill;
-        hipLaunchKernelGGL(topk_zero_fill, dim3((unsigned)tb.nzb), blk, 0, st, (const uint2*)tb.zmap, zcnt, kk, koff,
+        hipLaunchKernelGGL(topk_zero_fill, dim3((unsigned)tb.nzb), dim3(kSubThreads), 0, st, (const uint2*)tb.zmap, zcnt, kk, koff,
                            d_begins, d_sizes, tfirst, items, sub_cnt, cand, tp, scale, rz, values, indices);
         OMF_HIP(hipGetLastError());
       }
@@ -2726,6 +2743,8 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     if (host_status[1]) ++stats.redo;
     // fallback (a redo, a fine bin over kBucketHalf keys, or forced): device-wide radix sort
     if (rz) hipLaunchKernelGGL(topk_restore, grid, blk, 0, st, cand, items, sub_cnt, d_begins, rz);
+    hipLaunchKernelGGL(topk_item_counts, dim3((unsigned)((n_items + kThreads - 1) / kThreads)), blk, 0, st, sub_cnt,
+                       (int64_t)n_items, item_cnt);
     auto scan_and_check = [&]() -> int {
       hipLaunchKernelGGL(topk_scan_check, dim3(1), dim3(1024), 0, st, nt, kk, tfirst, tlast, item_cnt, item_off,
                          n_items, cstart, cnt, flag, status);
