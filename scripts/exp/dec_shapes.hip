@@ -117,6 +117,86 @@ __global__ __launch_bounds__(64 * WPB) void encw(const void* __restrict__ q, flo
   }
 }
 
+// Error-feedback shape (Top-K's streaming pass): r = r + x, V float4 of each per thread.
+template <int V, int T>
+__global__ __launch_bounds__(T) void efb(const void* __restrict__ q, float* __restrict__ y, float norm, float inv, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * (V * T * 4);
+  const float* x = reinterpret_cast<const float*>(q);
+  f32x4 a[V], b[V];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = min(base + 4 * ((int64_t)k * T + threadIdx.x), n - 4);
+    a[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(x + e));
+    b[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(y + e));
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = base + 4 * ((int64_t)k * T + threadIdx.x);
+    if (e >= n) continue;
+    f32x4 o = a[k] * norm + b[k];
+    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(y + e));
+  }
+}
+
+// Write-only stream (the Top-K decode's zero-filled tiles): V float4 stores per thread.
+template <int V, int T>
+__global__ __launch_bounds__(T) void wro(const void* __restrict__ q, float* __restrict__ y, float norm, float inv, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * (V * T * 4);
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = base + 4 * ((int64_t)k * T + threadIdx.x);
+    if (e >= n) continue;
+    const f32x4 o = {norm, 0.f, inv, 0.f};
+    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(y + e));
+  }
+}
+
+// Wave-contiguous layouts: wave w of the workgroup owns V consecutive 1 KiB pieces (lane l of
+// store k at 4 (w 64 V + k 64 + l)) instead of pieces T x 16 bytes apart.
+template <int V, int T>
+__global__ __launch_bounds__(T) void wroc(const void* __restrict__ q, float* __restrict__ y, float norm, float inv, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * (V * T * 4);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = base + 4 * ((int64_t)w * 64 * V + k * 64 + l);
+    if (e >= n) continue;
+    const f32x4 o = {norm, 0.f, inv, 0.f};
+    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(y + e));
+  }
+}
+template <int W, int V, int T>
+__global__ __launch_bounds__(T) void decc(const void* __restrict__ q, float* __restrict__ y, float norm, float inv, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * (V * T * 4);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  int32_t raw[V][W == 1 ? 1 : 4];
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = min(base + 4 * ((int64_t)w * 64 * V + k * 64 + l), n - 4);
+    if (W == 1) {
+      raw[k][0] = *reinterpret_cast<const int32_t*>(reinterpret_cast<const int8_t*>(q) + e);
+    } else {
+      const i32x4 t = __builtin_nontemporal_load(reinterpret_cast<const i32x4*>(reinterpret_cast<const int32_t*>(q) + e));
+      raw[k][0] = t[0]; raw[k][1] = t[1]; raw[k][2] = t[2]; raw[k][3] = t[3];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < V; ++k) {
+    const int64_t e = base + 4 * ((int64_t)w * 64 * V + k * 64 + l);
+    if (e >= n) continue;
+    int32_t qi[4];
+    if (W == 1) {
+      qi[0] = (int8_t)(raw[k][0] & 0xff); qi[1] = (int8_t)((raw[k][0] >> 8) & 0xff);
+      qi[2] = (int8_t)((raw[k][0] >> 16) & 0xff); qi[3] = (int8_t)((raw[k][0] >> 24) & 0xff);
+    } else {
+      qi[0] = raw[k][0]; qi[1] = raw[k][1]; qi[2] = raw[k][2]; qi[3] = raw[k][3];
+    }
+    f32x4 o;
+    for (int c = 0; c < 4; ++c) o[c] = __fmul_rn(__fmul_rn(norm, (float)qi[c]), inv);
+    __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(y + e));
+  }
+}
+
 struct Shape {
   const char* name;
   void (*fn)(const void*, float*, float, float, int64_t);
@@ -131,6 +211,14 @@ struct Shape {
                            (void (*)(const void*, float*, float, float, int64_t))enc<W, V, T>, V * T * 4, T, false}
 #define SHW(W, WPB) Shape{"ENCW W" #W " wpb" #WPB, \
                            (void (*)(const void*, float*, float, float, int64_t))encw<W, WPB>, 1024 * WPB, 64 * WPB, false}
+#define SHF(V, T) Shape{"EF V" #V " T" #T, \
+                           (void (*)(const void*, float*, float, float, int64_t))efb<V, T>, V * T * 4, T, true}
+#define SHWR(V, T) Shape{"WR V" #V " T" #T, \
+                           (void (*)(const void*, float*, float, float, int64_t))wro<V, T>, V * T * 4, T, false}
+#define SHWC(V, T) Shape{"WRC V" #V " T" #T, \
+                           (void (*)(const void*, float*, float, float, int64_t))wroc<V, T>, V * T * 4, T, false}
+#define SHDC(W, V, T) Shape{"DECC W" #W " V" #V " T" #T, \
+                           (void (*)(const void*, float*, float, float, int64_t))decc<W, V, T>, V * T * 4, T, false}
 #define SHA(W, V, T) Shape{"ACC W" #W " V" #V " T" #T, \
                            (void (*)(const void*, float*, float, float, int64_t))dec<W, V, T, true, true, false, true>, V * T * 4, T, true}
 
@@ -138,7 +226,27 @@ int main(int argc, char** argv) {
   const int64_t n = 401122304;
   const int W = argc > 1 ? atoi(argv[1]) : 1;
   std::vector<Shape> shapes;
-  if (argc > 2) {  // occupancy sweep of the encoder shapes
+  if (argc > 2 && W == 100) {  // wave-contiguous write-only
+    for (int lds : {0, 24576, 40960}) {
+      for (Shape a : {SHWR(1, 256), SHWR(8, 512), SHWC(8, 512), SHWC(4, 256), SHWC(8, 256), SHWC(16, 256)}) { a.lds = lds; shapes.push_back(a); }
+    }
+  } else if (argc > 2 && (W == 101 || W == 104)) {  // wave-contiguous decode
+    const int w = W - 100;
+    for (int lds : {0, 24576, 40960}) {
+      for (Shape a : (w == 1 ? std::vector<Shape>{SH(1, 2, 256, 0, 1, 0), SH(1, 4, 256, 0, 1, 0), SHDC(1, 4, 256), SHDC(1, 2, 256), SHDC(1, 8, 256)}
+                             : std::vector<Shape>{SH(4, 1, 256, 1, 1, 0), SH(4, 4, 256, 1, 1, 0), SHDC(4, 4, 256), SHDC(4, 2, 256), SHDC(4, 8, 256)})) {
+        a.lds = lds; shapes.push_back(a);
+      }
+    }
+  } else if (argc > 2 && W == 0) {  // write-only
+    for (int lds : {0, 24576, 40960}) {
+      for (Shape a : {SHWR(1, 256), SHWR(2, 256), SHWR(4, 256), SHWR(8, 256), SHWR(1, 128), SHWR(4, 512), SHWR(16, 512)}) { a.lds = lds; shapes.push_back(a); }
+    }
+  } else if (argc > 2 && W == 12) {  // the error-feedback shape (12 bytes per element)
+    for (int lds : {0, 16384, 24576}) {
+      for (Shape a : {SHF(1, 256), SHF(2, 256), SHF(1, 512), SHF(1, 128), SHF(2, 128)}) { a.lds = lds; shapes.push_back(a); }
+    }
+  } else if (argc > 2) {  // occupancy sweep of the encoder shapes
     for (int lds : {0, 16384, 24576, 32768, 40960}) {
       Shape a = W == 1 ? SHE(1, 4, 256) : SHE(4, 4, 256); a.lds = lds; shapes.push_back(a);
       Shape b = W == 1 ? SHE(1, 2, 256) : SHE(4, 1, 256); b.lds = lds; shapes.push_back(b);
@@ -155,9 +263,10 @@ int main(int argc, char** argv) {
               SHE(4, 4, 256), SHE(4, 2, 256), SHE(4, 1, 256), SHE(4, 8, 256), SHE(4, 1, 512), SHW(4, 4), SHW(4, 2), SHW(4, 1)};
   }
   void* q; float* y;
-  CK(hipMalloc(&q, n * W + 64));
+  const int qb = W == 12 ? 4 : (W == 0 || W == 100) ? 1 : W > 100 ? W - 100 : W;
+  CK(hipMalloc(&q, n * qb + 64));
   CK(hipMalloc(&y, n * 4 + 64));
-  CK(hipMemset(q, 3, n * W));
+  CK(hipMemset(q, 3, n * qb));
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   const int reps = 20, rounds = 7;
@@ -179,7 +288,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < shapes.size(); ++i) {
     std::sort(ms[i].begin(), ms[i].end());
     const double med = ms[i][rounds / 2];
-    const double bytes = (double)n * (W + (shapes[i].acc ? 8 : 4));
+    const double bytes = (W == 0 || W == 100) ? 4.0 * n : W > 100 ? (double)n * (W - 100 + 4) : W == 12 ? 12.0 * n : (double)n * (W + (shapes[i].acc ? 8 : 4));
     char nm[96];
     snprintf(nm, sizeof nm, "%s%s", shapes[i].name, shapes[i].lds ? (shapes[i].lds == 16384 ? " lds16K" : shapes[i].lds == 24576 ? " lds24K" : shapes[i].lds == 32768 ? " lds32K" : " lds40K") : "");
     printf("%-36s median %.4f ms  min %.4f  %.2f TB/s\n", nm, med, ms[i][0], bytes / med / 1e9);
