@@ -1711,11 +1711,14 @@ struct omf_plan {
   uint32_t* d_spec_cnt = nullptr;  // fold_cnt x nt
   uint32_t spec_epoch = 0;
   uint32_t spec_skip = 0;  // test / experiment switches (omf_plan_set_debug), 0 in production
-  float spec_zsig = 6.0f;  // experiment switch (OMF_SPEC_ZSIG): the bracket's width in sigmas
-  // wide levels: 5 sigmas (a tensor whose norm falls outside is requantised whole, exactly; the
-  // narrower bracket lists fewer undecided quads: Llama-400M s = 8 encode 0.601-0.611 ms against
-  // 0.616-0.622 at 6, profiles/r05_s8_variants.txt)
-  float spec_zsig_wide = 5.0f;
+  // The bracket's width in sigmas (OMF_SPEC_ZSIG overrides both): a tensor whose norm falls
+  // outside is requantised whole by the finish (exact; a miss per tensor at z sigmas has
+  // probability ~erfc(z / sqrt 2): 6e-5 at 4, 6e-7 at 5), and a narrower bracket lists fewer
+  // undecided quads.  scripts/exp/zsig_ab.sh, Llama-400M, two interleaved rounds: s = 4 encode
+  // 0.349-0.352 ms at 5 sigmas against 0.357-0.361 at 6 (4: 0.350); s = 8 0.546-0.547 ms at 4
+  // against 0.556-0.559 at 5 (3.5: 0.542-0.545).
+  float spec_zsig = 5.0f;
+  float spec_zsig_wide = 4.0f;
   SpecBracket* d_spec_br = nullptr;
   uint64_t* d_spec_ngran = nullptr;  // per tensor {epoch << 1 | bad, norm} granules of the fold
   uint64_t* d_spec_part = nullptr;
