@@ -197,6 +197,29 @@ __global__ __launch_bounds__(T) void decc(const void* __restrict__ q, float* __r
   }
 }
 
+// The encoder shape with its block's start read from a table first (the bracketed pass's item
+// lookup before its loads): IND = 1 table load, 0 = arithmetic.
+__device__ int64_t* g_btab;
+template <int IND>
+__global__ __launch_bounds__(256) void enci(const void* __restrict__ q, float* __restrict__ y, float norm, float inv, int64_t n) {
+  const int64_t base = IND ? reinterpret_cast<const int64_t* __restrict__>(g_btab)[blockIdx.x] : (int64_t)blockIdx.x * 4096;
+  f32x4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t e = min(base + 4 * ((int64_t)k * 256 + threadIdx.x), n - 4);
+    v[k] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(y + e));
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t e = base + 4 * ((int64_t)k * 256 + threadIdx.x);
+    if (e >= n) continue;
+    int32_t l[4];
+    for (int c = 0; c < 4; ++c) l[c] = (int32_t)__builtin_ceilf(__fmul_rn(v[k][c], norm) - inv);
+    const uint32_t w = (uint32_t)(l[0] & 0xff) | (uint32_t)(l[1] & 0xff) << 8 | (uint32_t)(l[2] & 0xff) << 16 | (uint32_t)l[3] << 24;
+    __builtin_nontemporal_store(w, reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(const_cast<void*>(q)) + e));
+  }
+}
+
 struct Shape {
   const char* name;
   void (*fn)(const void*, float*, float, float, int64_t);
@@ -219,6 +242,7 @@ struct Shape {
                            (void (*)(const void*, float*, float, float, int64_t))wroc<V, T>, V * T * 4, T, false}
 #define SHDC(W, V, T) Shape{"DECC W" #W " V" #V " T" #T, \
                            (void (*)(const void*, float*, float, float, int64_t))decc<W, V, T>, V * T * 4, T, false}
+#define SHI(I) Shape{"ENCI ind" #I, (void (*)(const void*, float*, float, float, int64_t))enci<I>, 4096, 256, false}
 #define SHA(W, V, T) Shape{"ACC W" #W " V" #V " T" #T, \
                            (void (*)(const void*, float*, float, float, int64_t))dec<W, V, T, true, true, false, true>, V * T * 4, T, true}
 
@@ -226,7 +250,9 @@ int main(int argc, char** argv) {
   const int64_t n = 401122304;
   const int W = argc > 1 ? atoi(argv[1]) : 1;
   std::vector<Shape> shapes;
-  if (argc > 2 && W == 100) {  // wave-contiguous write-only
+  if (argc > 2 && W == 200) {  // table-indirected block starts
+    shapes = {SHI(0), SHI(1), SHE(1, 4, 256)};
+  } else if (argc > 2 && W == 100) {  // wave-contiguous write-only
     for (int lds : {0, 24576, 40960}) {
       for (Shape a : {SHWR(1, 256), SHWR(8, 512), SHWC(8, 512), SHWC(4, 256), SHWC(8, 256), SHWC(16, 256)}) { a.lds = lds; shapes.push_back(a); }
     }
@@ -263,7 +289,15 @@ int main(int argc, char** argv) {
               SHE(4, 4, 256), SHE(4, 2, 256), SHE(4, 1, 256), SHE(4, 8, 256), SHE(4, 1, 512), SHW(4, 4), SHW(4, 2), SHW(4, 1)};
   }
   void* q; float* y;
-  const int qb = W == 12 ? 4 : (W == 0 || W == 100) ? 1 : W > 100 ? W - 100 : W;
+  if (W == 200) {
+    std::vector<int64_t> bt((n + 4095) / 4096);
+    for (size_t i = 0; i < bt.size(); ++i) bt[i] = (int64_t)i * 4096;
+    int64_t* d;
+    CK(hipMalloc(&d, bt.size() * 8));
+    CK(hipMemcpy(d, bt.data(), bt.size() * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(g_btab), &d, sizeof(d)));
+  }
+  const int qb = W == 200 ? 1 : W == 12 ? 4 : (W == 0 || W == 100) ? 1 : W > 100 ? W - 100 : W;
   CK(hipMalloc(&q, n * qb + 64));
   CK(hipMalloc(&y, n * 4 + 64));
   CK(hipMemset(q, 3, n * qb));
@@ -288,7 +322,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < shapes.size(); ++i) {
     std::sort(ms[i].begin(), ms[i].end());
     const double med = ms[i][rounds / 2];
-    const double bytes = (W == 0 || W == 100) ? 4.0 * n : W > 100 ? (double)n * (W - 100 + 4) : W == 12 ? 12.0 * n : (double)n * (W + (shapes[i].acc ? 8 : 4));
+    const double bytes = W == 200 ? 5.0 * n : (W == 0 || W == 100) ? 4.0 * n : W > 100 ? (double)n * (W - 100 + 4) : W == 12 ? 12.0 * n : (double)n * (W + (shapes[i].acc ? 8 : 4));
     char nm[96];
     snprintf(nm, sizeof nm, "%s%s", shapes[i].name, shapes[i].lds ? (shapes[i].lds == 16384 ? " lds16K" : shapes[i].lds == 24576 ? " lds24K" : shapes[i].lds == 32768 ? " lds32K" : " lds40K") : "");
     printf("%-36s median %.4f ms  min %.4f  %.2f TB/s\n", nm, med, ms[i][0], bytes / med / 1e9);

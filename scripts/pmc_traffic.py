@@ -28,8 +28,11 @@ def load(d, counter):
     return per
 
 
-TOPK_ENCODE = ("topk_sample", "topk_fused", "topk_fine_hist", "topk_plan",
-               "topk_bucket_scatter", "topk_bucket_sort")
+# one encode call's launches: the planned scatter (the default since round 5), or plan + scatter
+TOPK_ENCODE_SETS = (("topk_sample", "topk_fused", "topk_fine_hist", "topk_scatter_planned", "topk_bucket_sort"),
+                    ("topk_sample", "topk_fused", "topk_fine_hist", "topk_plan", "topk_bucket_scatter",
+                     "topk_bucket_sort"))
+TOPK_ENCODE = tuple(sorted(set(TOPK_ENCODE_SETS[0] + TOPK_ENCODE_SETS[1])))
 TOPK_DECODE = ("topk_dec_place", "topk_dec_tiles", "topk_dec_overflow")
 
 
@@ -66,7 +69,8 @@ def main():
             res["qsgd_spec_all"]["launches"] = res[spec[-2]]["launches"]
             break
     # Top-K: every launch of one encode call (resp. one tiled decode call), summed
-    for agg, parts in (("topk_encode_all", TOPK_ENCODE), ("topk_decode_all", TOPK_DECODE)):
+    enc = next((p for p in TOPK_ENCODE_SETS if all(k in res for k in p)), TOPK_ENCODE_SETS[0])
+    for agg, parts in (("topk_encode_all", enc), ("topk_decode_all", TOPK_DECODE)):
         if all(k in res for k in parts):
             res[agg] = {kk: sum(res[k][kk] for k in parts) for kk in ("fetch_bytes_corrected", "write_bytes")}
             res[agg]["launches"] = res[parts[-1]]["launches"]
