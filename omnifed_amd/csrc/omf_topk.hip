@@ -248,6 +248,9 @@ __device__ __forceinline__ int64_t sample_stride(int64_t n, int64_t max_runs) {
 #define OMF_SRUNS_PER_BLOCK 2048
 #endif
 constexpr int kSRunsPerBlock = OMF_SRUNS_PER_BLOCK;
+#ifndef OMF_SAMPLE_HIST_LATE  // experiment builds: 0 clears the redo histogram before the threshold's barriers
+#define OMF_SAMPLE_HIST_LATE 1
+#endif
 
 // The tensor's threshold from its sample histogram h (LDS, kSBins, loaded; 1024 threads) of
 // the non-zero samples and its count of exact-zero samples `zeros`: the threshold bin — the bin
@@ -258,7 +261,7 @@ constexpr int kSRunsPerBlock = OMF_SRUNS_PER_BLOCK;
 // as the PS's average of sparse Top-K updates).  Exact zeros are never candidates: when a tensor
 // has fewer than k non-zeros, its selection is completed by its lowest-index zeros (topk_plan
 // and topk_zero_fill), the order the exact path's stable sort gives ties.
-// Also clears the tensor's redo histogram, its items' candidate counts and its fine bins.
+// Also clears the tensor's redo histogram and its fine bins.
 __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, uint32_t zeros, float2 sure_zc,
                                         const int64_t* __restrict__ kk,
                                         const uint32_t* __restrict__ tfirst, const uint32_t* __restrict__ tlast,
@@ -268,7 +271,11 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, uin
                                         uint32_t* __restrict__ fcount, uint32_t* __restrict__ fhist) {
   constexpr int PER = kSBins / 1024;
   __shared__ uint32_t s_w[16];
-  for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;  // this call's redo histogram
+  // (the redo histogram is cleared after the last barrier below: a workgroup barrier waits for the
+  // workgroup's outstanding stores, so stores issued here would delay every block scan)
+#if !OMF_SAMPLE_HIST_LATE
+  for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;
+#endif
   uint32_t c[PER], loc = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -364,6 +371,9 @@ __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, uin
     fcount[t] = F;
   }
   for (uint32_t i = threadIdx.x; i < F; i += 1024) fhist[(size_t)t * kFineMax + i] = 0;
+#if OMF_SAMPLE_HIST_LATE
+  for (int b = threadIdx.x; b < kBins; b += 1024) hist[(size_t)t * kBins + b] = 0;  // this call's redo histogram
+#endif
 }
 
 template <int MODE>
@@ -386,6 +396,9 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   __shared__ uint32_t h[kSBins];
   __shared__ uint32_t s_last, s_zero;
   const uint32_t bid = blk0 + blockIdx.x;  // launches cover ranges of tensors (pipeline groups)
+#ifdef OMF_EXP_SAMPLE_TS  // experiment builds: per-phase wall-clock stamps of a few sample blocks
+  const uint64_t ts0 = wall_clock64();
+#endif
   const int t = (int)smap[2 * bid];
   const int64_t r0 = smap[2 * bid + 1];
   if (bid == 0 && threadIdx.x < 4) status[threadIdx.x] = 0u;
@@ -411,6 +424,9 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
     rv[u] = MODE == 1 ? *reinterpret_cast<const float4*>(r + e) : make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();  // h cleared
+#ifdef OMF_EXP_SAMPLE_TS
+  const uint64_t ts1 = wall_clock64();
+#endif
   uint32_t zc = 0;  // exact-zero samples: counted apart (one LDS atomic per wave, not per sample)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -431,8 +447,19 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
   __syncthreads();
   const uint32_t nblk = (uint32_t)((nr + kSRunsPerBlock - 1) / kSRunsPerBlock);
   if (nblk == 1) {  // the tensor's whole sample is in this block's histogram (the usual case)
+#ifdef OMF_EXP_SAMPLE_TS
+    const uint64_t ts2 = wall_clock64();
+#endif
     sample_threshold_tensor(t, n, h, s_zero, sure_zc, kk, tfirst, tlast, tkey, hist, item_cnt, thi, fmap, tlo, fcount,
                             fhist);
+#ifdef OMF_EXP_SAMPLE_TS
+    __syncthreads();
+    const uint64_t ts3 = wall_clock64();
+    if (threadIdx.x == 0 && (t == 0 || t == 1 || t == 2 || t == 50 || t == 100 || t == 181 || t == 182))
+      printf("SAMPLE_TS t=%d n=%lld start=%llu load+clear=%llu hist=%llu thr=%llu\n", t, (long long)n,
+             (unsigned long long)ts0, (unsigned long long)(ts1 - ts0), (unsigned long long)(ts2 - ts1),
+             (unsigned long long)(ts3 - ts2));
+#endif
     return;
   }
   uint32_t* g = gh + (size_t)t * kSBins;
