@@ -269,6 +269,28 @@ def pmc_traffic(kernel, config, bits):
     return run.get("bytes_per_launch", {}).get(kernel), f"rocprofv3 PMC, commit {tj.get('commit')}, {tj.get('date')}"
 
 
+SETTLE_S = 0.2  # untimed steps before the first leg's W warm-up steps (see settle)
+
+
+def settle(torch, step, seconds=SETTLE_S):
+    """Run untimed ``step`` calls for ``seconds`` of wall time, then synchronise.  The box's GPU idles
+    before the run, and from idle it takes ~10-20 ms of load to reach its steady clocks: measured
+    (scripts/exp/step_gap.py), the first 20 QSGD steps after 2 s idle take 0.676-0.680 ms each and
+    the next 20 0.631-0.633, while 100 ms of any GPU work first makes the first 20 take 0.639.  The
+    W warm-up steps (3.4 ms at the driver's W = 5) do not cover that ramp; this does.  Nothing of it
+    is timed or reused: the K timed steps still run every launch of every step."""
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    i = 0
+    while time.perf_counter() - t0 < seconds:
+        step(10_000_000 + i)
+        i += 1
+        if i % 16 == 0:
+            torch.cuda.synchronize()
+    torch.cuda.synchronize()
+    return i
+
+
 def event_ms(torch, st, fn, reps):
     """Mean duration of ``fn`` (its launches on stream ``st``) in a back-to-back loop, from two
     HIP events recorded on ``st`` around ``reps`` calls (the steady-state launch duration;
@@ -351,8 +373,10 @@ def main():
         plan.qsgd_decode(q, width, L, norms, y_out=y)
 
     qsgd = None
+    settled = 0
     if args.codec == "qsgd":
         progress("qsgd steps")
+        settled = settle(torch, q_step)
         for i in range(args.warmup):
             q_step(i)
         plan.check()
@@ -408,6 +432,8 @@ def main():
             t_enc(i)
             plan.topk_decode_arena(vals, idx, ratio, y=yt, mode=0)
 
+        if args.codec == "topk":
+            settled = settle(torch, t_step)
         for i in range(args.warmup):
             t_step(i)
         plan.topk_stats(reset=True)
@@ -529,7 +555,10 @@ def main():
         topk["cpu_baseline"] = cpu_t
 
     if rank == 0:
-        common = {"n_gpus": world, "warmup": args.warmup, "higher_is_better": True, "scaling": "weak",
+        common = {"n_gpus": world, "warmup": args.warmup,
+                  "settle": {"seconds": SETTLE_S, "untimed_steps": settled,
+                             "why": "GPU clock ramp from idle (bench.settle); before the W warm-up steps"},
+                  "higher_is_better": True, "scaling": "weak",
                   "vs_baseline": None, "dtype": "f32",
                   "data": "synthetic N(0,1)*1e-3 gradients of the named shapes (no checkpoints)"}
         if qsgd is not None:
