@@ -220,6 +220,36 @@ __global__ __launch_bounds__(256) void enci(const void* __restrict__ q, float* _
   }
 }
 
+// A looping tile writer: one workgroup of T threads per 64 Ki elements, one float4 per thread per
+// iteration (T x 4 elements), a workgroup barrier between iterations (the tile decoder's LDS phases).
+template <int T, bool BAR>
+__global__ __launch_bounds__(T) void wrl(const void* __restrict__ q, float* __restrict__ y, float norm, float inv, int64_t n) {
+  const int64_t base = (int64_t)blockIdx.x * 65536;
+  for (int it = 0; it < 65536 / (4 * T); ++it) {
+    const int64_t e = base + 4 * ((int64_t)it * T + threadIdx.x);
+    if (e < n) {
+      const f32x4 o = {norm, (float)it, inv, 0.f};
+      __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(y + e));
+    }
+    if (BAR) __syncthreads();
+  }
+}
+
+// The same with the workgroups' chunks interleaved: iteration it of workgroup g writes chunk
+// it * G + g (G workgroups), so the workgroups running together write neighbouring chunks.
+template <int T, bool BAR>
+__global__ __launch_bounds__(T) void wrs(const void* __restrict__ q, float* __restrict__ y, float norm, float inv, int64_t n) {
+  const int64_t G = gridDim.x;
+  for (int it = 0; it < 65536 / (4 * T); ++it) {
+    const int64_t e = ((int64_t)it * G + blockIdx.x) * (4 * T) + 4 * threadIdx.x;
+    if (e < n) {
+      const f32x4 o = {norm, (float)it, inv, 0.f};
+      __builtin_nontemporal_store(o, reinterpret_cast<f32x4*>(y + e));
+    }
+    if (BAR) __syncthreads();
+  }
+}
+
 struct Shape {
   const char* name;
   void (*fn)(const void*, float*, float, float, int64_t);
@@ -243,6 +273,10 @@ struct Shape {
 #define SHDC(W, V, T) Shape{"DECC W" #W " V" #V " T" #T, \
                            (void (*)(const void*, float*, float, float, int64_t))decc<W, V, T>, V * T * 4, T, false}
 #define SHI(I) Shape{"ENCI ind" #I, (void (*)(const void*, float*, float, float, int64_t))enci<I>, 4096, 256, false}
+#define SHL(T, B) Shape{"WRL T" #T " bar" #B, \
+                           (void (*)(const void*, float*, float, float, int64_t))wrl<T, B>, 65536, T, false}
+#define SHS(T, B) Shape{"WRS T" #T " bar" #B, \
+                           (void (*)(const void*, float*, float, float, int64_t))wrs<T, B>, 65536, T, false}
 #define SHA(W, V, T) Shape{"ACC W" #W " V" #V " T" #T, \
                            (void (*)(const void*, float*, float, float, int64_t))dec<W, V, T, true, true, false, true>, V * T * 4, T, true}
 
@@ -250,7 +284,11 @@ int main(int argc, char** argv) {
   const int64_t n = 401122304;
   const int W = argc > 1 ? atoi(argv[1]) : 1;
   std::vector<Shape> shapes;
-  if (argc > 2 && W == 200) {  // table-indirected block starts
+  if (argc > 2 && W == 300) {  // looping tile writers
+    for (int lds : {0, 40960, 81920}) {
+      for (Shape a : {SHWR(1, 256), SHL(256, true), SHS(256, true), SHS(256, false), SHS(512, true), SHS(1024, true)}) { a.lds = lds; shapes.push_back(a); }
+    }
+  } else if (argc > 2 && W == 200) {  // table-indirected block starts
     shapes = {SHI(0), SHI(1), SHE(1, 4, 256)};
   } else if (argc > 2 && W == 100) {  // wave-contiguous write-only
     for (int lds : {0, 24576, 40960}) {
@@ -297,7 +335,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d, bt.data(), bt.size() * 8, hipMemcpyHostToDevice));
     CK(hipMemcpyToSymbol(HIP_SYMBOL(g_btab), &d, sizeof(d)));
   }
-  const int qb = W == 200 ? 1 : W == 12 ? 4 : (W == 0 || W == 100) ? 1 : W > 100 ? W - 100 : W;
+  const int qb = W == 300 ? 1 : W == 200 ? 1 : W == 12 ? 4 : (W == 0 || W == 100) ? 1 : W > 100 ? W - 100 : W;
   CK(hipMalloc(&q, n * qb + 64));
   CK(hipMalloc(&y, n * 4 + 64));
   CK(hipMemset(q, 3, n * qb));
@@ -322,9 +360,9 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < shapes.size(); ++i) {
     std::sort(ms[i].begin(), ms[i].end());
     const double med = ms[i][rounds / 2];
-    const double bytes = W == 200 ? 5.0 * n : (W == 0 || W == 100) ? 4.0 * n : W > 100 ? (double)n * (W - 100 + 4) : W == 12 ? 12.0 * n : (double)n * (W + (shapes[i].acc ? 8 : 4));
+    const double bytes = W == 300 ? 4.0 * n : W == 200 ? 5.0 * n : (W == 0 || W == 100) ? 4.0 * n : W > 100 ? (double)n * (W - 100 + 4) : W == 12 ? 12.0 * n : (double)n * (W + (shapes[i].acc ? 8 : 4));
     char nm[96];
-    snprintf(nm, sizeof nm, "%s%s", shapes[i].name, shapes[i].lds ? (shapes[i].lds == 16384 ? " lds16K" : shapes[i].lds == 24576 ? " lds24K" : shapes[i].lds == 32768 ? " lds32K" : " lds40K") : "");
+    snprintf(nm, sizeof nm, "%s lds%dK", shapes[i].name, shapes[i].lds / 1024);
     printf("%-36s median %.4f ms  min %.4f  %.2f TB/s\n", nm, med, ms[i][0], bytes / med / 1e9);
   }
   return 0;
