@@ -1080,6 +1080,133 @@ __global__ __launch_bounds__(kThreads) void qsgd_spec_quant_fb(SpecArgs a, const
   else spec_block<WIDTH, false, DIV, kFmtF32>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f, (int)threadIdx.x);
 }
 
+// Wide levels (bit widths 5-8): the bracket folded into the one-wave pass the same way.  Its first
+// kWfbParts x (bracket items) one-wave workgroups sample the tensors — part g of a tensor its runs
+// g kPassesW .., every kWfbParts kPassesW-th round, kPassesW 1 KiB runs in flight per lane — and
+// the last part of each tensor to arrive combines the 16 parts' sums in part order and publishes
+// the multipliers; the pass's one-wave blocks poll them as qsgd_spec_quant_fb's do.  A bracket from
+// other partial sums than the separate launch's may list other quads: the payload is exact either
+// way (test_fused_bracket_equals_bracket_launch).
+#ifndef OMF_WFB_PARTS  // experiment builds may override them
+#define OMF_WFB_PARTS 16
+#endif
+#ifndef OMF_WFB_PASSES
+#define OMF_WFB_PASSES 8
+#endif
+constexpr int kWfbParts = OMF_WFB_PARTS;
+constexpr int kPassesW = OMF_WFB_PASSES;
+
+__device__ __forceinline__ void spec_bracket_part_wide(const SpecArgs& a, const SpecBrItem* __restrict__ items,
+                                                       int64_t wg) {
+  const int part = (int)(wg % kWfbParts);
+  const SpecBrItem bi = items[wg / kWfbParts];
+  const int32_t t = bi.tensor;
+  const int64_t tb = bi.begin, n = bi.n, R = bi.Rw;
+  const float* __restrict__ x = a.e.x + tb;
+  const bool exact = n <= kSpecExact;
+  if (exact && part != 0) return;
+  const int lane = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  if (exact) {  // 16 Ki elements at most: rounds of four float4 per lane
+    for (int64_t r0 = 0; r0 < n; r0 += 16 * 64) {
+      float4 v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int64_t e = r0 + 4 * ((int64_t)i * 64 + lane);
+        v[i] = e + 4 <= n ? *reinterpret_cast<const float4*>(x + e) : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (e < n && e + 4 > n) {  // the tensor's partial last quad
+          v[i].x = x[e];
+          if (e + 1 < n) v[i].y = x[e + 1];
+          if (e + 2 < n) v[i].z = x[e + 2];
+        }
+      }
+      float acc = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc = sq4(spec_prologue(v[i], a.e.alpha, a.divisor, a.e.fmt), acc);
+      s1 += (double)acc;
+    }
+  } else {
+    bracket_sample<kSpecRunWide, false, 64, kPassesW>(a, x, t, tb, n, R, part, kWfbParts, s1, s2);
+  }
+  double S1 = wave_sum_f64(s1), S2 = wave_sum_f64(s2);
+  if (lane != 0) return;
+  if (!exact) {  // the last part to arrive combines the partials in part order
+    double* bp = a.br_part + 2 * ((int64_t)t * kWfbParts + part);
+    st_agent(reinterpret_cast<uint64_t*>(bp), (uint64_t)__double_as_longlong(S1));
+    st_agent(reinterpret_cast<uint64_t*>(bp + 1), (uint64_t)__double_as_longlong(S2));
+    drain_vmem();
+    if (add_agent(&a.br_cnt[t], 1u) != (uint32_t)(kWfbParts - 1)) return;
+    __hip_atomic_store(&a.br_cnt[t], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    S1 = S2 = 0.0;
+    for (int g = 0; g < kWfbParts; ++g) {
+      const uint64_t* q = reinterpret_cast<const uint64_t*>(a.br_part + 2 * ((int64_t)t * kWfbParts + g));
+      S1 += __longlong_as_double((long long)ld_agent(q));
+      S2 += __longlong_as_double((long long)ld_agent(q + 1));
+    }
+  }
+  const SpecBracket o = bracket_from_sums(a, exact, n, R, kSpecRunWide, S1, S2);
+  a.br[t] = o;  // the finish launch reads it (a later launch)
+  const uint64_t ep = (uint64_t)a.epoch << 32;
+  st_agent(&a.brgran[2 * t], ep | __float_as_uint(o.c_lo));
+  st_agent(&a.brgran[2 * t + 1], ep | __float_as_uint(o.c_hi));
+}
+
+// The pass blocks' poll for their tensor's fused bracket (bounded: on expiry the tensor is flagged
+// and requantised whole by the finish — exact; the sampling workgroups have the lowest ids, so they
+// are dispatched before any pass block and never wait).
+__device__ __forceinline__ SpecBracket fb_poll(const SpecArgs& a, int32_t t) {
+  uint64_t g0 = ld_agent(&a.brgran[2 * t]), g1 = ld_agent(&a.brgran[2 * t + 1]);
+  if ((uint32_t)(g0 >> 32) != a.epoch || (uint32_t)(g1 >> 32) != a.epoch) {
+    const uint64_t t0 = wall_clock64(), min_polls = a.wait_ticks >> 10;
+    uint64_t polls = 0;
+    for (int k = 0;; k = min(k + 1, 6)) {
+      if (k < 2) __builtin_amdgcn_s_sleep(2);
+      else __builtin_amdgcn_s_sleep(8);
+      g0 = ld_agent(&a.brgran[2 * t]);
+      g1 = ld_agent(&a.brgran[2 * t + 1]);
+      if ((uint32_t)(g0 >> 32) == a.epoch && (uint32_t)(g1 >> 32) == a.epoch) break;
+      if (++polls > min_polls && wall_clock64() - t0 > a.wait_ticks) {  // never expected: requantise whole
+        __hip_atomic_fetch_or(&a.flags[t], 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        g0 = g1 = 0;
+        break;
+      }
+    }
+  }
+  return SpecBracket{__uint_as_float((uint32_t)g0), __uint_as_float((uint32_t)g1), 0.f, 0.f, 0u, {0u, 0u, 0u}};
+}
+
+template <int WIDTH, bool DIV>
+__global__ __launch_bounds__(64) void qsgd_spec_quant_wfb(SpecArgs a, const SpecBrItem* __restrict__ bitems,
+                                                          int64_t nbrw, const int64_t* __restrict__ begins) {
+  if ((int64_t)blockIdx.x < nbrw) {
+    spec_bracket_part_wide(a, bitems, blockIdx.x);
+    return;
+  }
+  const int64_t wgi = (int64_t)blockIdx.x - nbrw;
+  const int64_t blk = wgi / kWaves;
+  const int tid = (int)(wgi % kWaves) * 64 + (int)threadIdx.x;
+  const Item it = a.e.items[blk >> 2];
+  const int32_t t = it.tensor;
+  const int64_t tb = begins[t];
+  const int64_t b = it.begin + (blk & 3) * kSpecBlk;
+  const int wave = tid >> 6;
+  uint32_t* slot = a.slots + blk * spec_slot_words(kSpecPerWaveWide);
+  uint64_t* part = a.partials + blk * kWaves + wave;
+  if (b >= it.end) {
+    if (threadIdx.x == 0) {
+      *part = 0ull;
+      a.heads[blk * kWaves + wave] = (uint32_t)t << 8;
+    }
+    return;
+  }
+  auto get_br = [&]() { return fb_poll(a, t); };
+  const int64_t end = min(b + kSpecBlk, it.end);
+  if (end - b == kSpecBlk)
+    spec_block<WIDTH, true, DIV, kFmtF32, 0, kSpecPerWaveWide>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f, tid);
+  else
+    spec_block<WIDTH, false, DIV, kFmtF32, 0, kSpecPerWaveWide>(a, blk, b, end, t, tb, get_br, slot, part, 0.0f, tid);
+}
+
 // One fold segment (a workgroup of the finish launch); the last arriver of the tensor folds the
 // segments in order, checks the bracket and publishes {epoch, bad, norm} in the tensor's granule.
 __device__ void spec_fold(const SpecArgs& a, const SpecFoldItem& fi) {
@@ -2576,15 +2703,16 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
       OMF_HIP(hipMemsetAsync(p->d_spec_br_cnt, 0, 4 * (size_t)p->nt, st));  // left zero by every launch
     }
     const bool fb = p->spec_fb && !wide && !acc_in && fmt == 0 && width == 1 && !(p->spec_skip & 1u);
-    if (fb && !p->d_spec_fb_part) {  // once per plan: the fused bracket's sums, counters and granules
-      OMF_HIP(hipMalloc(&p->d_spec_fb_part, 16 * (size_t)kFbParts * (size_t)p->nt));
+    const bool wfb = p->spec_fb && wide && !acc_in && fmt == 0 && !(p->spec_skip & 1u);  // wide levels
+    if ((fb || wfb) && !p->d_spec_fb_part) {  // once per plan: the fused bracket's sums, counters and granules
+      OMF_HIP(hipMalloc(&p->d_spec_fb_part, 16 * (size_t)std::max(kFbParts, kWfbParts) * (size_t)p->nt));
       OMF_HIP(hipMalloc(&p->d_spec_fb_cnt, 4 * (size_t)p->nt));
       OMF_HIP(hipMalloc(&p->d_spec_brgran, 16 * (size_t)p->nt));
       OMF_HIP(hipMemsetAsync(p->d_spec_fb_cnt, 0, 4 * (size_t)p->nt, st));  // left zero by every launch
       OMF_HIP(hipMemsetAsync(p->d_spec_brgran, 0, 16 * (size_t)p->nt, st));  // epoch 0 is never a launch's
     }
-    sa.br_part = fb ? p->d_spec_fb_part : p->d_spec_br_part;
-    sa.br_cnt = fb ? p->d_spec_fb_cnt : p->d_spec_br_cnt;
+    sa.br_part = fb || wfb ? p->d_spec_fb_part : p->d_spec_br_part;
+    sa.br_cnt = fb || wfb ? p->d_spec_fb_cnt : p->d_spec_br_cnt;
     sa.brgran = p->d_spec_brgran;
     p->spec_last_pw = wide ? kSpecPerWaveWide : kSpecPerWave;
     sa.slots = wide ? p->d_spec_slots_w : p->d_spec_slots;
@@ -2614,6 +2742,13 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
       const dim3 gfb((unsigned)(nbrw + p->n_spec_blocks));
       if (div) hipLaunchKernelGGL((qsgd_spec_quant_fb<1, true>), gfb, blk, 0, st, sa, sa.br_items, nbrw, sa.begins);
       else hipLaunchKernelGGL((qsgd_spec_quant_fb<1, false>), gfb, blk, 0, st, sa, sa.br_items, nbrw, sa.begins);
+    } else if (wfb) {  // wide levels: the bracket's one-wave parts first, then the pass's one-wave blocks
+      const int64_t nbrw = (int64_t)kWfbParts * p->n_spec_br;
+      const dim3 gw((unsigned)(nbrw + p->n_spec_blocks * kWaves)), bw(64);
+      if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant_wfb<1, false>), gw, bw, plds_w, st, sa, sa.br_items, nbrw, sa.begins);
+      else if (width == 1) hipLaunchKernelGGL((qsgd_spec_quant_wfb<1, true>), gw, bw, plds_w, st, sa, sa.br_items, nbrw, sa.begins);
+      else if (!div) hipLaunchKernelGGL((qsgd_spec_quant_wfb<4, false>), gw, bw, plds_w, st, sa, sa.br_items, nbrw, sa.begins);
+      else hipLaunchKernelGGL((qsgd_spec_quant_wfb<4, true>), gw, bw, plds_w, st, sa, sa.br_items, nbrw, sa.begins);
     } else if (!(p->spec_skip & 1u)) {
       if (wide) hipLaunchKernelGGL(qsgd_spec_bracket_wide, gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
       else if (sa.aq) hipLaunchKernelGGL((qsgd_spec_bracket<false, true>), gbr, dim3(kBrThreads), 0, st, sa, sa.br_items);
@@ -2622,7 +2757,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     const float* an = sa.anorm;
     const int aw = acc_in ? (acc_in->width == 32 ? 4 : 1) : 0;
     constexpr int PWW = kSpecPerWaveWide;
-    if (fb) {
+    if (fb || wfb) {
       // (the pass ran above)
     } else if (wide) {  // fp32, no fused last client (spec_serves); one wave per workgroup unless OMF_SPEC_WPB=4
       static const bool wpb4 = [] { const char* v = getenv("OMF_SPEC_WPB"); return v && atoi(v) == 4; }();

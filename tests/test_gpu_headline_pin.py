@@ -138,7 +138,9 @@ def test_wide_levels_against_the_oracle(gpu, s):
 def test_fused_bracket_equals_bracket_launch(gpu, cfg):
     """The bracket folded into the pass (omf_plan_set_fused_bracket: its first workgroups sample, the
     pass's blocks poll for their tensor's bracket) writes the payload, norms and — for the fused PS
-    step — the average of the separate bracket launch, bit for bit (weighted, s = 3 and 4)."""
+    step — the average of the separate bracket launch, bit for bit (weighted, s = 3 and 4; and the
+    wide levels' one-wave version, s = 6 (int8 wire) and 8 (int32 wire), whose sixteen parts sum the
+    sample in another grouping: its bracket may list other quads, the payload is exact either way)."""
     named = shapes.model_shapes(cfg)
     sizes = [shapes.numel(sh) for _, sh in named]
     plan = codec.Plan(sizes, device=gpu)
@@ -146,7 +148,7 @@ def test_fused_bracket_equals_bracket_launch(gpu, cfg):
     g = torch.Generator(device=gpu)
     g.manual_seed(5)
     x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
-    for s in (3, 4):
+    for s in (3, 4, 6, 8):
         outs = []
         for fb in (False, True):
             plan.set_fused_bracket(fb)
