@@ -41,7 +41,7 @@ def short(name):
         return "qsgd_spec_bracket"
     for k in ("qsgd_encode_pc", "qsgd_encode_ordered", "qsgd_encode_win", "qsgd_encode_grid", "qsgd_decode_flat",
               "qsgd_decode_arena", "qsgd_quant_sub",
-              "qsgd_spec_bracket", "qsgd_spec_quant_fb", "qsgd_spec_quant", "qsgd_spec_finish",
+              "qsgd_spec_bracket", "qsgd_spec_quant_fb", "qsgd_spec_quant_wfb", "qsgd_spec_quant", "qsgd_spec_finish",
               "topk_prep_hist", "topk_collect", "topk_gather", "topk_scatter_arena") + TOPK_ENCODE + TOPK_DECODE:
         if k + "(" in name or k + "<" in name:
             return k
@@ -63,7 +63,9 @@ def main():
         res[k] = {"fetch_bytes_corrected": f, "write_bytes": w, "launches": len(vals)}
     # the bracketed encoder: one launch of each per encode — bracket + quant + finish, or (the fused
     # bracket, the default at widths <= 4) quant_fb + finish, the bracket being quant_fb's first blocks
-    for spec in (("qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_finish"), ("qsgd_spec_quant_fb", "qsgd_spec_finish")):
+    # (wide levels since round 5: quant_wfb + finish, the bracket being quant_wfb's first one-wave blocks)
+    for spec in (("qsgd_spec_bracket", "qsgd_spec_quant", "qsgd_spec_finish"), ("qsgd_spec_quant_fb", "qsgd_spec_finish"),
+                 ("qsgd_spec_quant_wfb", "qsgd_spec_finish")):
         if all(k in res for k in spec):
             res["qsgd_spec_all"] = {kk: sum(res[k][kk] for k in spec) for kk in ("fetch_bytes_corrected", "write_bytes")}
             res["qsgd_spec_all"]["launches"] = res[spec[-2]]["launches"]
