@@ -311,6 +311,12 @@ def main():
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args.gpus))
 
+    # stdout carries the one JSON line only: native libraries print banners to fd 1 (RCCL's version
+    # block at process-group init), so fd 1 becomes stderr and the line goes to a duplicate of it
+    sys.stdout.flush()
+    line_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
+
     import torch
     import torch.distributed as dist
 
@@ -581,7 +587,7 @@ def main():
                                "algorithmic_bytes_per_step_per_client": topk["algorithmic_bytes_per_step_per_client"],
                                "parallelism": f"clients{world}"},
                     "roofline": topk["roofline"], "cpu_baseline": cpu_t, **extras}
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=line_out, flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()
 
