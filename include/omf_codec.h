@@ -137,8 +137,9 @@ int32_t omf_plan_last_encoder(const omf_plan* plan);
 int omf_plan_set_wide_levels(omf_plan* plan, int32_t on);
 /* The bracketed encoder's bracket folded into its pass (on: the pass's first workgroups sample the
  * tensors and publish the brackets, the pass's blocks poll for theirs after issuing their loads — the
- * default; off: a launch of its own before the pass; OMF_SPEC_FB=0 turns it off for new plans).  Narrow fp32 encodes
- * (bit_width 1-4) only; identical payloads either way. */
+ * default; off: a launch of its own before the pass; OMF_SPEC_FB=0 turns it off for new plans).  fp32 encodes
+ * without a fused last client: bit_width 1-4, and 5-8 when wide levels are on (one-wave workgroups); identical
+ * payloads either way. */
 int omf_plan_set_fused_bracket(omf_plan* plan, int32_t on);
 /* Diagnostics of the last bracketed single-read encode (strategy 3; synchronises `stream`,
  * not for the hot path): out[0] tensors requantised whole (norm outside the sampled bracket,

@@ -212,8 +212,8 @@ class Plan:
             check(lib().omf_plan_set_wide_levels(self._h, 1 if on else 0), "omf_plan_set_wide_levels")
 
     def set_fused_bracket(self, on: bool) -> None:
-        """The bracketed encoder's bracket folded into its pass (omf_plan_set_fused_bracket);
-        identical payloads."""
+        """The bracketed encoder's bracket folded into its pass (omf_plan_set_fused_bracket: bit
+        widths 1-4, and 5-8 with wide levels); identical payloads."""
         with self._lock:
             check(lib().omf_plan_set_fused_bracket(self._h, 1 if on else 0), "omf_plan_set_fused_bracket")
 
