@@ -1,7 +1,8 @@
 """bench.py's host helpers (CPU): the CPU-baseline thread count is the process's affinity mask
 capped by its cgroup v2 quota (the GPU box lists 256 CPUs in the mask but grants 16), and the
-stratified sample picks every k-th tensor within its budget."""
+stratified sample picks every k-th tensor within its budget; the untimed settle before the warm-up."""
 import os
+import time
 
 import bench
 
@@ -44,3 +45,26 @@ def test_stratified_sample_stays_within_budget():
     assert picked == sorted(picked) and picked[0] == 0  # every k-th tensor from the first, largest dropped
     one, _ = bench.stratified_sample([("big", (10, 1000))], 10)
     assert one == [0]  # a single tensor is kept even over the budget
+
+
+def test_settle_runs_untimed_steps_for_its_wall_time():
+    """bench.settle: untimed steps for the given wall time (the GPU's clock ramp), synchronising
+    every 16 steps and at the end; the steps get offsets far from the timed loop's."""
+    calls, syncs = [], []
+
+    class _Cuda:
+        @staticmethod
+        def synchronize():
+            syncs.append(len(calls))
+
+    class _Torch:
+        cuda = _Cuda
+
+    def step(i):
+        calls.append(i)
+        time.sleep(0.001)
+
+    n = bench.settle(_Torch, step, seconds=0.05)
+    assert n == len(calls) >= 10
+    assert min(calls) >= 10_000_000
+    assert syncs[0] == 0 and syncs[-1] == n  # before the first step and after the last
