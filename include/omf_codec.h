@@ -16,8 +16,9 @@
  *    (synchronous, not on the hot path after that).  The hot-path calls never allocate or
  *    copy host memory, and never synchronise — except omf_topk_encode, which waits once
  *    per call for its plan kernel's verdict (a 16-byte word the GPU writes into mapped host
- *    memory; the launches that follow it are already queued), and omf_plan_check /
- *    omf_plan_spec_stats, which exist to synchronise.
+ *    memory; the launches that follow it are already queued), omf_topk_torch_order (host
+ *    work on the tied tensors), and omf_plan_check / omf_plan_spec_stats, which exist to
+ *    synchronise.
  *  - `stream` is a hipStream_t (NULL = the legacy default stream).  Calls are
  *    asynchronous on that stream; results are ready when the stream is.
  *  - Return value: 0 (OMF_OK) or a negative OMF_E* code; the message for the
@@ -62,7 +63,7 @@ extern "C" {
 typedef struct omf_plan omf_plan;
 
 /* ABI version (major*100 + minor). */
-#define OMF_ABI_VERSION 108
+#define OMF_ABI_VERSION 109
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -331,6 +332,31 @@ int omf_topk_stats(omf_plan* plan, int64_t* out6, int32_t reset);
 size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio);
 int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,
                     float alpha, float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream);
+/*
+ * The reference's own selection where magnitudes tie.  The reference selects with
+ * torch.topk(|t'|, k, sorted=False) on the CPU (topk.py:13; its compressor is always built on
+ * "cpu": grpc_leader_comm.py:59).  torch's CPU kernel (ATen TopKImpl.h) runs libstdc++'s
+ * partial_sort (heap select + heap sort) when k*64 <= n and nth_element otherwise, so among equal
+ * magnitudes both WHICH are selected at rank k and their ORDER in the selection are that
+ * algorithm's, not omf_topk_encode's (|t'| descending, index ascending).
+ * omf_topk_torch_order rewrites a finished omf_topk_encode (same plan, x, residual,
+ * residual_mode, ratio, alpha, values, indices and ws) into torch's bytes: a census on the device
+ * flags each tensor whose selection may differ (two selected values with one magnitude, an
+ * unselected element with the k-th magnitude, or the nth_element regime with k > 1; NaNs are one
+ * magnitude); for those, t' is fetched, torch's selection recomputed on the host (threads over
+ * tensors, omf_topk_select_host's algorithm) and values / indices — and the residual, when the
+ * selected SET changed (t' - t' on the new selection, t' back on the old) — written back.
+ * Synchronises `stream` (not stream-asynchronous: the host work is the point).
+ * *n_reordered (HOST, may be NULL) receives the number of tensors rewritten.
+ */
+int omf_topk_torch_order(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,
+                         float alpha, float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream,
+                         int64_t* n_reordered);
+/*
+ * HOST-only (no device, no plan): indices[0, k) = torch.topk(|t|, k, sorted=False).indices of the
+ * HOST array t[0, n) as the reference's CPU torch computes it (1 <= k <= n < 2^32), order included.
+ */
+int omf_topk_select_host(const float* t, int64_t n, int64_t k, int64_t* indices);
 
 /*
  * Top-K decode of ONE tensor of n elements: topk_desparse (topk.py:18-21),

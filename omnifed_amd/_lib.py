@@ -69,6 +69,9 @@ SIGNATURES = {
     "omf_topk_stats": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64), _c_i32]),
     "omf_topk_workspace_bytes": (_c_size, [_c_p, _c_f64]),
     "omf_topk_encode": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_f64, _c_f32, _c_p, _c_p, _c_p, _c_size, _c_p]),
+    "omf_topk_torch_order": (ctypes.c_int, [_c_p, _c_p, _c_p, _c_i32, _c_f64, _c_f32, _c_p, _c_p, _c_p, _c_size,
+                                            _c_p, ctypes.POINTER(_c_i64)]),
+    "omf_topk_select_host": (ctypes.c_int, [_c_p, _c_i64, _c_i64, _c_p]),
     "omf_topk_decode": (ctypes.c_int, [_c_p, _c_p, _c_i64, _c_p, _c_i64, _c_i32, _c_p]),
     "omf_topk_decode_arena": (ctypes.c_int, [_c_p, _c_f64, _c_p, _c_p, _c_p, _c_i32, _c_p]),
     "omf_topk_decode_workspace_bytes": (_c_size, [_c_p, _c_f64]),
@@ -87,7 +90,7 @@ class CodecError(RuntimeError):
     pass
 
 
-ABI_VERSION = 108  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+ABI_VERSION = 109  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
 
 
 def lib() -> ctypes.CDLL:

@@ -18,7 +18,8 @@ CSRC = os.path.join(HERE, "csrc")
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 LIB = os.path.join(HERE, "libomf_codec.so")
 
-SOURCES = ["omf_runtime.cpp", "omf_qsgd.hip", "omf_qsgd_ring.hip", "omf_qsgd_pack.hip", "omf_topk.hip"]
+SOURCES = ["omf_runtime.cpp", "omf_qsgd.hip", "omf_qsgd_ring.hip", "omf_qsgd_pack.hip", "omf_topk.hip",
+           "omf_topk_host.cpp"]
 
 # Exact IEEE fp32 (no contraction, denormals kept, correctly rounded / and sqrt): the
 # payload must match the reference bit for bit.
@@ -70,10 +71,25 @@ def needs_build() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def _toolchain_stamp() -> str:
+    """The compiler and flags the objects in _obj were built with."""
+    return "\n".join([os.path.realpath(hipcc()), *FLAGS]) + "\n"
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    objdir = os.path.join(HERE, "_obj")
+    # beside the library (it travels with it to the GPU box; _obj does not)
+    stamp_path = LIB + ".stamp"
+    stamp = _toolchain_stamp()
+    try:
+        with open(stamp_path) as fh:
+            stale = fh.read() != stamp
+    except OSError:
+        stale = True
+    if stale:
+        force = True  # another compiler or flag set (or no record of one): nothing is reused
     if not force and not needs_build():
         return LIB
-    objdir = os.path.join(HERE, "_obj")
     os.makedirs(objdir, exist_ok=True)
     objs = []
     procs = []
@@ -98,6 +114,8 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError("link failed:\n" + r.stdout.decode(errors="replace"))
     os.replace(tmp, LIB)
+    with open(stamp_path, "w") as fh:
+        fh.write(stamp)
     # the offload linker leaves per-target unbundling temporaries beside the output
     for f in os.listdir(HERE):
         if f.startswith("libomf_codec.so.") and ("-amdhsa-" in f or "-linux-gnu" in f):

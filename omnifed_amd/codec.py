@@ -120,6 +120,7 @@ class Plan:
         self._dec_need: Dict[float, int] = {}
         self._counts_cache: Dict[tuple, tuple] = {}
         self._topk_cache: Dict[float, tuple] = {}
+        self.topk_reordered = 0  # tensors the latest tie_order="torch" encode rewrote (diagnostics)
         # the library's choice (by arena size, or OMF_ENCODE_STRATEGY)
         self.strategy = STRATEGIES[int(L.omf_plan_encode_strategy(h))]
 
@@ -497,10 +498,17 @@ class Plan:
 
     def topk_encode(self, x: torch.Tensor, ratio: float, residual: Optional[torch.Tensor] = None,
                     residual_mode: int = 0, values: Optional[torch.Tensor] = None,
-                    indices: Optional[torch.Tensor] = None, stream: Optional[int] = None, alpha: float = 1.0):
+                    indices: Optional[torch.Tensor] = None, stream: Optional[int] = None, alpha: float = 1.0,
+                    tie_order: str = "index"):
         """Returns ``(values, indices, ks)``; tensor t's selection at ``[sum(ks[:t]), +ks[t])``.
 
-        ``alpha``: the client weighting (t' = residual + fl32(alpha * x)), fused in."""
+        ``alpha``: the client weighting (t' = residual + fl32(alpha * x)), fused in.
+        ``tie_order``: "index" — the device selection alone, (|t'| descending, index ascending),
+        asynchronous on the stream; "torch" — then ``omf_topk_torch_order``: where magnitudes tie,
+        which of them are selected and their order are torch's CPU ``topk`` (the reference's bytes;
+        synchronises the stream).  Without ties the two are the same bytes."""
+        if tie_order not in ("index", "torch"):
+            raise ValueError(f"tie_order must be 'index' or 'torch', not {tie_order!r}")
         dev = self.device
         ks, K, need = self._topk_geom(ratio)
         ks = list(ks)
@@ -528,6 +536,14 @@ class Plan:
                                     float(ratio), float(alpha), _ptr(values), _ptr(indices), _ptr(ws),
                                     ctypes.c_size_t(ws.numel()), ctypes.c_void_p(st)),
                   "omf_topk_encode")
+            if tie_order == "torch":
+                nre = ctypes.c_int64(0)
+                check(L.omf_topk_torch_order(self._h, _ptr(x), _ptr(residual) if residual_mode else None,
+                                             int(residual_mode), float(ratio), float(alpha), _ptr(values),
+                                             _ptr(indices), _ptr(ws), ctypes.c_size_t(ws.numel()),
+                                             ctypes.c_void_p(st), ctypes.byref(nre)),
+                      "omf_topk_torch_order")
+                self.topk_reordered = int(nre.value)
         return values, indices, ks
 
 

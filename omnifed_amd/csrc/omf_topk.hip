@@ -38,7 +38,10 @@
 #include <rocprim/rocprim.hpp>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -1849,6 +1852,102 @@ __global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict_
   }
 }
 
+// ---- tie census of a finished selection (omf_topk_torch_order)
+// torch's comparison sees magnitudes only, every NaN equal to every other: one key per class.
+__device__ __forceinline__ uint32_t tie_key(float v) {
+  const uint32_t u = __float_as_uint(v) & 0x7fffffffu;
+  return u > 0x7f800000u ? 0x7fc00000u : u;
+}
+constexpr uint32_t kNanKey = 0x7fc00000u;
+
+// Per tensor: how many source elements carry the tie key of its k-th selected value (the
+// selection's last, smallest entry).  MODE 0: the source is x and t' = fl32(alpha * x); MODE 1:
+// the source is the residual the encode left (t' where unselected).  One block per 16 Ki item.
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void topk_tie_count(const float* __restrict__ src, float alpha,
+                                                           const Item* __restrict__ items,
+                                                           const int64_t* __restrict__ kk,
+                                                           const int64_t* __restrict__ koff,
+                                                           const float* __restrict__ values,
+                                                           uint32_t* __restrict__ cnt) {
+  __shared__ uint32_t s_w[kWaves];
+  const Item it = items[blockIdx.x];
+  const uint32_t T = tie_key(values[koff[it.tensor] + kk[it.tensor] - 1]);
+  uint32_t c = 0;
+  for (int64_t e = it.begin + threadIdx.x; e < it.end; e += kThreads) {
+    const float v = MODE == 0 ? __fmul_rn(src[e], alpha) : src[e];
+    c += tie_key(v) == T ? 1u : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+  if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += s_w[w];
+    if (s) atomicAdd(&cnt[it.tensor], s);
+  }
+}
+
+// Per tensor (one block): does torch's CPU selection of the tensor possibly differ from this
+// encoder's (|t'| descending, index ascending) one?  It can only where magnitudes tie —
+//   dup:      two selected values with one key (their relative order is the heap's), or
+//   boundary: an unselected element with the k-th key (which of them are selected is the heap's),
+// and always in the introselect regime (k * 64 > n, torch leaves the partition order) unless
+// k == 1.  The residual holds t' - t' on the selected slots: +0 for a finite t', NaN otherwise,
+// which the count of the k-th key has to discount when that key is 0 or NaN (EF modes).
+__global__ __launch_bounds__(kThreads) void topk_tie_flags(const int64_t* __restrict__ kk,
+                                                           const int64_t* __restrict__ koff,
+                                                           const int64_t* __restrict__ tsize,
+                                                           const float* __restrict__ values,
+                                                           const uint32_t* __restrict__ cnt, int32_t ef,
+                                                           uint32_t* __restrict__ flags) {
+  __shared__ uint32_t s_w[3][kWaves];
+  const int t = blockIdx.x;
+  const int64_t k = kk[t], n = tsize[t];
+  const float* v = values + koff[t];
+  const uint32_t T = tie_key(v[k - 1]);
+  uint32_t dup = 0, sel_t = 0, fin = 0;
+  for (int64_t j = threadIdx.x; j < k; j += kThreads) {
+    const float a = v[j];
+    const uint32_t key = tie_key(a);
+    if (j + 1 < k && tie_key(v[j + 1]) == key) dup = 1;
+    sel_t += key == T ? 1u : 0u;
+    fin += (__float_as_uint(a) & 0x7fffffffu) < 0x7f800000u ? 1u : 0u;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    dup |= __shfl_xor(dup, o, 64);
+    sel_t += __shfl_xor(sel_t, o, 64);
+    fin += __shfl_xor(fin, o, 64);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    s_w[0][threadIdx.x >> 6] = dup;
+    s_w[1][threadIdx.x >> 6] = sel_t;
+    s_w[2][threadIdx.x >> 6] = fin;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    dup = 0, sel_t = 0, fin = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      dup |= s_w[0][w];
+      sel_t += s_w[1][w];
+      fin += s_w[2][w];
+    }
+    int64_t unsel = (int64_t)cnt[t];
+    if (ef) {
+      if (T == 0u) unsel -= fin;
+      if (T == kNanKey) unsel -= k - (int64_t)fin;
+    } else {
+      unsel -= sel_t;
+    }
+    const bool boundary = unsel > 0;
+    flags[t] = (k * 64 > n) ? (k > 1 || boundary) : (dup || boundary);
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void topk_scatter(const float* __restrict__ values,
                                                          const int64_t* __restrict__ indices, int64_t k,
                                                          float* __restrict__ y, int64_t n, int add) {
@@ -2822,6 +2921,173 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     hipLaunchKernelGGL((topk_gather<false>), dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted_keys, d_begins,
                        d_sizes, cstart, kk, koff, values, indices);
   OMF_HIP(hipGetLastError());
+  return OMF_OK;
+}
+
+}  // extern "C"
+
+namespace omf {
+int torch_topk_select(const float* t, int64_t n, int64_t k, int64_t* out);  // omf_topk_host.cpp
+}
+
+namespace {
+
+// One tensor of omf_topk_torch_order: its t' fetched (the residual with the selected values put
+// back, or fl32(alpha * x)), torch's CPU selection recomputed on the host, and the tensor's values /
+// indices (and, when the selected set changed, its residual) written back.  Returns OMF_OK or an
+// error with *msg set (the worker's thread-local error string is not the caller's).
+int reorder_tensor(hipStream_t s, const float* src, float* residual, bool ef, float alpha, int64_t off, int64_t n,
+                   int64_t k, float* values, int64_t* indices, bool* changed, std::string* msg) {
+  std::vector<float> tp, v, nv;
+  std::vector<int64_t> ix, sel;
+  try {
+    tp.resize((size_t)n);
+    v.resize((size_t)k);
+    nv.resize((size_t)k);
+    ix.resize((size_t)k);
+    sel.resize((size_t)k);
+  } catch (const std::bad_alloc&) {
+    *msg = "omf_topk_torch_order: host buffers";
+    return OMF_ENOMEM;
+  }
+  auto hip = [&](hipError_t e, const char* what) {
+    if (e != hipSuccess) *msg = std::string(what) + ": " + hipGetErrorString(e);
+    return e == hipSuccess;
+  };
+  if (!hip(hipMemcpyAsync(tp.data(), src + off, 4 * (size_t)n, hipMemcpyDeviceToHost, s), "t' to host") ||
+      !hip(hipMemcpyAsync(v.data(), values, 4 * (size_t)k, hipMemcpyDeviceToHost, s), "values to host") ||
+      !hip(hipMemcpyAsync(ix.data(), indices, 8 * (size_t)k, hipMemcpyDeviceToHost, s), "indices to host") ||
+      !hip(hipStreamSynchronize(s), "copy to host"))
+    return OMF_EHIP;
+  if (ef) {
+    for (int64_t j = 0; j < k; ++j)
+      if (ix[j] >= 0 && ix[j] < n) tp[ix[j]] = v[j];
+  } else if (alpha != 1.0f) {
+    for (int64_t i = 0; i < n; ++i) tp[i] = tp[i] * alpha;  // one IEEE multiply, as the encoder's
+  }
+  if (int rc = omf::torch_topk_select(tp.data(), n, k, sel.data())) {
+    *msg = omf_last_error();
+    return rc;
+  }
+  if (sel == ix) return OMF_OK;
+  *changed = true;
+  for (int64_t j = 0; j < k; ++j) nv[j] = tp[sel[j]];
+  bool same_set = true;
+  if (ef) {
+    std::vector<int64_t> a(ix), b(sel);
+    std::sort(a.begin(), a.end());
+    std::sort(b.begin(), b.end());
+    same_set = a == b;
+  }
+  if (!same_set) {  // the residual: t' with torch's selection zeroed (t' - t')
+    for (int64_t j = 0; j < k; ++j) tp[sel[j]] = tp[sel[j]] - tp[sel[j]];
+    if (!hip(hipMemcpyAsync(residual + off, tp.data(), 4 * (size_t)n, hipMemcpyHostToDevice, s), "residual to device"))
+      return OMF_EHIP;
+  }
+  if (!hip(hipMemcpyAsync(values, nv.data(), 4 * (size_t)k, hipMemcpyHostToDevice, s), "values to device") ||
+      !hip(hipMemcpyAsync(indices, sel.data(), 8 * (size_t)k, hipMemcpyHostToDevice, s), "indices to device") ||
+      !hip(hipStreamSynchronize(s), "copy to device"))
+    return OMF_EHIP;
+  return OMF_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int omf_topk_torch_order(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,
+                         float alpha, float* values, int64_t* indices, void* ws, size_t ws_bytes, void* stream,
+                         int64_t* n_reordered) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (!values || !indices || !ws) return fail(OMF_EINVAL, "values, indices and ws must be non-NULL");
+  if (residual_mode < 0 || residual_mode > 2 || (residual_mode != 0 && !residual) || (residual_mode == 0 && !x))
+    return fail(OMF_EINVAL, "residual_mode 0 needs x, modes 1 / 2 the residual the encode updated");
+  if (!(ratio == ratio)) return fail(OMF_EINVAL, "ratio is NaN");
+  const std::vector<int64_t>& sizes = omf_plan_access::sizes(plan);
+  const std::vector<int64_t>& offsets = omf_plan_access::offsets(plan);
+  const int32_t nt = (int32_t)sizes.size();
+  std::vector<int64_t> K(nt + 1, 0);
+  for (int32_t t = 0; t < nt; ++t) {
+    const int64_t k = omf_topk_k(sizes[t], ratio);
+    if (k > sizes[t]) return fail(OMF_EINVAL, "selected index k out of range (k > numel): compress_ratio too large");
+    K[t + 1] = K[t] + k;
+  }
+  const WsLayout L = layout(plan);
+  if (ws_bytes < L.total) return fail(OMF_EINVAL, "workspace too small (see omf_topk_workspace_bytes)");
+  if (n_reordered) *n_reordered = 0;
+  if (nt == 0) return OMF_OK;
+  const int dev = omf_plan_access::device(plan);
+  DeviceGuard g(dev);
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  hipStream_t st = (hipStream_t)stream;
+  uint8_t* w = static_cast<uint8_t*>(ws);
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);  // the encode's scratch, free once it is done
+  uint32_t* flags = reinterpret_cast<uint32_t*>(w + L.flag);
+  SetupTable tb;
+  HostSync* hsync = host_sync(dev);
+  if (!hsync) return fail(OMF_EHIP, "omf_topk_torch_order: pinned status buffer");
+  if (int r = setup_table(plan, ratio, sample_max_runs(knobs(plan)), st, reinterpret_cast<uint32_t*>(w + L.status), &tb))
+    return r;
+  int64_t n_items = 0;
+  const Item* items = static_cast<const Item*>(omf_plan_access::flat_items(plan, &n_items));
+  const bool ef = residual_mode != 0;
+  OMF_HIP(hipMemsetAsync(cnt, 0, 4 * (size_t)nt, st));
+  if (n_items > 0) {
+    if (ef)
+      hipLaunchKernelGGL((topk_tie_count<1>), dim3((unsigned)n_items), dim3(kThreads), 0, st, residual, 1.0f, items,
+                         tb.kk, tb.koff, values, cnt);
+    else
+      hipLaunchKernelGGL((topk_tie_count<0>), dim3((unsigned)n_items), dim3(kThreads), 0, st, x, alpha, items, tb.kk,
+                         tb.koff, values, cnt);
+  }
+  hipLaunchKernelGGL(topk_tie_flags, dim3((unsigned)nt), dim3(kThreads), 0, st, tb.kk, tb.koff,
+                     omf_plan_access::d_sizes(plan), values, cnt, ef ? 1 : 0, flags);
+  OMF_HIP(hipGetLastError());
+  std::vector<uint32_t> hflags(nt);
+  OMF_HIP(hipMemcpyAsync(hflags.data(), flags, 4 * (size_t)nt, hipMemcpyDeviceToHost, st));
+  OMF_HIP(hipStreamSynchronize(st));
+  std::vector<int32_t> todo;
+  for (int32_t t = 0; t < nt; ++t)
+    if (hflags[t]) todo.push_back(t);
+  if (todo.empty()) return OMF_OK;
+  std::sort(todo.begin(), todo.end(), [&](int32_t a, int32_t b) { return sizes[a] > sizes[b]; });  // largest first
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int nw = (int)std::min<size_t>(todo.size(), std::min(16u, hw));
+  std::atomic<size_t> next{0};
+  std::atomic<int64_t> changed_count{0};
+  std::mutex err_mu;
+  int err = OMF_OK;
+  std::string err_msg;
+  const float* src = ef ? residual : x;
+  auto work = [&]() {
+    DeviceGuard wg(dev);
+    hipStream_t s = nullptr;
+    if (!wg.ok || hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+      std::lock_guard<std::mutex> lk(err_mu);
+      if (!err) err = OMF_EHIP, err_msg = "omf_topk_torch_order: worker stream";
+      return;
+    }
+    for (size_t i = next++; i < todo.size(); i = next++) {
+      const int32_t t = todo[i];
+      bool changed = false;
+      std::string msg;
+      const int rc = reorder_tensor(s, src, residual, ef, alpha, offsets[t], sizes[t], K[t + 1] - K[t], values + K[t],
+                                    indices + K[t], &changed, &msg);
+      if (rc) {
+        std::lock_guard<std::mutex> lk(err_mu);
+        if (!err) err = rc, err_msg = "omf_topk_torch_order: tensor " + std::to_string(t) + ": " + msg;
+        break;
+      }
+      if (changed) ++changed_count;
+    }
+    (void)hipStreamDestroy(s);
+  };
+  std::vector<std::thread> pool;
+  for (int i = 1; i < nw; ++i) pool.emplace_back(work);
+  work();
+  for (std::thread& th : pool) th.join();
+  if (err) return fail(err, err_msg);
+  if (n_reordered) *n_reordered = changed_count.load();
   return OMF_OK;
 }
 

@@ -7,8 +7,12 @@ residual lives on the GPU in ``self.residual.residuals[name]`` (flat fp32).  ``e
 (the batched wire path, ``encode_updates_dict``) encodes a whole update dict in one call; its
 residuals live in one compressor-owned arena per dict layout and ``residuals[name]`` are views
 of it, so the per-tensor and the batched paths share the same error-feedback state.
-Selection order: descending |t'|, ties by ascending index — torch.topk's order
-for k·64 <= n on the reference CPU path (its ties are unspecified).
+Selection (``tie_order``, default "torch"): the reference's bytes — where magnitudes tie, which of
+them are selected at rank k and their order are those of torch's CPU ``topk`` (libstdc++
+partial_sort / nth_element; ``omf_topk_torch_order``, host work on the tied tensors only).
+"index": the device selection alone, (|t'| descending, index ascending), asynchronous; identical
+bytes whenever k*64 <= n and no two of the k+1 largest |t'| of a tensor tie (decoded tensors also
+agree when ties stay inside the selection, and in the nth_element regime k*64 > n without ties).
 """
 
 from __future__ import annotations
@@ -21,13 +25,13 @@ from .core import Compression, ResidualUpdates, compute_device, gather_arena, to
 TOPK_COMPRESSION_NAME = "TopKCompression"
 
 
-def topk_sparse(tensor: torch.Tensor, compress_ratio: float):
+def topk_sparse(tensor: torch.Tensor, compress_ratio: float, tie_order: str = "torch"):
     """topk.py:10-15 without error feedback: ``(values, indices)`` of the flat tensor."""
     dev = compute_device(tensor, torch.device("cpu"))
     n = tensor.numel()
     plan = codec.Plan.get([n], device=dev)
     x = to_arena(tensor, dev, plan)
-    values, indices, _ = plan.topk_encode(x, compress_ratio)
+    values, indices, _ = plan.topk_encode(x, compress_ratio, tie_order=tie_order)
     vdt = tensor.dtype if tensor.dtype in (torch.float16, torch.bfloat16) else values.dtype
     return values.to(tensor.device, vdt), indices.to(tensor.device)
 
@@ -53,11 +57,14 @@ def topk_index_offset(K: int) -> int:
 class TopKCompression(Compression):
     """Top-k sparsification with error feedback (largest-magnitude elements)."""
 
-    def __init__(self, device="cpu", compress_ratio: float = 0.01):
+    def __init__(self, device="cpu", compress_ratio: float = 0.01, tie_order: str = "torch"):
         super().__init__()
         self.residual = ResidualUpdates()
         self.device = torch.device(device)
         self.compress_ratio = float(compress_ratio)
+        if tie_order not in ("torch", "index"):
+            raise ValueError(f"tie_order must be 'torch' or 'index', not {tie_order!r}")
+        self.tie_order = tie_order  # module docstring
         self._arenas = {}  # residual arenas of the batched path, per dict layout
 
     def compress(self, tensor: torch.Tensor, name: str):
@@ -97,7 +104,7 @@ class TopKCompression(Compression):
         if res is None:
             res = torch.empty(numel, dtype=torch.float32, device=dev)
         values, indices, _ = plan.topk_encode(x, self.compress_ratio, residual=res, residual_mode=mode,
-                                              alpha=float(alpha))
+                                              alpha=float(alpha), tie_order=self.tie_order)
         self.residual.residuals[name] = res
         ctx = (numel, shape)
         return (values.to(self.device), indices.to(self.device)), ctx
@@ -123,7 +130,8 @@ class TopKCompression(Compression):
         plan = codec.Plan.get([numel], device=dev)
         x = to_arena(t, dev, plan)  # exact widening (or t itself when the compensate promoted to fp32)
         r = torch.empty(numel, dtype=torch.float32, device=dev)
-        values, indices, _ = plan.topk_encode(x, self.compress_ratio, residual=r, residual_mode=2)
+        values, indices, _ = plan.topk_encode(x, self.compress_ratio, residual=r, residual_mode=2,
+                                              tie_order=self.tie_order)
         self.residual.residuals[name] = r.to(t.dtype)
         return (values.to(self.device, t.dtype), indices.to(self.device)), (numel, shape)
 
@@ -209,7 +217,8 @@ class TopKCompression(Compression):
         io = topk_index_offset(K)
         values = out[:4 * K].view(torch.float32)
         indices = out[io:io + 8 * K].view(torch.int64)
-        plan.topk_encode(x, self.compress_ratio, residual=r, residual_mode=2, values=values, indices=indices)
+        plan.topk_encode(x, self.compress_ratio, residual=r, residual_mode=2, values=values, indices=indices,
+                         tie_order=self.tie_order)
         res[:plan.arena_end].copy_(r)  # exact narrowing (t' and zeros are dt values)
         for t, name in enumerate(names):
             o, n = plan.offsets[t], plan.sizes[t]
@@ -238,7 +247,7 @@ class TopKCompression(Compression):
         values = out[:4 * K].view(torch.float32)
         indices = out[io:io + 8 * K].view(torch.int64)
         plan.topk_encode(x, self.compress_ratio, residual=res, residual_mode=mode, values=values, indices=indices,
-                         alpha=float(alpha))
+                         alpha=float(alpha), tie_order=self.tie_order)
         base = res.data_ptr()
         for t, name in enumerate(names):
             o, n = plan.offsets[t], plan.sizes[t]

@@ -83,9 +83,10 @@ class GpuOps:
     def div_(self, y, d):
         return codec.div_(y, d)
 
-    def topk_encode(self, x, ratio, residual, residual_mode, alpha, values=None, indices=None):
+    def topk_encode(self, x, ratio, residual, residual_mode, alpha, values=None, indices=None, tie_order="torch"):
+        """The client's Top-K encode (the reference's selection where magnitudes tie: tie_order)."""
         values, indices, _ = self.plan.topk_encode(x, ratio, residual=residual, residual_mode=residual_mode,
-                                                   values=values, indices=indices, alpha=alpha)
+                                                   values=values, indices=indices, alpha=alpha, tie_order=tie_order)
         return values, indices
 
     def topk_decode(self, values, indices, ratio, y, mode):
@@ -107,12 +108,21 @@ class DeviceAggregator:
         self.avg: Optional[torch.Tensor] = None  # the fused step's output arena (disjoint from acc)
         self.update_count = 0
         self.total_samples = 0
+        # set by accumulate_apply_encode(keep_sum=False): acc lacks the last client's term, so
+        # every call that reads or extends the sum raises until reset()
+        self._stale = False
 
     def reset(self):
         """_initialize_accumulated_updates (global_grpc_server.py:58-62)."""
         self.acc.zero_()
         self.update_count = 0
         self.total_samples = 0
+        self._stale = False
+
+    def _check_fresh(self):
+        if self._stale:
+            raise RuntimeError("the accumulator lacks the last client's term (accumulate_apply_encode with "
+                               "keep_sum=False): reset() it before the next round")
 
     def _slice(self, name):
         i = self.index[name]
@@ -138,6 +148,7 @@ class DeviceAggregator:
         from .hybrid.communicator.global_grpc_compression import (_decode_topk_layer, _validate_layer,
                                                                   check_topk_indices, stage_topk)
 
+        self._check_fresh()
         last: Dict[str, object] = {}
         topk_payload: Dict[str, tuple] = {}
         for L in layers:
@@ -222,6 +233,7 @@ class DeviceAggregator:
         for the same draws (same kernels, same payload and norms)."""
         from .hybrid.compression.qsgd import QSGDQuantCompression, encode_groups, should_compress_tensor
 
+        self._check_fresh()
         names = [n for n in self.names if n in updates]
         if (not isinstance(compressor, QSGDQuantCompression) or compressor.packed_wire
                 or not all(should_compress_tensor(updates[n]) and updates[n].dtype == torch.float32 for n in names)
@@ -270,6 +282,7 @@ class DeviceAggregator:
         from .hybrid.compression.qsgd import QSGDQuantCompression
         from .hybrid.communicator.global_grpc_compression import _encode_dense_layer, qsgd_layers_from_arena
 
+        self._check_fresh()
         total = self.total_samples if total_samples is None else int(total_samples)
         if self.avg is None:
             self.avg = torch.empty_like(self.acc)
@@ -295,21 +308,26 @@ class DeviceAggregator:
             layers.append(L if L is not None and int(np.prod(self.shapes[n])) > 0 else _encode_dense_layer(n, avg[n]))
         return avg, layers
 
-    def accumulate_apply_encode(self, layers, number_samples: int, compressor, keep_sum: bool = False):
+    def accumulate_apply_encode(self, layers, number_samples: int, compressor, keep_sum: bool = True):
         """The last arriving client's ``SendUpdate`` and the round's first ``GetUpdatedModel`` in one
         pass (global_grpc_server.py:108-125, 147-171, 213-234): ``acc + decode(update)``, the
         average over ``total_samples`` (this client's included) and its QSGD downlink — for a QSGD
         update and a Philox QSGD compressor on a bracketed plan, ONE encoder pass that reads the
         accumulator and the update's payload once (omf_ps_accumulate_apply_encode; 10 B per element
-        at s = 4 instead of 18 for accumulate_layers + apply_and_encode).  The accumulator then lacks
-        this client's term unless ``keep_sum`` (the reference re-initialises it at the next round's
-        first update, :86-92, and reads it only in _apply_model_updates).  Same return as
+        at s = 4 instead of 18 for accumulate_layers + apply_and_encode).  ``keep_sum`` (default)
+        stores the sum in the accumulator, as the two calls leave it (4 more bytes per element);
+        ``keep_sum=False`` skips that store — the reference reads the sum only in
+        _apply_model_updates and re-initialises it at the next round's first update (:86-92) — and
+        marks the accumulator stale: every later call that reads or extends it raises until
+        ``reset()``.  The counters advance once the sum (stored or not) has been formed; a payload
+        that fails its checks leaves accumulator and counters as they were.  Same return as
         ``apply_and_encode``; bytes equal to ``accumulate_layers`` followed by it.  Any other
         message or compressor takes those two calls."""
         from .hybrid.compression.qsgd import QSGDQuantCompression
         from .hybrid.communicator.global_grpc_compression import (_encode_dense_layer, _validate_layer,
                                                                   qsgd_layers_from_arena)
 
+        self._check_fresh()
         layers = list(layers)
         last: Dict[str, object] = {}
         for L in layers:
@@ -351,6 +369,8 @@ class DeviceAggregator:
             seed=compressor.philox_key(), offset=compressor._next_call())
         self.update_count += 1
         self.total_samples = total
+        if not keep_sum:
+            self._stale = True
         avg = {n: self._avg_slice(n).view(self.shapes[n]) for n in self.names}
         got = qsgd_layers_from_arena(self.plan, q, norms_out, self.names, [self.shapes[n] for n in self.names], 2**s,
                                      compressor.packed_wire)
@@ -361,6 +381,7 @@ class DeviceAggregator:
 
     def apply(self, total_samples: Optional[int] = None) -> Dict[str, torch.Tensor]:
         """_apply_model_updates (global_grpc_server.py:155-171): acc / total_samples per tensor."""
+        self._check_fresh()
         total = self.total_samples if total_samples is None else int(total_samples)
         if self.compute_mean:
             codec.div_(self.acc, float(total))

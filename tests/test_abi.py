@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 import subprocess
+import threading
 
 import pytest
 
@@ -26,7 +27,11 @@ def test_build_and_load():
     assert L.omf_abi_version() == _lib.ABI_VERSION
     # the header's define, the library and the Python binding agree
     assert re.search(r"#define OMF_ABI_VERSION (\d+)", open(HEADER).read()).group(1) == str(_lib.ABI_VERSION)
-    assert L.omf_last_error() == b""
+    seen = []  # a thread that made no call has no error (the string is per thread)
+    th = threading.Thread(target=lambda: seen.append(L.omf_last_error()))
+    th.start()
+    th.join()
+    assert seen == [b""]
 
 
 def test_every_declared_symbol_exported_and_bound():

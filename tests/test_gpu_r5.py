@@ -150,3 +150,32 @@ def test_aggregator_last_client_fused_equals_two_calls(gpu):
     assert [L.SerializeToString() for L in la] == [L.SerializeToString() for L in lb]
     for n, _ in named:
         assert torch.equal(avg_a[n], avg_b[n]), n
+
+
+def test_aggregator_fused_without_sum_marks_the_accumulator_stale(gpu):
+    """accumulate_apply_encode(keep_sum=False) leaves the accumulator without the last client's
+    term: apply(), apply_and_encode() and a further accumulate raise until reset(); with the
+    default keep_sum the accumulator holds the full sum, as accumulate_layers leaves it."""
+    from omnifed_amd.hybrid.communicator.global_grpc_compression import build_global_compressor, encode_updates_dict
+
+    named = [("a", (300, 1000)), ("e", (8192, 4096))]
+    g = torch.Generator(device=gpu).manual_seed(9)
+    comp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=gpu)
+    msgs = [encode_updates_dict({n: torch.randn(s, device=gpu, generator=g) for n, s in named}, comp)
+            for _ in range(2)]
+    srv = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=gpu)
+    A, B = DeviceAggregator(named, device=gpu), DeviceAggregator(named, device=gpu)
+    for agg in (A, B):
+        agg.accumulate_layers(msgs[0], number_samples=5)
+    A.accumulate_apply_encode(msgs[1], 5, srv)  # keep_sum (default)
+    B.accumulate_layers(msgs[1], number_samples=5)
+    assert torch.equal(A.acc, B.acc) and A.total_samples == B.total_samples == 10
+    C = DeviceAggregator(named, device=gpu)
+    C.accumulate_layers(msgs[0], number_samples=5)
+    C.accumulate_apply_encode(msgs[1], 5, srv, keep_sum=False)
+    for call in (C.apply, lambda: C.apply_and_encode(srv), lambda: C.accumulate_layers(msgs[0], 5)):
+        with pytest.raises(RuntimeError, match="reset"):
+            call()
+    C.reset()
+    C.accumulate_layers(msgs[0], number_samples=5)
+    assert C.total_samples == 5

@@ -2,10 +2,8 @@
 in the tensor's dtype (hybrid/compression/topk.py:33-42, core.py:26-37) and sends fp32 values
 (global_grpc_compression.py:84-98: astype(float32); a bf16 tensor fails there in .numpy()); its
 overlay decode returns the base's dtype (:151-156).  Checked against the reference's own torch op
-sequence replayed on the CPU.  torch.topk's order among equal magnitudes is unspecified, and half
-precision makes ties common, so the selection is compared with the kernel's documented rule
-(descending |t'|, ties by ascending index) — a valid torch.topk result — and its magnitudes with
-torch.topk's (tie-independent)."""
+sequence replayed on the CPU.  Half precision makes equal magnitudes common; the selection —
+members at rank k and order — is torch's CPU topk's on the half tensor (tie_order="torch")."""
 
 import numpy as np
 import pytest
@@ -28,8 +26,7 @@ def _bits(t: torch.Tensor) -> np.ndarray:
 
 
 def _rule_topk(t: torch.Tensor, k: int) -> np.ndarray:
-    a = t.float().abs().numpy()
-    return np.lexsort((np.arange(a.size), -a))[:k]  # descending |t|, ties by ascending index
+    return torch.topk(t.abs(), k, sorted=False).indices.numpy()  # topk.py:13, on the CPU
 
 
 @pytest.mark.parametrize("dtype", [torch.float16, torch.bfloat16])
