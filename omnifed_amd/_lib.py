@@ -1,4 +1,5 @@
-"""ctypes binding of ``libomf_codec.so`` (declarations: ``include/omf_codec.h``).
+"""ctypes binding of ``libomf_codec.so`` (declarations: ``include/omf_codec.h``, and the test /
+experiment hooks of ``include/omf_codec_experimental.h``).
 
 There is no CPU fallback: if the library is missing, ``lib()`` raises.  The
 library is built in-tree by ``omnifed_amd.build`` and loaded from
@@ -28,7 +29,7 @@ _c_f64 = ctypes.c_double
 _c_p = ctypes.c_void_p
 _c_size = ctypes.c_size_t
 
-# name -> (restype, argtypes); every symbol include/omf_codec.h declares.
+# name -> (restype, argtypes); every symbol include/omf_codec.h and omf_codec_experimental.h declare.
 SIGNATURES = {
     "omf_abi_version": (ctypes.c_int, []),
     "omf_last_error": (ctypes.c_char_p, []),
@@ -90,7 +91,7 @@ class CodecError(RuntimeError):
     pass
 
 
-ABI_VERSION = 109  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+ABI_VERSION = 110  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
 
 
 def lib() -> ctypes.CDLL:

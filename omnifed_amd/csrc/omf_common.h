@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <string>
 
 namespace omf {
@@ -27,7 +28,7 @@ struct TopkStats {
   double verdict_us = 0.0;
 };
 
-// Top-K encoder settings of a plan (omf_topk.hip): read from the OMF_TOPK_* environment once, at
+// Top-K encoder settings of a plan (omf_topk.hip): in experiment builds read from the OMF_TOPK_* environment once, at
 // the plan's first Top-K call, and settable by the omf_plan_set_topk test / experiment hook.
 struct TopkKnobs {
   TopkStats stats;
@@ -40,6 +41,19 @@ struct TopkKnobs {
   bool scatter_small = true;   // the bucket scatter's LDS-staged bucket table (OMF_TOPK_SCATTER_SMALL=0 off)
   bool planned_scatter = true; // the bucket plan inside the scatter launch (OMF_TOPK_PLANNED_SCATTER=0 off)
 };
+
+// Tuning knobs from the environment (OMF_TOPK_*, OMF_SPEC_*, OMF_RING_*, OMF_ENCODE_STRATEGY,
+// OMF_DEC_LDS): read only by experiment builds (-DOMF_EXPERIMENTS, scripts/exp/variant_lib.sh);
+// the product library ignores its environment and takes settings through the API alone
+// (omf_codec_experimental.h for the test / experiment hooks).
+inline const char* knob(const char* name) {
+#ifdef OMF_EXPERIMENTS
+  return std::getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // Thread-local error string behind omf_last_error().
 void set_error(const std::string& msg);

@@ -27,6 +27,7 @@
 #include <vector>
 
 #include "../../include/omf_codec.h"
+#include "../../include/omf_codec_experimental.h"
 #include "omf_common.h"
 #include "omf_qsgd_dev.h"
 #include "omf_ring.h"
@@ -2351,7 +2352,7 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
       delete p;
       return fail(OMF_EHIP, "omf_plan_create: cannot query the device");
     }
-    if (const char* ev = getenv("OMF_ENCODE_ROWS")) p->ev = atoi(ev) == 16 ? 16 : 8;  // tuning knob
+    if (const char* ev = omf::knob("OMF_ENCODE_ROWS")) p->ev = atoi(ev) == 16 ? 16 : 8;  // tuning knob
     const void* k16[5] = {(const void*)qsgd_encode_ordered<1, false, false, 16>,
                           (const void*)qsgd_encode_ordered<1, true, false, 16>,
                           (const void*)qsgd_encode_ordered<4, false, false, 16>,
@@ -2371,24 +2372,24 @@ int omf_plan_create(const int64_t* sizes, const int64_t* offsets, int32_t ntenso
     }
     p->cap = std::max<int64_t>(1, (int64_t)nb_min * prop.multiProcessorCount / 2);
     // Ring encoder: configuration and grid (tuning knobs for experiments only).
-    if (const char* rc = getenv("OMF_RING_CFG")) p->ring_cfg = std::max(0, std::min(atoi(rc), omf::ring::num_configs() - 1));
-    if (const char* bm = getenv("OMF_RING_BIG")) p->ring_big_mode = atoi(bm) == 1 ? 1 : 0;
-    if (const char* gp = getenv("OMF_RING_GAP")) p->ring_gap = atoll(gp);
+    if (const char* rc = omf::knob("OMF_RING_CFG")) p->ring_cfg = std::max(0, std::min(atoi(rc), omf::ring::num_configs() - 1));
+    if (const char* bm = omf::knob("OMF_RING_BIG")) p->ring_big_mode = atoi(bm) == 1 ? 1 : 0;
+    if (const char* gp = omf::knob("OMF_RING_GAP")) p->ring_gap = atoll(gp);
     // Switches that change what an encode writes (skipped launches, no quantisation) are never
     // read from the environment of a release build: tests set them per plan (omf_plan_set_debug);
     // experiment builds (-DOMF_EXPERIMENTS, scripts/exp/build_variants.sh) also take them here.
 #ifdef OMF_EXPERIMENTS
-    if (const char* dg = getenv("OMF_RING_DBG")) p->ring_dbg = (uint32_t)atoi(dg);
-    if (const char* sk = getenv("OMF_SPEC_SKIP")) p->spec_skip = (uint32_t)atoi(sk);
+    if (const char* dg = omf::knob("OMF_RING_DBG")) p->ring_dbg = (uint32_t)atoi(dg);
+    if (const char* sk = omf::knob("OMF_SPEC_SKIP")) p->spec_skip = (uint32_t)atoi(sk);
 #endif
-    if (const char* zs = getenv("OMF_SPEC_ZSIG")) p->spec_zsig = p->spec_zsig_wide = std::max(1.0f, (float)atof(zs));
+    if (const char* zs = omf::knob("OMF_SPEC_ZSIG")) p->spec_zsig = p->spec_zsig_wide = std::max(1.0f, (float)atof(zs));
     // Default strategy by arena size: the bracketed single-read encoder from 2^25 elements
     // (Llama-400M 0.386 ms against the two-pass 0.59 and the ring 0.63; Llama-150M 0.25 against
     // 0.35), the ring below (ResNet-18: 0.032 ms against 0.08 for the bracket's four launches).
     p->strategy = p->arena_end >= ((int64_t)1 << 25) ? 3 : 2;
-    if (const char* st = getenv("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 4));
-    if (const char* sw = getenv("OMF_SPEC_WIDE")) p->spec_wide = atoi(sw) != 0 ? 1 : 0;
-    if (const char* fb = getenv("OMF_SPEC_FB")) p->spec_fb = atoi(fb) != 0 ? 1 : 0;
+    if (const char* st = omf::knob("OMF_ENCODE_STRATEGY")) p->strategy = std::max(0, std::min(atoi(st), 4));
+    if (const char* sw = omf::knob("OMF_SPEC_WIDE")) p->spec_wide = atoi(sw) != 0 ? 1 : 0;
+    if (const char* fb = omf::knob("OMF_SPEC_FB")) p->spec_fb = atoi(fb) != 0 ? 1 : 0;
     {  // grid encoder: one 1024-thread workgroup per CU must fit
       int nb = 0;
       if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, (const void*)qsgd_encode_grid<1>, 1024, 0) == hipSuccess &&
@@ -2667,9 +2668,10 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     p->last_encoder = 4;
     return OMF_OK;
   }
-  // Bracketed single-read encoder: fp32 / bf16 / fp16 values with on-device draws at s <= 4
-  // (int32 payloads take the ring, caller uniforms the two-pass encoder; the fused PS step is
-  // fp32).  Three launches, no host interaction.
+  // Bracketed single-read encoder: fp32 / bf16 / fp16 values with on-device draws at s <= 4, and
+  // fp32 at s = 5-8 with wide levels (the default; int8 at 5-6, the int32 wire at 7-8); the rest
+  // (wide levels off: the int32 wire on the ring, s = 5-6 and caller uniforms on the two-pass
+  // encoder; the fused PS step is fp32).  No host interaction.
   if (!norm_only && spec_serves(p, s, u, divisor, fmt, acc_in == nullptr)) {
     // (the fused PS step too: the pass divides, stores the average and quantises it)
     SpecArgs sa;
@@ -2736,7 +2738,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     // waves per SIMD — 0.556-0.559 ms per Llama-400M s = 8 encode against 0.589 uncapped, 0.565 at 12
     // KiB, 0.635 at 16 KiB (scripts/exp/occ_ab.sh, two interleaved rounds); OMF_SPEC_LDS_W overrides.
     // The s <= 4 pass is co-bound by its VALU and keeps every wave (24 KiB: 0.367 against 0.360 ms).
-    static const size_t plds_w = [] { const char* v = getenv("OMF_SPEC_LDS_W"); return v ? (size_t)atoi(v) : (size_t)10240; }();
+    static const size_t plds_w = [] { const char* v = omf::knob("OMF_SPEC_LDS_W"); return v ? (size_t)atoi(v) : (size_t)10240; }();
     if (fb) {  // the bracket folded into the pass (its first workgroups)
       const int64_t nbrw = (int64_t)kFbParts * p->n_spec_br;
       const dim3 gfb((unsigned)(nbrw + p->n_spec_blocks));
@@ -2760,7 +2762,7 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     if (fb || wfb) {
       // (the pass ran above)
     } else if (wide) {  // fp32, no fused last client (spec_serves); one wave per workgroup unless OMF_SPEC_WPB=4
-      static const bool wpb4 = [] { const char* v = getenv("OMF_SPEC_WPB"); return v && atoi(v) == 4; }();
+      static const bool wpb4 = [] { const char* v = omf::knob("OMF_SPEC_WPB"); return v && atoi(v) == 4; }();
       const dim3 g1((unsigned)(p->n_spec_blocks * kWaves)), b1(64);
       if (wpb4) {
         if (width == 1 && !div) hipLaunchKernelGGL((qsgd_spec_quant<1, false, kFmtF32, 0, PWW>), gb, blk, 0, st, sa, sa.br, sa.begins, an);
@@ -2816,10 +2818,12 @@ static int encode_launch(omf_plan* p, const float* x, float alpha, int32_t s, co
     return OMF_OK;
   }
   // The ring also serves the fused PS step (divide + encode in one launch) under any strategy,
-  // and the bracketed plans' int32-wire encodes (s >= 7, fp32, on-device draws): Llama-400M s = 8
-  // 0.68 ms against 0.74 for the two-pass encoder, whose second pass rewrites the 4 N payload
-  // after re-reading x (scripts/exp/s8_strategies.sh).  bf16 / fp16 values and caller uniforms
-  // stay on the two-pass encoder (0.61 / 0.78 ms against the ring's 0.70 / 0.83).
+  // and — with wide levels off (omf_plan_set_wide_levels) — the bracketed plans' int32-wire
+  // encodes (s >= 7, fp32, on-device draws): Llama-400M s = 8 0.68 ms against 0.74 for the
+  // two-pass encoder, whose second pass rewrites the 4 N payload after re-reading x (round 4).
+  // With wide levels on (the default) those take the bracketed encoder above.  bf16 / fp16
+  // values and caller uniforms stay on the two-pass encoder (0.61 / 0.78 ms against the ring's
+  // 0.70 / 0.83).
   const bool wide_ring = p->strategy == 3 && width == 4 && !u && fmt == 0;
   if ((p->strategy == 2 || p->strategy == 4 || divisor != 0.0f || wide_ring) && !norm_only) {
     omf::ring::Args r;
@@ -2991,7 +2995,7 @@ static int decode_blocks(omf_plan* p, const void* q, int32_t width, int32_t leve
   // A plain decode's workgroups reserve 24 KiB of LDS each (unused): six per CU — Llama-400M 0.294-
   // 0.296 ms at s = 4 and 0.482-0.484 at s = 8 against 0.301 / 0.490 uncapped, 0.308 / 0.489 at 28 KiB
   // (scripts/exp/occ_ab.sh); OMF_DEC_LDS overrides.  Accumulating decodes keep every wave.
-  static const size_t dlds = [] { const char* v = getenv("OMF_DEC_LDS"); return v ? (size_t)atoi(v) : (size_t)24576; }();
+  static const size_t dlds = [] { const char* v = omf::knob("OMF_DEC_LDS"); return v ? (size_t)atoi(v) : (size_t)24576; }();
   // the last whole quad of the payload the caller holds (width 8: round_up(arena_end, 4) bytes
   // are not promised, so a clamped load never passes the last full quad)
   const int64_t qlast = (p->arena_end & ~(int64_t)3) - 4;  // < 0 only for arenas of < 4 elements

@@ -30,6 +30,7 @@
 // so a wave reads 1 KiB contiguous per instruction and a thread's four consecutive rows
 // form one Philox group of the stream in oracle/philox.py.
 #include "../../include/omf_codec.h"
+#include "../../include/omf_codec_experimental.h"
 #include "omf_common.h"
 #include "omf_qsgd_dev.h"
 #include "omf_ring.h"

@@ -46,6 +46,7 @@
 #include <vector>
 
 #include "../../include/omf_codec.h"
+#include "../../include/omf_codec_experimental.h"
 #include "omf_common.h"
 
 using namespace omf;
@@ -2398,7 +2399,8 @@ std::vector<Group> make_groups(const std::vector<int64_t>& sizes, double ratio, 
   return gs;
 }
 
-// The plan's Top-K settings: the OMF_TOPK_* environment read once, at its first Top-K call
+// The plan's Top-K settings: in experiment builds (omf::knob) the OMF_TOPK_* environment read once, at
+// its first Top-K call
 // (OMF_TOPK_GROUPS, OMF_TOPK_DBG, OMF_TOPK_FALLBACK, OMF_TOPK_SAMPLE_RUNS, OMF_TOPK_SURE="z,c",
 // OMF_TOPK_SCATTER_SMALL, OMF_TOPK_PLANNED_SCATTER),
 // unless omf_plan_set_topk set them first.
@@ -2406,8 +2408,8 @@ const TopkKnobs& knobs(omf_plan* p) {
   TopkKnobs& k = omf_plan_access::topk_knobs(p);
   if (k.init) return k;
   k.init = true;
-  if (const char* e = std::getenv("OMF_TOPK_GROUPS")) k.groups = std::max(1, std::atoi(e));
-  if (const char* e = std::getenv("OMF_TOPK_DBG")) {
+  if (const char* e = omf::knob("OMF_TOPK_GROUPS")) k.groups = std::max(1, std::atoi(e));
+  if (const char* e = omf::knob("OMF_TOPK_DBG")) {
     // 4 = print the verdict flags, 8 = print over-full fine bins; experiment builds only
     // (-DOMF_EXPERIMENTS; they change what an encode writes): 1 = no bucket sort, 2 = no residual zeroing
     const int d = std::atoi(e);
@@ -2417,14 +2419,14 @@ const TopkKnobs& knobs(omf_plan* p) {
     k.dbg = d & ~3;
 #endif
   }
-  if (const char* e = std::getenv("OMF_TOPK_FALLBACK")) k.force_fallback = e[0] == '1';
-  if (const char* e = std::getenv("OMF_TOPK_SCATTER_SMALL")) k.scatter_small = e[0] != '0';
-  if (const char* e = std::getenv("OMF_TOPK_PLANNED_SCATTER")) k.planned_scatter = e[0] != '0';
-  if (const char* e = std::getenv("OMF_TOPK_SAMPLE_RUNS")) {
+  if (const char* e = omf::knob("OMF_TOPK_FALLBACK")) k.force_fallback = e[0] == '1';
+  if (const char* e = omf::knob("OMF_TOPK_SCATTER_SMALL")) k.scatter_small = e[0] != '0';
+  if (const char* e = omf::knob("OMF_TOPK_PLANNED_SCATTER")) k.planned_scatter = e[0] != '0';
+  if (const char* e = omf::knob("OMF_TOPK_SAMPLE_RUNS")) {
     const long long v = std::atoll(e);
     if (v >= 64 && v <= (1 << 20)) k.sample_runs = v;
   }
-  if (const char* e = std::getenv("OMF_TOPK_SURE")) {
+  if (const char* e = omf::knob("OMF_TOPK_SURE")) {
     float z = 0.f, c = 0.f;
     if (std::sscanf(e, "%f,%f", &z, &c) == 2 && z >= 0.f && c >= 0.f) {
       k.sure_z = z;

@@ -12,12 +12,25 @@ from omnifed_amd import _lib
 from omnifed_amd.build import INCLUDE, LIB, build
 
 HEADER = os.path.join(INCLUDE, "omf_codec.h")
+EXPERIMENTAL = os.path.join(INCLUDE, "omf_codec_experimental.h")
 
 
-def _declared():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(omf_[a-z0-9_]+)\s*\(", src)))
+def _declared(path=None):
+    paths = [path] if path else [HEADER, EXPERIMENTAL]
+    names = set()
+    for p in paths:
+        src = re.sub(r"/\*.*?\*/", "", open(p).read(), flags=re.S)
+        names |= set(re.findall(r"\b(omf_[a-z0-9_]+)\s*\(", src))
+    return sorted(names)
+
+
+def test_drop_in_header_has_no_experiment_hooks():
+    """The drop-in boundary (omf_codec.h) declares no tuning / debug hook; those live in
+    omf_codec_experimental.h, and neither header declares a symbol twice."""
+    main, exp = set(_declared(HEADER)), set(_declared(EXPERIMENTAL))
+    assert not main & exp
+    assert not any(re.search(r"(debug|ring|set_topk|set_wide|fused_bracket|resident|spec_stats)", n) for n in main), main
+    assert {"omf_plan_set_debug", "omf_plan_set_topk", "omf_plan_set_ring"} <= exp
 
 
 def test_build_and_load():

@@ -303,9 +303,10 @@ def test_full_config_parity_mt_stream(gpu, cfg, bits):
 @pytest.mark.parametrize("cfg,s", [("llama400m", 4), ("llama150m", 4), ("llama150m", 8)])
 def test_full_config_properties(gpu, cfg, s):
     """Full-size arenas: size-independent properties + exact oracle spot checks on 3 tensors.
-    llama150m s=4 is the bench's other_configs arena on the bracketed encoder; s=8 (the int32
-    wire) takes the ring encoder on these bracketed plans — every tensor of it is pinned to the
-    oracle in test_gpu_headline_pin.py."""
+    llama150m s=4 is the bench's other_configs arena; every encode here takes the bracketed
+    encoder (s = 8, the int32 wire, through its wide-level variant: plan.last_encoder is asserted),
+    and every tensor of each configuration is pinned to the oracle in test_gpu_headline_pin.py.
+    The ring's int32-wire path is covered with wide levels off (test_full_config_ring_int32)."""
     named = shapes.model_shapes(cfg)
     sizes = [shapes.numel(sh) for _, sh in named]
     plan = codec.Plan.get(sizes, device=gpu)
@@ -315,6 +316,7 @@ def test_full_config_properties(gpu, cfg, s):
     seed, off = 42, 3
     q, norms = plan.qsgd_encode(x, s, seed=seed, offset=off)
     plan.check()
+    assert plan.last_encoder == "bracket", (cfg, s)
     L = 2**s
     width = 8 if L <= 127 else 32
     y = plan.qsgd_decode(q, width, L, norms)
@@ -339,3 +341,22 @@ def test_full_config_properties(gpu, cfg, s):
         u = oracle.philox_uniforms(seed, off, t, n)
         want = _oracle_q(xh[o:o + n], s, float(nh[t]), u)
         assert qh[o:o + n].tobytes() == want.tobytes(), t
+
+
+def test_full_config_ring_int32(gpu):
+    """The ring encoder's int32 wire on a bracketed plan (wide levels off: s = 8 goes to the ring):
+    every tensor of Llama-150M equals the oracle given the norm."""
+    named = shapes.model_shapes("llama150m")
+    sizes = [shapes.numel(sh) for _, sh in named]
+    plan = codec.Plan(sizes, device=gpu)
+    plan.set_wide_levels(False)
+    g = torch.Generator(device=gpu).manual_seed(1)
+    x = torch.randn(plan.arena_end, device=gpu, generator=g) * 1e-3
+    seed, off, s = 7, 2, 8
+    q, norms = plan.qsgd_encode(x, s, seed=seed, offset=off)
+    plan.check()
+    assert plan.last_encoder == "ring"
+    xh, qh, nh = x.cpu().numpy(), q.cpu().numpy(), norms.cpu()
+    for t, (o, n) in enumerate(zip(plan.offsets, sizes)):
+        u = oracle.philox_uniforms(seed, off, t, n)
+        assert qh[o:o + n].tobytes() == _oracle_q(xh[o:o + n], s, float(nh[t]), u).tobytes(), t
