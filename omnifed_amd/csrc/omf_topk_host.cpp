@@ -15,18 +15,18 @@
 //   - magnitudes become 31-bit keys (the bits of |t|, every NaN one key above +inf), so
 //     comp(a, b) == key(a) > key(b) exactly (equal keys <=> neither is before the other);
 //   - the heap regime is libstdc++'s algorithm restated on a k-entry heap: make the heap of the
-//     first k pairs, then for each later pair that compares before the top, the top's
-//     replacement (__pop_heap(first, middle, i): the hole walks from the root to a leaf along the
-//     child that is not "before" its sibling — the right one on a tie — and the new pair bubbles
-//     up from there), then the heap sort (the same replacement with the last entry, shrinking).
-//     Pairs that never enter the heap are only compared, so the n-pair array is never built;
+//     first k pairs (std::make_heap), then for each later pair that compares before the top, the
+//     top's replacement (__pop_heap(first, middle, i): the hole walks from the root to a leaf along
+//     the child that is not "before" its sibling — the right one on a tie — and the new pair
+//     bubbles up from there), then the heap sort (the same replacement with the last entry,
+//     shrinking).  Pairs that never enter the heap are only compared, so the n-pair array is never
+//     built; keys and indices live in two arrays, the walk reading keys only;
 //   - the introselect regime calls std::nth_element on the n pairs with the same comparison.
 // tests/test_topk_order_host.py pins both against torch.topk on tie-heavy inputs (CPU).
 #include <algorithm>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
-#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -52,47 +52,55 @@ struct Before {  // torch's comparison: a goes before b
   bool operator()(Entry a, Entry b) const { return (a >> 32) > (b >> 32); }
 };
 
-// libstdc++'s __adjust_heap(h, 0, len, v) followed by its __push_heap: the replacement of the
-// top of the heap h[0, len) by v.  The walk prefetches the one 64-byte line that holds the hole's
-// descendants three levels down (the heap's base is placed so that line is aligned).
-inline void replace_top(Entry* h, int64_t len, Entry v) {
-  const Before before;
-  int64_t hole = 0, child = 0;
-  const int64_t inner = (len - 1) / 2;
-  while (child < inner) {
-    __builtin_prefetch(&h[8 * (child + 1) - 1]);
-    child = 2 * (child + 1);
-    if (before(h[child], h[child - 1])) --child;
-    h[hole] = h[child];
-    hole = child;
+// libstdc++'s __adjust_heap(h, 0, len, v) followed by its __push_heap — the replacement of the
+// top of the heap [0, len) by (kv, iv) — on split key / index arrays (the walk reads keys only).
+// The hole walks from the root to a leaf along the child that is not "before" its sibling (the
+// right one on a tie), two levels per step where both exist: the children and the four
+// grandchildren are loaded together and the two choices made without branches, so one memory
+// round trip serves two levels; then the new pair bubbles up from the leaf.
+inline void replace_top(uint32_t* __restrict K, uint32_t* __restrict I, int64_t len, uint32_t kv, uint32_t iv) {
+  int64_t hole = 0;
+  const int64_t inner = (len - 1) / 2;    // a hole below this has two children
+  const int64_t inner2 = (inner - 1) / 2;  // ... and so do both of them
+  while (hole < inner2) {
+    __builtin_prefetch(&K[16 * hole + 15]);  // four levels down
+    const int64_t c = 2 * hole + 1;
+    const uint32_t kl = K[c], kr = K[c + 1];
+    const uint32_t g0 = K[2 * c + 1], g1 = K[2 * c + 2], g2 = K[2 * c + 3], g3 = K[2 * c + 4];
+    const bool left = kr > kl;
+    const int64_t cc = left ? c : c + 1;
+    const uint32_t a = left ? g0 : g2, b = left ? g1 : g3;
+    const bool left2 = b > a;
+    const int64_t c2 = 2 * cc + (left2 ? 1 : 2);
+    K[hole] = left ? kl : kr;
+    I[hole] = I[cc];
+    K[cc] = left2 ? a : b;
+    I[cc] = I[c2];
+    hole = c2;
   }
-  if ((len & 1) == 0 && child == (len - 2) / 2) {
-    child = 2 * (child + 1);
-    h[hole] = h[child - 1];
-    hole = child - 1;
+  while (hole < inner) {
+    const int64_t c = 2 * hole + 1;
+    const int64_t cc = K[c + 1] > K[c] ? c : c + 1;
+    K[hole] = K[cc];
+    I[hole] = I[cc];
+    hole = cc;
+  }
+  if ((len & 1) == 0 && hole == (len - 2) / 2) {  // the one node with a left child only
+    const int64_t c = 2 * hole + 1;
+    K[hole] = K[c];
+    I[hole] = I[c];
+    hole = c;
   }
   int64_t parent = (hole - 1) / 2;
-  while (hole > 0 && before(h[parent], v)) {
-    h[hole] = h[parent];
+  while (hole > 0 && K[parent] > kv) {
+    K[hole] = K[parent];
+    I[hole] = I[parent];
     hole = parent;
     parent = (hole - 1) / 2;
   }
-  h[hole] = v;
+  K[hole] = kv;
+  I[hole] = iv;
 }
-
-struct AlignedEntries {
-  Entry* base = nullptr;
-  Entry* data = nullptr;  // data[8m - 1] starts a 64-byte line
-  explicit AlignedEntries(int64_t n) {
-    base = static_cast<Entry*>(::operator new[](sizeof(Entry) * (size_t)(n + 8), std::align_val_t(64), std::nothrow));
-    data = base ? base + 1 : nullptr;
-  }
-  ~AlignedEntries() {
-    if (base) ::operator delete[](base, std::align_val_t(64));
-  }
-  AlignedEntries(const AlignedEntries&) = delete;
-  AlignedEntries& operator=(const AlignedEntries&) = delete;
-};
 
 }  // namespace
 
@@ -101,25 +109,34 @@ int torch_topk_select(const float* t, int64_t n, int64_t k, int64_t* out) {
   if (k < 1 || k > n || n > 0xffffffffLL) return fail(OMF_EINVAL, "omf_topk_select_host: need 1 <= k <= n < 2^32");
   const Before before;
   if (k * 64 <= n) {
-    AlignedEntries heap(k);
-    if (!heap.data) return fail(OMF_ENOMEM, "omf_topk_select_host: heap allocation failed");
-    Entry* h = heap.data;
+    std::vector<Entry> h;
+    std::vector<uint32_t> K, I;
+    try {
+      h.resize((size_t)k);
+      K.resize((size_t)k + 64);
+      I.resize((size_t)k + 64);
+    } catch (const std::bad_alloc&) {
+      return fail(OMF_ENOMEM, "omf_topk_select_host: heap allocation failed");
+    }
     for (int64_t i = 0; i < k; ++i) h[i] = (Entry)mag_key_host(t[i]) << 32 | (uint32_t)i;
-    std::make_heap(h, h + k, before);
-    uint32_t top = (uint32_t)(h[0] >> 32);
+    std::make_heap(h.begin(), h.end(), before);
+    for (int64_t i = 0; i < k; ++i) {
+      K[i] = (uint32_t)(h[i] >> 32);
+      I[i] = (uint32_t)h[i];
+    }
+    uint32_t* kp = K.data();
+    uint32_t* ip = I.data();
     for (int64_t i = k; i < n; ++i) {
       const uint32_t key = mag_key_host(t[i]);
-      if (key > top) {  // before(pair i, top): it replaces the top
-        replace_top(h, k, (Entry)key << 32 | (uint32_t)i);
-        top = (uint32_t)(h[0] >> 32);
-      }
+      if (key > kp[0]) replace_top(kp, ip, k, key, (uint32_t)i);  // before(pair i, top): it replaces the top
     }
     for (int64_t last = k - 1; last > 0; --last) {  // the heap sort: __pop_heap(h, h + last, h + last)
-      const Entry v = h[last];
-      h[last] = h[0];
-      replace_top(h, last, v);
+      const uint32_t kv = kp[last], iv = ip[last];
+      kp[last] = kp[0];
+      ip[last] = ip[0];
+      replace_top(kp, ip, last, kv, iv);
     }
-    for (int64_t j = 0; j < k; ++j) out[j] = (int64_t)(uint32_t)h[j];
+    for (int64_t j = 0; j < k; ++j) out[j] = (int64_t)ip[j];
     return OMF_OK;
   }
   std::vector<Entry> q;
