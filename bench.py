@@ -460,7 +460,23 @@ def main():
                              "kernel": "omf_topk_encode (all launches of one call, host sync included)",
                              "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(tenc, 4),
                              "decode_ms": round(tdec, 4)},
-                "encoder_paths": plan.topk_stats()}  # timed calls: bucket-sort fast path vs fallbacks
+                "encoder_paths": plan.topk_stats(),  # timed calls: bucket-sort fast path vs fallbacks
+                "tie_order": "index"}
+        if not args.no_extras:
+            # the drop-in's default order (the reference's bytes where magnitudes tie): the device encode,
+            # then omf_topk_torch_order's census and host rewrite of the tied tensors; wall clock
+            progress("topk torch order")
+            tw, nre = [], []
+            for i in range(3):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                plan.topk_encode(xs[i % len(xs)], ratio, residual=res, residual_mode=1, values=vals, indices=idx,
+                                 alpha=weight, tie_order="torch")
+                torch.cuda.synchronize()
+                tw.append((time.perf_counter() - t0) * 1e3)
+                nre.append(plan.topk_reordered)
+            topk["torch_order"] = {"ms_per_encode": round(sorted(tw)[1], 2), "tensors_rewritten": nre,
+                                   "tensors": plan.nt, "host_threads": min(16, os.cpu_count() or 1)}
         del res, yt, xs
 
     extras = {}
@@ -516,10 +532,54 @@ def main():
             pcie_step(i)
         torch.cuda.synchronize()
         pt = (time.perf_counter() - t1) / 5
+        # Pipelined: the uplink (x in, encode, payload out) and the downlink (payload in, decode,
+        # fp32 out) on two streams, step i's downlink beside step i+1's uplink, so each PCIe
+        # direction carries 4 N + w N bytes per step at once (PCIe is full duplex).  Double-buffered
+        # device payloads and norms; the downlink of step i waits for its payload's arrival on the host.
+        s_up, s_dn = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+        q2 = [torch.empty_like(q) for _ in range(2)]
+        n2 = [torch.empty_like(norms) for _ in range(2)]
+        nh = torch.empty(norms.numel(), dtype=norms.dtype, pin_memory=True)
+        qd = torch.empty_like(q)
+        nd = torch.empty_like(norms)
+        ev_q = [torch.cuda.Event() for _ in range(2)]
+        ev_free = [torch.cuda.Event() for _ in range(2)]
+
+        def pipe_step(i):
+            b = i & 1
+            with torch.cuda.stream(s_up):
+                s_up.wait_event(ev_free[b])  # the host payload buffer's previous reader is done
+                xd.copy_(xh, non_blocking=True)
+                plan.qsgd_encode(xd, s, q_out=q2[b], norm_out=n2[b], alpha=weight, seed=seed, offset=20_000 + i)
+                qh.copy_(q2[b], non_blocking=True)
+                nh.copy_(n2[b], non_blocking=True)
+                ev_q[b].record(s_up)
+            with torch.cuda.stream(s_dn):
+                s_dn.wait_event(ev_q[b])
+                qd.copy_(qh, non_blocking=True)
+                nd.copy_(nh, non_blocking=True)
+                ev_free[b].record(s_dn)
+                plan.qsgd_decode(qd, width, L, nd, y_out=y)
+                yh.copy_(y, non_blocking=True)
+
+        for b in range(2):
+            ev_free[b].record(torch.cuda.current_stream(dev))
+        pipe_step(0)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for i in range(1, 9):
+            pipe_step(i)
+        torch.cuda.synchronize()
+        pp = (time.perf_counter() - t1) / 8
         extras["pcie_inclusive"] = {"ms_per_step": round(pt * 1e3, 3),
                                     "algorithmic_GBs": round((8 + 2 * w) * N / pt / 1e9, 2),
-                                    "fp32_gradient_GBs": round(4 * N / pt / 1e9, 2)}
-        del xh, qh, yh, xd
+                                    "fp32_gradient_GBs": round(4 * N / pt / 1e9, 2),
+                                    "serial": "H2D x, encode, D2H payload, H2D payload, decode, D2H y on one stream",
+                                    "pipelined_ms_per_step": round(pp * 1e3, 3),
+                                    "pipelined_algorithmic_GBs": round((8 + 2 * w) * N / pp / 1e9, 2),
+                                    "pipelined": "uplink and downlink on two streams, step i's downlink beside step "
+                                                 "i+1's uplink (PCIe full duplex); steady state over 8 steps"}
+        del xh, qh, yh, xd, q2, n2, qd, nd
     if not args.no_extras and dist.is_initialized():
         progress("PS aggregates over the process group")
         from omnifed_amd.ps import GpuOps, qsgd_weighted_round, topk_sparse_aggregate, total_weight

@@ -393,13 +393,22 @@ def set_pinned_arenas(max_bytes: int) -> None:
 
 
 def pinned_arena(nbytes: int) -> Optional[torch.Tensor]:
-    """A page-locked pooled arena of ``nbytes`` if the budget allows, else None."""
+    """A page-locked pooled arena of ``nbytes`` if the budget allows, else None.  With no budget,
+    the buffers of leases handed out before it was removed are unlocked and freed here as they come
+    back (their finalisers only queue them)."""
     if PINNED_ARENAS.max_bytes <= 0:
+        if PINNED_ARENAS._returned:
+            with PINNED_ARENAS._lock:
+                PINNED_ARENAS._drain()
         return None
     return PINNED_ARENAS.empty(nbytes)
 
 
-RING_CHUNK_BYTES = 8 << 20
+# 32 MiB chunks x max(4, workers()) slots (256 MiB of staging at 8 copy threads): the pageable CPU
+# placement of a Llama-400M QSGD decode took 56.7 / 52.8 / 47.6-54.6 / 45.8 ms at 8 / 16 / 32 / 64 MiB
+# chunks on one box (scripts/exp/host_decode_sweep.py; fewer, larger chunks cost the feeder thread
+# fewer Python round trips), 16 slots no better than 8.
+RING_CHUNK_BYTES = 32 << 20
 
 
 class D2HRing:
@@ -411,12 +420,12 @@ class D2HRing:
     on its own stream while earlier results flow out (PCIe is full duplex).  ``close()`` (or the
     context's exit) returns when every byte has landed; a failure in the feeder is raised there."""
 
-    def __init__(self, dst_ptr: int, stream, key: str = "d2h", limit: int = RING_CHUNK_BYTES,
+    def __init__(self, dst_ptr: int, stream, key: str = "d2h", limit: Optional[int] = None,
                  slots: Optional[int] = None):
         import queue
 
-        self.dst, self.stream, self.limit = int(dst_ptr), stream, int(limit)
-        self.n_slots = slots or max(4, 2 * workers())
+        self.dst, self.stream, self.limit = int(dst_ptr), stream, int(limit or RING_CHUNK_BYTES)
+        self.n_slots = slots or max(4, workers())
         self._cm = STAGING.lease(key, self.n_slots * self.limit)
         self._lease = self._cm.__enter__()
         self._base = self._lease.buf.data_ptr()
@@ -483,7 +492,7 @@ class D2HRing:
         self.close()
 
 
-def device_to_host(src: torch.Tensor, stream=None, key: str = "d2h", limit: int = RING_CHUNK_BYTES,
+def device_to_host(src: torch.Tensor, stream=None, key: str = "d2h", limit: Optional[int] = None,
                    slots: Optional[int] = None, pool_memory: bool = True) -> torch.Tensor:
     """A CPU copy of the device tensor ``src`` (1-D, same dtype), queued on ``stream`` (default the
     current stream of ``src``'s device) behind the work already there.  Into a page-locked pooled

@@ -1,6 +1,6 @@
 """ResNet-18 (BASELINE config 2) encoder variants, interleaved in one process (HIP events around
 `reps` back-to-back calls, median over rounds): the ring encoder (default below 2^25 elements), the
-grid encoder, and two launches — the norms pass (omf_qsgd_norms) then the quantiser with those
+grid encoder, the bracketed single-read encoder (fused bracket), and two launches — the norms pass (omf_qsgd_norms) then the quantiser with those
 norms (omf_qsgd_encode norm_in) — plus the decoder and encode + decode steps.  s = 3 (8 levels)."""
 import json
 import sys
@@ -15,9 +15,10 @@ rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 9
 reps = 50
 dev = torch.device("cuda", 0)
 sizes = [shapes.numel(sh) for _, sh in shapes.model_shapes("resnet18")]
-plans = {name: codec.Plan(sizes, device=dev) for name in ("ring", "grid", "two")}
+plans = {name: codec.Plan(sizes, device=dev) for name in ("ring", "grid", "two", "bracket")}
 plans["grid"].set_encode_strategy("grid")
 plans["two"].set_encode_strategy("ordered")
+plans["bracket"].set_encode_strategy("bracket")  # the fused-bracket single-read encoder
 g = torch.Generator(device=dev).manual_seed(1000)
 x = torch.randn(plans["ring"].arena_end, device=dev, generator=g) * 1e-3
 L = 2**s
@@ -68,4 +69,5 @@ for name in plans:
     torch.cuda.synchronize()
     outs[name] = (q.clone(), nr.clone())
 out["norms_equal_ring_grid"] = bool(torch.equal(outs["ring"][1], outs["grid"][1]))
+out["bracket_encoder"] = plans["bracket"].last_encoder
 print(json.dumps(out), flush=True)

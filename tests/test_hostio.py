@@ -73,3 +73,27 @@ def test_wire_host_memory_policy_once_and_opt_out(monkeypatch):
 
 def test_retain_host_memory_sets_mallopt():
     assert hostio.retain_host_memory() in (True, False)  # False only without glibc
+
+
+def test_pinned_leases_returned_after_the_budget_is_removed_are_released(monkeypatch):
+    """A page-locked arena handed out while the budget allowed it, dropped after set_pinned_arenas(0):
+    the next pinned_arena call (which returns None) unlocks and frees it, so no page-locked memory
+    outlives the budget (the early return used to skip the drain)."""
+    import gc
+
+    from omnifed_amd import hostio
+
+    locked = {}
+    monkeypatch.setattr(hostio, "_register", lambda ptr, n: locked.__setitem__(ptr, n) or True)
+    monkeypatch.setattr(hostio, "_unregister", lambda ptr: locked.pop(ptr))
+    pool = hostio.HostArenaPool(max_bytes=0, pinned=True)
+    monkeypatch.setattr(hostio, "PINNED_ARENAS", pool)
+    hostio.set_pinned_arenas(64 << 20)
+    a = hostio.pinned_arena(8 << 20)
+    assert a is not None and len(locked) == 1 and pool.live_bytes > 0
+    hostio.set_pinned_arenas(0)  # the lease is still out: nothing to drain yet
+    assert len(locked) == 1
+    del a
+    gc.collect()
+    assert hostio.pinned_arena(8 << 20) is None
+    assert not locked and pool.live_bytes == 0
