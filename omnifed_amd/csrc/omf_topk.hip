@@ -94,7 +94,10 @@ constexpr int kFineMargin = OMF_FINE_MARGIN;  // a fine bin expects <= kBucketHa
 constexpr int kBucketHalf = 2048;
 constexpr int kBT = 512;              // bucket-sort block: 512 threads x 8 keys = 2 kBucketHalf
 constexpr int kBI = 8;
-constexpr int kPlanMaxBuckets = (1 << 25) / kBucketHalf + 2;
+constexpr int kPlanMaxBuckets = (1 << 25) / kBucketHalf + 2;  // topk_plan's rule (no big-bin buckets)
+// A tensor's bucket-key region: k + kBucketPad keys (the k-th key's bin may run past rank k by up to
+// one bucket's worth: a fine bin of up to 2 kBucketHalf keys sits in a bucket of its own).
+constexpr int kBucketPad = 2 * kBucketHalf;
 #ifndef OMF_TK_SUBPER  // experiment builds may override it
 #define OMF_TK_SUBPER 512
 #endif
@@ -162,9 +165,11 @@ __device__ __forceinline__ float tprime(float x, float r, float alpha) {
 
 // Per tensor: k, the output offset, the tensor's flat-item range (items are 16 Ki
 // sub-chunks in tensor order: omf_qsgd.hip upload_plan), its bucket-table range (bbase) and
-// bucket-buffer region (kb2, k + kBucketHalf keys).  One block; nt may exceed it.  Clears the
+// bucket-buffer region (kb2, k + kBucketPad keys).  One block; nt may exceed it.  Clears the
 // call's status words.
-__host__ __device__ __forceinline__ uint32_t bucket_slots(int64_t k) { return (uint32_t)((k + kBucketHalf) / kBucketHalf + 1); }
+// Bucket slots of a tensor: the kBucketHalf-wide rank windows below k, plus one bucket of its own for
+// each "big" fine bin (> kBucketHalf keys, topk_scatter_planned), at most k / (kBucketHalf + 1) + 1 of them.
+__host__ __device__ __forceinline__ uint32_t bucket_slots(int64_t k) { return (uint32_t)(2 * (k / kBucketHalf) + 3); }
 
 __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict__ tsize, int32_t nt, double ratio,
                                                        int64_t* __restrict__ kk, int64_t* __restrict__ koff,
@@ -212,7 +217,7 @@ __global__ __launch_bounds__(kThreads) void topk_setup(const int64_t* __restrict
       tlast[t] = (uint32_t)(carry_i + s_i[threadIdx.x] - 1);
       bbase[t] = (uint32_t)(carry_b + s_b[threadIdx.x] - nb);
       sbase[t] = carry_s + s_s[threadIdx.x] - ns;
-      kb2[t] = carry_k + s_k[threadIdx.x] - k + (int64_t)t * kBucketHalf;
+      kb2[t] = carry_k + s_k[threadIdx.x] - k + (int64_t)t * kBucketPad;
       if (t == nt - 1) {
         koff[nt] = carry_k + s_k[threadIdx.x];
         bbase[nt] = (uint32_t)(carry_b + s_b[threadIdx.x]);
@@ -1134,6 +1139,7 @@ __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const ui
   const bool zero_mode = tkey[t] == 1u;
   uint64_t k = (uint64_t)kk[t];
   const uint32_t b0 = bbase[t], nbmax = bbase[t + 1] - b0;
+  const uint32_t nbl = min(nbmax, (uint32_t)kPlanMaxBuckets);  // this rule's buckets: se / kBucketHalf < nbl
   const uint32_t* ht = fhist + (size_t)t * kFineMax;
   uint32_t h[PER], loc = 0;
 #pragma unroll
@@ -1147,7 +1153,7 @@ __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const ui
     s_nb = 0;
     s_over = 0;
   }
-  for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) s_bs[j] = 0xffffffffu;
+  for (uint32_t j = threadIdx.x; j < nbl; j += 1024) s_bs[j] = 0xffffffffu;
   uint32_t tot32;
   const uint32_t inc = block_scan_incl<1024>(loc, part, tot32);
   const uint64_t total = tot32;
@@ -1195,7 +1201,7 @@ __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const ui
   for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) {
     const uint32_t g = b0 + j;
     uint32_t st = 0, c = 0;
-    if (j < nb && s_bs[j] != 0xffffffffu) {
+    if (j < nb && j < nbl && s_bs[j] != 0xffffffffu) {
       st = s_bs[j];
       const uint32_t en = j + 1 < nb ? s_bs[j + 1] : s_kend;
       c = en > st ? en - st : 0u;
@@ -1249,7 +1255,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   const int t = v.t;
   const uint32_t lo = tlo[t], F = fcount[t], b0 = bbase[t], nb = bbase[t + 1] - b0, hi = thi[t];
   const int64_t base = tbegin[t];
-  for (uint32_t j = threadIdx.x; j < nb; j += 1024) s_b[j] = 0;
+  const uint32_t nbl = SMALL ? nb : min(nb, (uint32_t)kPlanMaxBuckets);  // topk_plan's buckets are < nbl
+  for (uint32_t j = threadIdx.x; j < nbl; j += 1024) s_b[j] = 0;
   const uint32_t* map_t = s_map;
   const int32_t* fb = fbucket + (size_t)t * kFineMax;
   if (SMALL)
@@ -1306,7 +1313,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     }
     __syncthreads();
     if (phase == 0) {  // reserve each touched bucket's range; s_b := this block's first slot
-      for (uint32_t q = threadIdx.x; q < nb; q += 1024)
+      for (uint32_t q = threadIdx.x; q < nbl; q += 1024)
         if (s_b[q]) s_b[q] = bstart[b0 + q] + atomicAdd(&bfill[b0 + q], s_b[q]);
       __syncthreads();
     }
@@ -1622,30 +1629,47 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     s_bs[j] = 0xffffffffu;
     s_b[j] = 0;
   }
-  uint32_t tot32;
+  uint32_t tot32, big_tot;
   const uint32_t inc = block_scan_incl<1024>(loc, s_part, tot32);  // begins with a barrier
+  // Big fine bins (> kBucketHalf keys, up to 2 kBucketHalf) get a bucket of their own: bin i goes to
+  // bucket floor(se_i / kBucketHalf) + B_i + big_i, B_i = big bins above it, so every other bucket
+  // still holds the bins whose rank starts fall in one kBucketHalf window (<= 2 kBucketHalf keys)
+  // and a big bin's bucket holds it alone.  Only a bin of more than 2 kBucketHalf keys (one
+  // magnitude key shared that widely, a cluster the fine bins cannot split) takes the fallback.
+  uint32_t my_big = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) my_big += h[j] > (uint32_t)kBucketHalf ? 1u : 0u;
+  const uint32_t big_inc = block_scan_incl<1024>(my_big, s_part, big_tot);
   const bool zero_mode = tkey[t] == 1u;
   uint64_t k = (uint64_t)kk[t];
   const bool redo = tot32 < k && !zero_mode;  // the sampled threshold was too high: exact redo
   const bool zero_fill = tot32 < k && zero_mode;  // every candidate selected, then zeros
   if (zero_fill) k = tot32;
   if (!redo) {
-    uint64_t se = tot32 - inc;  // keys in the bins of higher threads
+    uint64_t se = tot32 - inc;          // keys in the bins of higher threads
+    uint32_t above = big_tot - big_inc;  // big bins of higher threads
 #pragma unroll
     for (int j = PER - 1; j >= 0; --j) {
       const uint32_t i = PER * threadIdx.x + j;
       int32_t bucket = -1;
+      const bool big = h[j] > (uint32_t)kBucketHalf;
       if (h[j] && se < k) {
-        bucket = (int32_t)(se / kBucketHalf);
-        atomicMin(&s_bs[bucket], (uint32_t)se);
-        if (h[j] > (uint32_t)kBucketHalf) s_over = 1u;  // (OMF_TOPK_PLANNED_SCATTER=0 with OMF_TOPK_DBG=8 names it)
-        if (se + h[j] >= k) {  // the bin of the k-th key (exactly one)
-          s_kend = (uint32_t)(se + h[j]);
-          s_nb = (uint32_t)bucket + 1u;
+        bucket = (int32_t)(se / kBucketHalf + above + (big ? 1u : 0u));
+        if ((uint32_t)bucket >= nbmax || h[j] > (uint32_t)kBucketPad) {
+          s_over = 1u;  // (never: the slots cover every big bin) / a bin the bucket sort cannot hold
+          bucket = -1;
+        } else {
+          atomicMin(&s_bs[bucket], (uint32_t)se);
+          atomicAdd(&s_b[bucket], h[j]);  // the bucket's key count (s_b is zeroed again below)
+          if (se + h[j] >= k) {  // the bin of the k-th key (exactly one)
+            s_kend = (uint32_t)(se + h[j]);
+            s_nb = (uint32_t)bucket + 1u;
+          }
         }
       }
       if (i < F) s_fb[i] = (int16_t)bucket;
       se += h[j];
+      above += big ? 1u : 0u;
     }
   }
   __syncthreads();
@@ -1654,10 +1678,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const uint32_t nb = s_nb;
     for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) {
       uint32_t st = 0, c = 0;
-      if (!redo && j < nb && s_bs[j] != 0xffffffffu) {
+      if (!skip && j < nb && s_bs[j] != 0xffffffffu) {
         st = s_bs[j];
-        const uint32_t en = j + 1 < nb ? s_bs[j + 1] : s_kend;
-        c = en > st ? en - st : 0u;
+        c = s_b[j];
       }
       brec[b0 + j] = BucketRec{(uint64_t)kb2[t] + st, st, min(c, 0xffffu) | ((uint32_t)t << 16)};
     }
@@ -1682,6 +1705,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     }
   }
   if (skip) return;
+  for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) s_b[j] = 0;  // this block's per-bucket counts next
+  __syncthreads();
   // ---- the scatter (topk_bucket_scatter<true> with the LDS plan)
   const uint32_t* map_t = s_map;
   uint64_t* dst = bkeys + kb2[t];
@@ -2469,7 +2494,7 @@ struct WsLayout {
 // Bucket-table slots for any ratio (k <= n).
 size_t bucket_slots_max(const omf_plan* p) {
   size_t nb = 0;
-  for (int64_t n : omf_plan_access::sizes(p)) nb += (size_t)((n + kBucketHalf) / kBucketHalf + 1);
+  for (int64_t n : omf_plan_access::sizes(p)) nb += (size_t)bucket_slots(n);
   return nb;
 }
 
@@ -2519,8 +2544,8 @@ WsLayout layout_uncached(const omf_plan* p) {
   L.item_cnt = o; o = align256(o + 4 * (size_t)n_items);
   L.item_off = o; o = align256(o + 4 * (size_t)n_items);
   L.cand = o; o = align256(o + 8 * (size_t)ae);
-  // the fallback's packed keys, or the fast path's buckets (k_t + kBucketHalf per tensor)
-  L.sorted = o; o = align256(o + 8 * ((size_t)ae + (size_t)nt * kBucketHalf));
+  // the fallback's packed keys, or the fast path's buckets (k_t + kBucketPad per tensor)
+  L.sorted = o; o = align256(o + 8 * ((size_t)ae + (size_t)nt * kBucketPad));
   L.bbase = o; o = align256(o + 4 * (size_t)(nt + 1));
   L.sbase = o; o = align256(o + 4 * (size_t)(nt + 1));
   L.kb2 = o; o = align256(o + 8 * (size_t)nt);
