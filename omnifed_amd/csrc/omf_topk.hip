@@ -156,6 +156,29 @@ __device__ __forceinline__ uint32_t block_scan_incl(uint32_t v, uint32_t* s_w, u
   return v + pre;
 }
 
+// block_scan_incl for 64-bit values (two 32-bit fields scanned at once, one barrier pair).
+template <int NT>
+__device__ __forceinline__ uint64_t block_scan_incl64(uint64_t v, uint64_t* s_w, uint64_t& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t u = __shfl_up(v, d, 64);
+    if (lane >= d) v += u;
+  }
+  __syncthreads();
+  if (lane == 63) s_w[w] = v;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) {
+    const uint64_t x = s_w[i];
+    pre += i < w ? x : 0u;
+    tot += x;
+  }
+  total = tot;
+  return v + pre;
+}
+
 // t' of one element: MODE 0/2: alpha * x ; MODE 1: r + alpha * x (the reference's order).
 template <int MODE>
 __device__ __forceinline__ float tprime(float x, float r, float alpha) {
@@ -1605,6 +1628,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   __shared__ int64_t s_ibeg[kSupItems];
   __shared__ uint32_t s_map[kCoarse];
   __shared__ uint32_t s_kend, s_nb, s_over;
+  __shared__ uint64_t s_w64[16];
   SupView v{s_spre, s_ibeg, 0, 0, false};
   v.init(supinfo, items, sub_cnt, fmap, s_map, s_part, sup0 + blockIdx.x);
   const int t = v.t;
@@ -1613,12 +1637,15 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   // ---- the plan (topk_plan_tensor's rule)
   constexpr int PER = kFineMax / 1024;
   const uint32_t* ht = fhist + (size_t)t * kFineMax;
-  uint32_t h[PER], loc = 0;
+  // (the counts are read twice — here for the scan, then in the bucket loop — so that they do not
+  // hold 16 registers across the scan's barriers: the scatter below is at the 64-VGPR limit)
+  uint32_t loc = 0, my_big = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const uint32_t i = PER * threadIdx.x + j;
-    h[j] = i < F ? ht[i] : 0u;
-    loc += h[j];
+    const uint32_t hj = i < F ? ht[i] : 0u;
+    loc += hj;
+    my_big += hj > (uint32_t)kBucketHalf ? 1u : 0u;
   }
   if (threadIdx.x == 0) {
     s_kend = 0;
@@ -1629,25 +1656,31 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     s_bs[j] = 0xffffffffu;
     s_b[j] = 0;
   }
-  uint32_t tot32, big_tot;
-  const uint32_t inc = block_scan_incl<1024>(loc, s_part, tot32);  // begins with a barrier
   // Big fine bins (> kBucketHalf keys, up to 2 kBucketHalf) get a bucket of their own: bin i goes to
   // bucket floor(se_i / kBucketHalf) + B_i + big_i, B_i = big bins above it, so every other bucket
   // still holds the bins whose rank starts fall in one kBucketHalf window (<= 2 kBucketHalf keys)
   // and a big bin's bucket holds it alone.  Only a bin of more than 2 kBucketHalf keys (one
   // magnitude key shared that widely, a cluster the fine bins cannot split) takes the fallback.
-  uint32_t my_big = 0;
-#pragma unroll
-  for (int j = 0; j < PER; ++j) my_big += h[j] > (uint32_t)kBucketHalf ? 1u : 0u;
-  const uint32_t big_inc = block_scan_incl<1024>(my_big, s_part, big_tot);
+  // One scan carries the key counts (low word) and the big-bin counts (high word).
+  uint64_t tot64;
+  const uint64_t inc64 =
+      block_scan_incl64<1024>((uint64_t)loc | ((uint64_t)my_big << 32), s_w64, tot64);
+  const uint32_t inc = (uint32_t)inc64, tot32 = (uint32_t)tot64;
+  const uint32_t big_inc = (uint32_t)(inc64 >> 32), big_tot = (uint32_t)(tot64 >> 32);
   const bool zero_mode = tkey[t] == 1u;
-  uint64_t k = (uint64_t)kk[t];
+  uint32_t k = (uint32_t)kk[t];  // (k <= n <= 2^25)
   const bool redo = tot32 < k && !zero_mode;  // the sampled threshold was too high: exact redo
   const bool zero_fill = tot32 < k && zero_mode;  // every candidate selected, then zeros
   if (zero_fill) k = tot32;
   if (!redo) {
-    uint64_t se = tot32 - inc;          // keys in the bins of higher threads
+    uint32_t se = tot32 - inc;          // keys in the bins of higher threads
     uint32_t above = big_tot - big_inc;  // big bins of higher threads
+    uint32_t h[PER];
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const uint32_t i = PER * threadIdx.x + j;
+      h[j] = i < F ? ht[i] : 0u;
+    }
 #pragma unroll
     for (int j = PER - 1; j >= 0; --j) {
       const uint32_t i = PER * threadIdx.x + j;
@@ -1659,10 +1692,10 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
           s_over = 1u;  // (never: the slots cover every big bin) / a bin the bucket sort cannot hold
           bucket = -1;
         } else {
-          atomicMin(&s_bs[bucket], (uint32_t)se);
-          atomicAdd(&s_b[bucket], h[j]);  // the bucket's key count (s_b is zeroed again below)
+          atomicMin(&s_bs[bucket], se);
+          if (v.first) atomicAdd(&s_b[bucket], h[j]);  // the bucket's key count, for its record
           if (se + h[j] >= k) {  // the bin of the k-th key (exactly one)
-            s_kend = (uint32_t)(se + h[j]);
+            s_kend = se + h[j];
             s_nb = (uint32_t)bucket + 1u;
           }
         }
@@ -1685,6 +1718,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       brec[b0 + j] = BucketRec{(uint64_t)kb2[t] + st, st, min(c, 0xffffu) | ((uint32_t)t << 16)};
     }
     __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) s_b[j] = 0;  // this block's per-bucket counts next
     if (threadIdx.x == 0) {
       flag[t] = redo ? 1u : 0u;
       zcnt[t] = zero_fill ? tot32 : kNoZeroFill;
@@ -1705,8 +1739,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     }
   }
   if (skip) return;
-  for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) s_b[j] = 0;  // this block's per-bucket counts next
-  __syncthreads();
+  if (v.first) __syncthreads();  // (its s_b cleared)
   // ---- the scatter (topk_bucket_scatter<true> with the LDS plan)
   const uint32_t* map_t = s_map;
   uint64_t* dst = bkeys + kb2[t];

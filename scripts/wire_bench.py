@@ -54,6 +54,15 @@ def tm(fn, reps=7, warm=3):
     return round(sorted(ts)[len(ts) // 2] * 1e3, 2)
 
 
+TK_ORDER = "index"  # the Top-K legs time the device order; "topk_torch_order" below the reference's
+
+
+def topk_comp(**kw):
+    c = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev, **kw)
+    c.tie_order = TK_ORDER
+    return c
+
+
 def leg(comp, tag):
     """The wire legs of one compressor; returns a dict of medians (ms) and rates."""
     r = {}
@@ -72,7 +81,8 @@ def leg(comp, tag):
     r["agg_accumulate_layers_ms"] = tm(lambda: agg.accumulate_layers(layers, number_samples=1))
     # GetUpdatedModel: the server's compressor re-encodes the average (apply_and_encode).  A dense
     # accumulator (QSGD decodes are dense; a Top-K average over many clients' updates):
-    srv = build_global_compressor(enabled=True, scheme=tag, bit_width=4, compress_ratio=0.01, device=dev)
+    srv = (topk_comp() if tag == "topk" else
+           build_global_compressor(enabled=True, scheme=tag, bit_width=4, compress_ratio=0.01, device=dev))
     agg.acc.copy_(torch.randn(agg.acc.numel(), device=dev, generator=g) * 4e-2)
     agg.total_samples = 40
     r["ps_apply_and_encode_dense_ms"] = tm(lambda: agg.apply_and_encode(srv, total_samples=40))
@@ -89,7 +99,7 @@ def leg(comp, tag):
         for label, noise in (("overlap", 0.05), ("disjoint", None)):
             agg2 = DeviceAggregator(named, device=dev)
             for c in range(2):
-                cc = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+                cc = topk_comp()
                 if noise is None:  # disjoint: independent gradients
                     u = upd if c == 0 else {n: torch.randn(t.shape, device=dev, generator=g) * 1e-3
                                             for n, t in upd.items()}
@@ -100,7 +110,7 @@ def leg(comp, tag):
                 agg2.accumulate_layers(encode_updates_dict(u, cc), number_samples=1)
                 del u, cc
             nnz = int((agg2.acc != 0).sum())
-            srv2 = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+            srv2 = topk_comp()
             plan_t.topk_stats(reset=True)
             r[f"ps_apply_and_encode_sparse_{label}_ms"] = tm(lambda: agg2.apply_and_encode(srv2, total_samples=2))
             r[f"sparse_{label}_nnz_per_k"] = round(nnz / sum(plan_t.topk_ks(0.01)), 3)
@@ -120,22 +130,37 @@ def leg(comp, tag):
 res = {"config": cfg, "elements": N, "tensors": len(named), "copy_threads": hostio.workers()}
 qcomp = build_global_compressor(enabled=True, scheme="qsgd", bit_width=4, device=dev)
 res["qsgd_s4"], layers = leg(qcomp, "qsgd")
-tcomp = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+tcomp = topk_comp()
 res["topk_1pct"], tlayers = leg(tcomp, "topk")
 progress("per-layer Top-K loop, copy threads, device-side steps")
 # the round-3 per-layer Top-K loop (one encode + host wait + small D2H per tensor), for comparison
-tper = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+tper = topk_comp()
 res["topk_1pct"]["per_layer_encode_ms"] = tm(lambda: [encode_layer_state(n, t, tper) for n, t in upd.items()],
                                              reps=3, warm=1)
 # an fp16 model's update (the reference's default scheme on a half-precision model): one batched
 # selection launch over the dict, residuals in fp16 (round 4), against the per-layer loop
 upd16 = {n: t.half() for n, t in upd.items()}
-t16 = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+t16 = topk_comp()
 res["topk_1pct"]["fp16_encode_updates_dict_ms"] = tm(lambda: encode_updates_dict(upd16, t16), reps=5, warm=2)
-t16p = build_global_compressor(enabled=True, scheme="topk", compress_ratio=0.01, device=dev)
+t16p = topk_comp()
 res["topk_1pct"]["fp16_per_layer_encode_ms"] = tm(lambda: [encode_layer_state(n, t, t16p) for n, t in upd16.items()],
                                                   reps=3, warm=1)
 del upd16, t16, t16p
+# the drop-in's default Top-K order (tie_order="torch": the reference's bytes where magnitudes tie,
+# omf_topk_torch_order's host rewrite of the tied tensors) on the client encode and the PS re-encode
+progress("Top-K in torch order")
+TK_ORDER = "torch"
+ttc = topk_comp()
+res["topk_torch_order"] = {"encode_updates_dict_ms": tm(lambda: encode_updates_dict(upd, ttc), reps=3, warm=1)}
+plan_tt = codec.Plan.get([t.numel() for t in upd.values()], device=dev)
+res["topk_torch_order"]["tensors_rewritten"] = plan_tt.topk_reordered
+agg_t = DeviceAggregator(named, device=dev)
+agg_t.accumulate_layers(encode_updates_dict(upd, topk_comp()), number_samples=1)
+srv_t = topk_comp()
+res["topk_torch_order"]["ps_apply_and_encode_sparse_ms"] = tm(lambda: agg_t.apply_and_encode(srv_t, total_samples=1),
+                                                              reps=3, warm=1)
+TK_ORDER = "index"
+del ttc, agg_t, srv_t
 # the host copies on the calling thread vs worker threads (hostio.set_workers), same process
 res["by_copy_threads"] = {}
 for nthr in (0, 2, 4, 8):
