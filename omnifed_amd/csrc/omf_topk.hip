@@ -98,6 +98,7 @@ constexpr int kPlanMaxBuckets = (1 << 25) / kBucketHalf + 2;  // topk_plan's rul
 // A tensor's bucket-key region: k + kBucketPad keys (the k-th key's bin may run past rank k by up to
 // one bucket's worth: a fine bin of up to 2 kBucketHalf keys sits in a bucket of its own).
 constexpr int kBucketPad = 2 * kBucketHalf;
+constexpr int kMaxBigBins = 128;  // kept fine bins over kBucketHalf keys per tensor on the fast path
 #ifndef OMF_TK_SUBPER  // experiment builds may override it
 #define OMF_TK_SUBPER 512
 #endif
@@ -149,29 +150,6 @@ __device__ __forceinline__ uint32_t block_scan_incl(uint32_t v, uint32_t* s_w, u
 #pragma unroll
   for (int i = 0; i < NT / 64; ++i) {
     const uint32_t x = s_w[i];
-    pre += i < w ? x : 0u;
-    tot += x;
-  }
-  total = tot;
-  return v + pre;
-}
-
-// block_scan_incl for 64-bit values (two 32-bit fields scanned at once, one barrier pair).
-template <int NT>
-__device__ __forceinline__ uint64_t block_scan_incl64(uint64_t v, uint64_t* s_w, uint64_t& total) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t u = __shfl_up(v, d, 64);
-    if (lane >= d) v += u;
-  }
-  __syncthreads();
-  if (lane == 63) s_w[w] = v;
-  __syncthreads();
-  uint64_t pre = 0, tot = 0;
-#pragma unroll
-  for (int i = 0; i < NT / 64; ++i) {
-    const uint64_t x = s_w[i];
     pre += i < w ? x : 0u;
     tot += x;
   }
@@ -1627,8 +1605,8 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   __shared__ uint32_t s_spre[1025], s_part[1024];
   __shared__ int64_t s_ibeg[kSupItems];
   __shared__ uint32_t s_map[kCoarse];
-  __shared__ uint32_t s_kend, s_nb, s_over;
-  __shared__ uint64_t s_w64[16];
+  __shared__ uint32_t s_kend, s_nb, s_over, s_nbig;
+  __shared__ uint32_t s_big[kMaxBigBins];    // first ranks of the kept big fine bins
   SupView v{s_spre, s_ibeg, 0, 0, false};
   v.init(supinfo, items, sub_cnt, fmap, s_map, s_part, sup0 + blockIdx.x);
   const int t = v.t;
@@ -1637,59 +1615,62 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   // ---- the plan (topk_plan_tensor's rule)
   constexpr int PER = kFineMax / 1024;
   const uint32_t* ht = fhist + (size_t)t * kFineMax;
-  // (the counts are read twice — here for the scan, then in the bucket loop — so that they do not
-  // hold 16 registers across the scan's barriers: the scatter below is at the 64-VGPR limit)
-  uint32_t loc = 0, my_big = 0;
+  uint32_t h[PER], loc = 0;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
     const uint32_t i = PER * threadIdx.x + j;
-    const uint32_t hj = i < F ? ht[i] : 0u;
-    loc += hj;
-    my_big += hj > (uint32_t)kBucketHalf ? 1u : 0u;
+    h[j] = i < F ? ht[i] : 0u;
+    loc += h[j];
   }
   if (threadIdx.x == 0) {
     s_kend = 0;
     s_nb = 0;
     s_over = 0;
+    s_nbig = 0;
   }
   for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) {
     s_bs[j] = 0xffffffffu;
     s_b[j] = 0;
   }
-  // Big fine bins (> kBucketHalf keys, up to 2 kBucketHalf) get a bucket of their own: bin i goes to
-  // bucket floor(se_i / kBucketHalf) + B_i + big_i, B_i = big bins above it, so every other bucket
-  // still holds the bins whose rank starts fall in one kBucketHalf window (<= 2 kBucketHalf keys)
-  // and a big bin's bucket holds it alone.  Only a bin of more than 2 kBucketHalf keys (one
-  // magnitude key shared that widely, a cluster the fine bins cannot split) takes the fallback.
-  // One scan carries the key counts (low word) and the big-bin counts (high word).
-  uint64_t tot64;
-  const uint64_t inc64 =
-      block_scan_incl64<1024>((uint64_t)loc | ((uint64_t)my_big << 32), s_w64, tot64);
-  const uint32_t inc = (uint32_t)inc64, tot32 = (uint32_t)tot64;
-  const uint32_t big_inc = (uint32_t)(inc64 >> 32), big_tot = (uint32_t)(tot64 >> 32);
+  uint32_t tot32;
+  const uint32_t inc = block_scan_incl<1024>(loc, s_part, tot32);  // begins with a barrier
   const bool zero_mode = tkey[t] == 1u;
   uint32_t k = (uint32_t)kk[t];  // (k <= n <= 2^25)
   const bool redo = tot32 < k && !zero_mode;  // the sampled threshold was too high: exact redo
   const bool zero_fill = tot32 < k && zero_mode;  // every candidate selected, then zeros
   if (zero_fill) k = tot32;
+  // Big fine bins (> kBucketHalf keys, up to 2 kBucketHalf) get a bucket of their own: bin i goes to
+  // bucket floor(se_i / kBucketHalf) + B_i + big_i, B_i = kept big bins above it, so every other
+  // bucket still holds the bins whose rank starts fall in one kBucketHalf window (<= 2 kBucketHalf
+  // keys) and a big bin's bucket holds it alone.  The kept big bins' first ranks go to an LDS list
+  // (rare: usually empty) that each bin counts below its own.  Only a bin of more than 2 kBucketHalf
+  // keys (one magnitude key shared that widely, a cluster the fine bins cannot split), or more than
+  // kMaxBigBins of them, takes the fallback.
   if (!redo) {
-    uint32_t se = tot32 - inc;          // keys in the bins of higher threads
-    uint32_t above = big_tot - big_inc;  // big bins of higher threads
-    uint32_t h[PER];
+    uint32_t se = tot32 - inc;  // keys in the bins of higher threads
 #pragma unroll
-    for (int j = 0; j < PER; ++j) {
-      const uint32_t i = PER * threadIdx.x + j;
-      h[j] = i < F ? ht[i] : 0u;
+    for (int j = PER - 1; j >= 0; --j) {
+      if (h[j] > (uint32_t)kBucketHalf && se < k) {
+        const uint32_t q = atomicAdd(&s_nbig, 1u);
+        if (q < (uint32_t)kMaxBigBins) s_big[q] = se;
+      }
+      se += h[j];
     }
+  }
+  __syncthreads();
+  const uint32_t nbig = s_nbig;
+  if (!redo) {
+    uint32_t se = tot32 - inc;
 #pragma unroll
     for (int j = PER - 1; j >= 0; --j) {
       const uint32_t i = PER * threadIdx.x + j;
       int32_t bucket = -1;
-      const bool big = h[j] > (uint32_t)kBucketHalf;
       if (h[j] && se < k) {
-        bucket = (int32_t)(se / kBucketHalf + above + (big ? 1u : 0u));
-        if ((uint32_t)bucket >= nbmax || h[j] > (uint32_t)kBucketPad) {
-          s_over = 1u;  // (never: the slots cover every big bin) / a bin the bucket sort cannot hold
+        uint32_t above = 0;
+        for (uint32_t q = 0; q < min(nbig, (uint32_t)kMaxBigBins); ++q) above += s_big[q] < se ? 1u : 0u;
+        bucket = (int32_t)(se / kBucketHalf + above + (h[j] > (uint32_t)kBucketHalf ? 1u : 0u));
+        if (nbig > (uint32_t)kMaxBigBins || (uint32_t)bucket >= nbmax || h[j] > (uint32_t)kBucketPad) {
+          s_over = 1u;  // a bin the bucket sort cannot hold (or too many big ones)
           bucket = -1;
         } else {
           atomicMin(&s_bs[bucket], se);
@@ -1702,7 +1683,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       }
       if (i < F) s_fb[i] = (int16_t)bucket;
       se += h[j];
-      above += big ? 1u : 0u;
     }
   }
   __syncthreads();
