@@ -118,6 +118,84 @@ def run_round(r18, device, compressor_factory=None):
     return server_model, servicer, out
 
 
+class Turns:
+    """Serialises one phase of the clients in a fixed order (the reference's server state depends
+    on the order of its requests: arrival order of the sum, and a Top-K server compressor's error
+    feedback shared by the GetUpdatedModel requests)."""
+
+    def __init__(self, n):
+        self.n, self.next = n, 0
+        self.cv = threading.Condition()
+
+    def wait(self, c, timeout=120):
+        with self.cv:
+            if not self.cv.wait_for(lambda: self.next % self.n == c, timeout):
+                raise TimeoutError(f"client {c} never got its turn")
+
+    def done(self):
+        with self.cv:
+            self.next += 1
+            self.cv.notify_all()
+
+
+def run_rounds(named, updates, samples, device, client_comp, server_comp=None, rounds=1):
+    """``rounds`` rounds of ``len(samples)`` clients over a loopback gRPC server.  ``updates[r][c]``:
+    client c's update dict of round r (sent as is, with ``number_samples = samples[c]``);
+    ``client_comp()`` builds a client's compressor, ``server_comp`` is the servicer's (None:
+    dense downlink).  Uplinks and downlinks run in client order (Turns).  Returns per round the
+    server's parameters and each client's parameters after its downlink (CPU copies)."""
+    import grpc
+
+    from omnifed_amd.hybrid.communicator.global_grpc_client import GrpcClient
+    from omnifed_amd.hybrid.communicator.global_grpc_limits import GRPC_OPTIONS
+    from omnifed_amd.hybrid.communicator.global_grpc_pb2_grpc import add_CentralServerServicer_to_server
+    from omnifed_amd.hybrid.communicator.global_grpc_server import CentralServerServicer
+
+    C = len(samples)
+    server_model = nested_model(named, device)
+    servicer = CentralServerServicer(num_clients=C, model=server_model, compressor=server_comp, device=device)
+    server = grpc.server(futures.ThreadPoolExecutor(max_workers=10), options=GRPC_OPTIONS)
+    add_CentralServerServicer_to_server(servicer, server)
+    port = server.add_insecure_port("127.0.0.1:0")
+    server.start()
+    up, down = Turns(C), Turns(C)
+    out = {"server": [None] * rounds, "clients": [[None] * C for _ in range(rounds)]}
+    lock = threading.Lock()
+    errors = []
+
+    def client(c):
+        try:
+            model = nested_model(named, device)
+            cl = GrpcClient(client_id=f"client_{c + 1}", master_addr="127.0.0.1", master_port=port,
+                            compressor=client_comp())
+            for r in range(rounds):
+                up.wait(c)
+                ok = cl.send_update_to_server(updates[r][c], samples[c])
+                up.done()
+                assert ok, "SendUpdate failed"
+                down.wait(c)
+                cl.get_averaged_model(model, communicate_params=True, max_polls=20)
+                with lock:
+                    if out["server"][r] is None:
+                        out["server"][r] = {n: p.data.detach().cpu().clone() for n, p in server_model.named_parameters()}
+                out["clients"][r][c] = {n: p.data.detach().cpu().clone() for n, p in model.named_parameters()}
+                down.done()
+                cl.round_number += 1
+            cl.channel.close()
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=client, args=(c,)) for c in range(C)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(600)
+    server.stop(grace=1)
+    if errors:
+        raise RuntimeError("; ".join(errors))
+    return out, servicer
+
+
 def main():
     dev = torch.device("cuda", 0)
     with open(os.path.join(ROOT, "tests", "golden", "golden_r2_index.json")) as f:
