@@ -293,9 +293,8 @@ def settle(torch, step, seconds=SETTLE_S):
 
 def event_ms(torch, st, fn, reps):
     """Mean duration of ``fn`` (its launches on stream ``st``) in a back-to-back loop, from two
-    HIP events recorded on ``st`` around ``reps`` calls (the steady-state launch duration;
-    per-call event pairs would also count the host's part of a call that waits mid-way, as
-    the Top-K encoder does for its verdict)."""
+    HIP events recorded on ``st`` around ``reps`` calls (the steady-state launch duration of
+    calls queued back to back)."""
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn(0)  # one untimed call: the loop starts in steady state
     a.record(st)
@@ -457,7 +456,7 @@ def main():
                 "algorithmic_bytes_per_step_per_client": alg_t,
                 "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": t_traffic, "traffic_source": t_tsrc,
-                             "kernel": "omf_topk_encode (all launches of one call, host sync included)",
+                             "kernel": "omf_topk_encode (all launches of one call; stream-asynchronous, no host wait)",
                              "algorithmic_bytes_per_launch": enc_alg, "avg_launch_ms": round(tenc, 4),
                              "decode_ms": round(tdec, 4)},
                 "encoder_paths": plan.topk_stats(),  # timed calls: bucket-sort fast path vs fallbacks

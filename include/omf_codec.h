@@ -14,11 +14,11 @@
  *    The library allocates only in omf_plan_create (its own workspace) and, once per
  *    (plan, Top-K ratio), a small constant table on the first Top-K call at that ratio
  *    (synchronous, not on the hot path after that).  The hot-path calls never allocate or
- *    copy host memory, and never synchronise — except omf_topk_encode, which waits once
- *    per call for its plan kernel's verdict (a 16-byte word the GPU writes into mapped host
- *    memory; the launches that follow it are already queued), omf_topk_torch_order (host
- *    work on the tied tensors), and omf_plan_check / omf_plan_spec_stats, which exist to
- *    synchronise.
+ *    copy host memory, and never synchronise — except omf_topk_torch_order (host work on
+ *    the tied tensors) and omf_plan_check / omf_plan_spec_stats / omf_topk_stats, which exist
+ *    to synchronise.  Since ABI 1.11 omf_topk_encode is stream-asynchronous too (its fallback
+ *    is decided and run on the device) and may be captured into a HIP graph after its first
+ *    call at a ratio.
  *  - `stream` is a hipStream_t (NULL = the legacy default stream).  Calls are
  *    asynchronous on that stream; results are ready when the stream is.
  *  - Return value: 0 (OMF_OK) or a negative OMF_E* code; the message for the
@@ -63,7 +63,7 @@ extern "C" {
 typedef struct omf_plan omf_plan;
 
 /* ABI version (major*100 + minor). */
-#define OMF_ABI_VERSION 110
+#define OMF_ABI_VERSION 111
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -263,18 +263,22 @@ int omf_qsgd_decode_packed(omf_plan* plan, const uint32_t* packed, int32_t level
  * Order within a tensor: descending |t'|, ties by ascending index (torch.topk's
  * order for k*64 <= n on the reference CPU path; ties there are unspecified).
  * ws: caller workspace of omf_topk_workspace_bytes(plan, ratio) bytes.
- * Waits once for the plan kernel's verdict (mapped host memory, no stream synchronisation;
- * the bucket kernels are queued before the wait); on the rare fallback verdict (a sampled
- * threshold too high, or an over-full fine bin) it synchronises `stream` once or twice to size
- * the device-wide sort.
+ * Stream-asynchronous: the plan kernel's verdict is read by the launches queued behind it (the
+ * bucket kernels, the zero fill and the exact tail, each leaving at once when the verdict does
+ * not need it); the rare fallback (a sampled threshold too high, or an over-full fine bin) runs
+ * on the device in the exact tail — a grid-barrier kernel, one workgroup per CU, sized by the
+ * device's own candidate count.  A tail barrier that exceeded its bound (never expected) is
+ * reported by omf_plan_check as OMF_ETIMEOUT.  The first call at a ratio builds the plan's
+ * constant tables synchronously (not capturable); later calls launch only.
  */
 int64_t omf_topk_k(int64_t numel, double ratio);
-/* The plan's Top-K encoder counters (diagnostics; no synchronisation): out6[0] calls of the
- * sampled path, [1] of those that took the bucket-sort fast path, [2] of those that completed a
- * tensor with its lowest-index exact zeros (zero mode: fewer than k non-zero t', e.g. the PS
- * re-encoding an average of sparse Top-K updates), [3] calls that took the device-wide
- * radix-sort fallback, [4] of those that redid a tensor exactly, [5] calls of the exact path
- * (plans of > 256 tensors or a tensor over 2^25 elements).  reset != 0 zeroes them after reading. */
+/* The plan's Top-K encoder counters (diagnostics; waits for the device, hipDeviceSynchronize,
+ * since the device counts the path each call took): out6[0] calls of the sampled path, [1] of
+ * those that took the bucket-sort fast path, [2] of those that completed a tensor with its
+ * lowest-index exact zeros (zero mode: fewer than k non-zero t', e.g. the PS re-encoding an
+ * average of sparse Top-K updates), [3] calls that took the exact tail's fallback (device-wide
+ * radix sort), [4] of those that redid a tensor exactly, [5] calls of the exact path (plans of
+ * > 256 tensors or a tensor over 2^25 elements).  reset != 0 zeroes them after reading. */
 int omf_topk_stats(omf_plan* plan, int64_t* out6, int32_t reset);
 size_t omf_topk_workspace_bytes(const omf_plan* plan, double ratio);
 int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t residual_mode, double ratio,

@@ -91,7 +91,7 @@ class CodecError(RuntimeError):
     pass
 
 
-ABI_VERSION = 110  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+ABI_VERSION = 111  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
 
 
 def lib() -> ctypes.CDLL:

@@ -18,14 +18,11 @@ constexpr int kWaves = kThreads / 64;
 // encode call of round 3); the kernels' own completion already releases at device scope.
 constexpr unsigned kOrderEventFlags = hipEventDisableTiming | hipEventDisableSystemFence;
 
-// Top-K encoder counters of a plan (omf_topk_stats): calls of the sampled path, how many took
-// the bucket-sort fast path (of those, how many completed a tensor with exact zeros) and how
-// many the device-wide radix-sort fallback (of those, how many redid a tensor); and the plan's
-// recent launch-to-verdict time, which paces the host's wait (per plan: a small plan's call
-// must not sleep for a large plan's time).
+// Top-K encoder counters of a plan (omf_topk_stats) that the host knows: calls of the sampled
+// path and of the exact path.  Which path a sampled call took (bucket-sort fast path, zero fill,
+// the exact tail's fallback, a redo) is decided on the device, which counts it (omf_topk.hip).
 struct TopkStats {
-  int64_t calls = 0, fast = 0, zero_fill = 0, fallback = 0, redo = 0, exact = 0;
-  double verdict_us = 0.0;
+  int64_t calls = 0, exact = 0;
 };
 
 // Top-K encoder settings of a plan (omf_topk.hip): in experiment builds read from the OMF_TOPK_* environment once, at

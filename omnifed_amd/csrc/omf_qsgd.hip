@@ -1982,6 +1982,8 @@ void* topk_table_counts(omf_plan* p, const int64_t* counts, size_t bytes, bool* 
 }
 const std::vector<int64_t>& offsets(const omf_plan* p) { return p->offsets; }
 omf::TopkKnobs& topk_knobs(omf_plan* p) { return p->topk_knobs; }
+// The plan's device error word (omf_plan_check reports and clears it).
+uint32_t* err_word(omf_plan* p) { return reinterpret_cast<uint32_t*>(p->d_sync + 4); }
 }  // namespace omf_plan_access
 
 static size_t round16(size_t b) { return (b + 15) & ~(size_t)15; }
@@ -2557,6 +2559,9 @@ int omf_plan_check(omf_plan* plan, void* stream) {
     return fail(OMF_ETIMEOUT, "QSGD encoder: an on-chip wait exceeded its bound (a ring hand-off, or a "
                               "bracketed-encoder fix waiting for its tensor's norm) and was abandoned; the "
                               "payload of that launch is invalid");
+  if (err & 8u)
+    return fail(OMF_ETIMEOUT, "Top-K encoder: a grid barrier of the exact tail (the device-side fallback) "
+                              "exceeded its bound and was abandoned; the selection of that call is invalid");
   if (err & 2u) {
     set_error("encoder recomputed a norm after a bounded wait (items not co-resident); results are exact");
     return 1;

@@ -411,7 +411,7 @@ __global__ __launch_bounds__(1024) void topk_sample(const float* __restrict__ x,
 #endif
   const int t = (int)smap[2 * bid];
   const int64_t r0 = smap[2 * bid + 1];
-  if (bid == 0 && threadIdx.x < 4) status[threadIdx.x] = 0u;
+  if (bid == 0 && threadIdx.x < 9) status[threadIdx.x] = 0u;  // the verdict and the exact tail's words
   for (int b = threadIdx.x; b < kSBins; b += 1024) h[b] = 0;
   if (threadIdx.x == 0) s_zero = 0;
   const int64_t base = tbegin[t], n = tsize[t];
@@ -687,38 +687,21 @@ __global__ __launch_bounds__(kSubThreads) void topk_fused(const float* __restric
   if (threadIdx.x == 0) sub_cnt[bid] = total;  // (the fallback sums an item's subs: topk_item_counts)
 }
 
-// Fallback path: each item's candidate count, the sum of its sub-chunks' (one thread per item).
-__global__ __launch_bounds__(kThreads) void topk_item_counts(const uint32_t* __restrict__ sub_cnt, int64_t n_items,
-                                                             uint32_t* __restrict__ item_cnt) {
-  const int64_t i = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n_items) return;
-  const uint4* p = reinterpret_cast<const uint4*>(sub_cnt + i * kSubsPerItem);
-  uint32_t c = 0;
-#pragma unroll
-  for (int j = 0; j < kSubsPerItem / 4; ++j) {
-    const uint4 v = p[j];
-    c += v.x + v.y + v.z + v.w;
-  }
-  item_cnt[i] = c;
-}
-
-// One block: exclusive scan of the per-item candidate counts (items in tensor order) in
-// tiles of 4 Ki items (coalesced loads, an LDS scan, a running carry), then per tensor its
-// candidate count and start; flag the tensors whose threshold was too high.
-// status[0] = all candidates, status[1] = any flagged.
-__global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_t* __restrict__ kk,
-                                                        const uint32_t* __restrict__ tfirst,
-                                                        const uint32_t* __restrict__ tlast,
-                                                        const uint32_t* __restrict__ item_cnt,
-                                                        uint32_t* __restrict__ item_off, int64_t n_items,
-                                                        int64_t* __restrict__ cstart, uint32_t* __restrict__ cnt,
-                                                        uint32_t* __restrict__ flag, uint32_t* __restrict__ status) {
-  __shared__ uint32_t part[1024];
+// Exact tail, one block (kThreads): exclusive scan of the per-item candidate counts (items in
+// tensor order) in tiles of 1 Ki items (coalesced loads, an LDS scan, a running carry), then per
+// tensor its candidate count and start; flag the tensors whose threshold was too high.
+// out[0] = all candidates, out[1] = any flagged (agent-scope stores: other blocks read them
+// after the tail's grid barrier).
+__device__ void scan_check_block(int32_t nt, const int64_t* __restrict__ kk, const uint32_t* __restrict__ tfirst,
+                                 const uint32_t* __restrict__ tlast, const uint32_t* __restrict__ item_cnt,
+                                 uint32_t* __restrict__ item_off, int64_t n_items, int64_t* __restrict__ cstart,
+                                 uint32_t* __restrict__ cnt, uint32_t* __restrict__ flag, uint32_t* out) {
+  __shared__ uint32_t part[kWaves];
   __shared__ uint32_t s_any;
   const int t = threadIdx.x;
   if (t == 0) s_any = 0;
   uint32_t carry = 0;
-  for (int64_t t0 = 0; t0 < n_items; t0 += 4096) {
+  for (int64_t t0 = 0; t0 < n_items; t0 += 4 * kThreads) {
     uint32_t c[4], loc = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {  // items t0 + 4t + j
@@ -727,7 +710,7 @@ __global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_
       loc += c[j];
     }
     uint32_t tot;
-    const uint32_t inc = block_scan_incl<1024>(loc, part, tot);
+    const uint32_t inc = block_scan_incl<kThreads>(loc, part, tot);
     uint32_t run = carry + inc - loc;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -739,7 +722,7 @@ __global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_
   }
   __threadfence_block();
   __syncthreads();  // item_off of every item visible to the block
-  for (int32_t q = t; q < nt; q += 1024) {
+  for (int32_t q = t; q < nt; q += kThreads) {
     const uint32_t f = tfirst[q], l = tlast[q];
     const uint32_t of = item_off[f];
     const uint32_t c = item_off[l] + item_cnt[l] - of;
@@ -751,8 +734,8 @@ __global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_
   }
   __syncthreads();
   if (t == 0) {
-    status[0] = carry;
-    status[1] = s_any;
+    __hip_atomic_store(&out[0], carry, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&out[1], s_any, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -760,12 +743,11 @@ __global__ __launch_bounds__(1024) void topk_scan_check(int32_t nt, const int64_
 // MODE as topk_fused.  flag != null: only the flagged tensors (a redo reads t' as x with
 // MODE 0 and alpha = the scale of t').
 template <int MODE>
-__global__ __launch_bounds__(kThreads) void topk_prep_hist(const float* __restrict__ x, float* __restrict__ r,
-                                                           float alpha, const Item* __restrict__ items,
-                                                           const uint32_t* __restrict__ flag,
-                                                           uint32_t* __restrict__ hist) {
+__device__ void prep_hist_item(const float* __restrict__ x, float* __restrict__ r, float alpha,
+                               const Item* __restrict__ items, const uint32_t* __restrict__ flag,
+                               uint32_t* __restrict__ hist, int64_t item) {
   __shared__ uint32_t h[kBins];
-  const Item it = items[blockIdx.x];
+  const Item it = items[item];
   if (flag && !flag[it.tensor]) return;  // block-uniform
   for (int b = threadIdx.x; b < kBins; b += kThreads) h[b] = 0;
   __syncthreads();
@@ -801,14 +783,17 @@ __global__ __launch_bounds__(kThreads) void topk_prep_hist(const float* __restri
   for (int b = threadIdx.x; b < kBins; b += kThreads)
     if (h[b]) atomicAdd(&ht[b], h[b]);
 }
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void topk_prep_hist(const float* __restrict__ x, float* __restrict__ r,
+                                                           float alpha, const Item* __restrict__ items,
+                                                           uint32_t* __restrict__ hist) {
+  prep_hist_item<MODE>(x, r, alpha, items, nullptr, hist, blockIdx.x);
+}
 
 // One block per tensor: b1 = max bin with suffix count >= k (flag: only flagged tensors).
-__global__ __launch_bounds__(kThreads) void topk_select_bin(const uint32_t* __restrict__ hist,
-                                                            const int64_t* __restrict__ kk,
-                                                            const uint32_t* __restrict__ flag,
-                                                            uint32_t* __restrict__ bin) {
+__device__ void select_bin_tensor(const uint32_t* __restrict__ hist, const int64_t* __restrict__ kk,
+                                  const uint32_t* __restrict__ flag, uint32_t* __restrict__ bin, int t) {
   __shared__ uint32_t s_part[kThreads];
-  const int t = blockIdx.x;
   if (flag && !flag[t]) return;
   const uint32_t* ht = hist + (size_t)t * kBins;
   // thread i owns bins [4i, 4i+4); suffix sums over threads from the top.
@@ -830,6 +815,10 @@ __global__ __launch_bounds__(kThreads) void topk_select_bin(const uint32_t* __re
     above += c[j];
   }
 }
+__global__ __launch_bounds__(kThreads) void topk_select_bin(const uint32_t* __restrict__ hist,
+                                                            const int64_t* __restrict__ kk, uint32_t* __restrict__ bin) {
+  select_bin_tensor(hist, kk, nullptr, bin, blockIdx.x);
+}
 
 // Segment bounds of the exact path's per-tensor sort.
 __global__ void topk_segments(int32_t nt, const int64_t* __restrict__ tbegin, const uint32_t* __restrict__ cnt,
@@ -845,16 +834,14 @@ __global__ void topk_segments(int32_t nt, const int64_t* __restrict__ tbegin, co
 // tensors only).  Otherwise (|t'|bits << 32 | ~index) appended to the tensor's region
 // through one atomic per block pass.
 template <bool GLOBAL>
-__global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict__ tp, float scale,
-                                                         const Item* __restrict__ items,
-                                                         const int64_t* __restrict__ tbegin,
-                                                         const uint32_t* __restrict__ bin,
-                                                         const uint32_t* __restrict__ flag, uint32_t* __restrict__ cnt,
-                                                         uint32_t* __restrict__ sub_cnt, uint32_t* __restrict__ item_cnt,
-                                                         uint64_t* __restrict__ cand) {
+__device__ void collect_item(const float* __restrict__ tp, float scale, const Item* __restrict__ items,
+                             const int64_t* __restrict__ tbegin, const uint32_t* __restrict__ bin,
+                             const uint32_t* __restrict__ flag, uint32_t* __restrict__ cnt,
+                             uint32_t* __restrict__ sub_cnt, uint32_t* __restrict__ item_cnt,
+                             uint64_t* __restrict__ cand, int64_t item) {
   __shared__ uint32_t s_wsum[4 * kWaves];
   __shared__ uint32_t s_base;
-  const Item it = items[blockIdx.x];
+  const Item it = items[item];
   if (flag && !flag[it.tensor]) return;  // block-uniform
   const uint32_t b1 = bin[it.tensor];
   const int64_t base = tbegin[it.tensor];
@@ -925,8 +912,15 @@ __global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict
     __syncthreads();  // s_wsum / s_base reuse
   }
   if (GLOBAL && threadIdx.x < kSubsPerItem)  // the item's candidates as one run (sub 0)
-    sub_cnt[(size_t)blockIdx.x * kSubsPerItem + threadIdx.x] = threadIdx.x == 0 ? item_total : 0u;
-  if (GLOBAL && threadIdx.x == 0) item_cnt[blockIdx.x] = item_total;
+    sub_cnt[(size_t)item * kSubsPerItem + threadIdx.x] = threadIdx.x == 0 ? item_total : 0u;
+  if (GLOBAL && threadIdx.x == 0) item_cnt[item] = item_total;
+}
+__global__ __launch_bounds__(kThreads) void topk_collect(const float* __restrict__ tp, float scale,
+                                                         const Item* __restrict__ items,
+                                                         const int64_t* __restrict__ tbegin,
+                                                         const uint32_t* __restrict__ bin, uint32_t* __restrict__ cnt,
+                                                         uint64_t* __restrict__ cand) {
+  collect_item<false>(tp, scale, items, tbegin, bin, nullptr, cnt, nullptr, nullptr, cand, blockIdx.x);
 }
 
 // The kSubsPerItem sub-chunk candidate counts of item `item` -> s_pre[0..32] (exclusive prefix, s_pre[32]
@@ -956,19 +950,17 @@ __device__ __forceinline__ uint64_t item_key(const uint64_t* __restrict__ cand, 
   return cand[begin + (int64_t)j * kSubPer + (e - s_pre[j])];
 }
 
-// Fallback path: pack every item's candidates at its scanned offset, in order, as device-wide
+// Exact tail: pack every item's candidates at its scanned offset, in order, as device-wide
 // sort keys index << 39 | tensor << 31 | (2^31 - 1 - |t'|bits) (a stable sort of the low 39
 // bits gives tensor ascending, |t'| descending, index ascending).
-__global__ __launch_bounds__(kThreads) void topk_compact(const uint64_t* __restrict__ cand,
-                                                         const Item* __restrict__ items,
-                                                         const uint32_t* __restrict__ sub_cnt,
-                                                         const uint32_t* __restrict__ item_off,
-                                                         uint64_t* __restrict__ packed) {
+__device__ void compact_item(const uint64_t* __restrict__ cand, const Item* __restrict__ items,
+                             const uint32_t* __restrict__ sub_cnt, const uint32_t* __restrict__ item_off,
+                             uint64_t* __restrict__ packed, int64_t item) {
   __shared__ uint32_t s_pre[kSubsPerItem + 1];
-  const Item it = items[blockIdx.x];
-  item_prefix(sub_cnt, blockIdx.x, s_pre);
+  const Item it = items[item];
+  item_prefix(sub_cnt, item, s_pre);
   const uint32_t n = s_pre[kSubsPerItem];
-  uint64_t* dst = packed + item_off[blockIdx.x];
+  uint64_t* dst = packed + item_off[item];
   const uint64_t tag = (uint64_t)it.tensor << 31;
   for (uint32_t e = threadIdx.x; e < n; e += kThreads) {
     const uint64_t key = item_key(cand, it.begin, s_pre, e);
@@ -1015,17 +1007,18 @@ struct SupView {
   }
 };
 
-// Fallback path, first step in the EF modes: the residual of every candidate back to t'
-// (the fused pass stored t' - t' there), so the radix-sort path sees the plain t' state.
-__global__ __launch_bounds__(kThreads) void topk_restore(const uint64_t* __restrict__ cand,
-                                                         const Item* __restrict__ items,
-                                                         const uint32_t* __restrict__ sub_cnt,
-                                                         const int64_t* __restrict__ tbegin,
-                                                         float* __restrict__ r) {
+// Exact tail, first step: the item's candidate count (item_cnt) and, in the EF modes, the
+// residual of every candidate back to t' (the fused pass stored t' - t' there), so the exact
+// sort sees the plain t' state.
+__device__ void restore_item(const uint64_t* __restrict__ cand, const Item* __restrict__ items,
+                             const uint32_t* __restrict__ sub_cnt, const int64_t* __restrict__ tbegin,
+                             float* __restrict__ r, uint32_t* __restrict__ item_cnt, int64_t item) {
   __shared__ uint32_t s_pre[kSubsPerItem + 1];
-  const Item it = items[blockIdx.x];
-  item_prefix(sub_cnt, blockIdx.x, s_pre);
+  const Item it = items[item];
+  item_prefix(sub_cnt, item, s_pre);
   const uint32_t n = s_pre[kSubsPerItem];
+  if (threadIdx.x == 0) item_cnt[item] = n;
+  if (!r) return;
   const int64_t base = tbegin[it.tensor];
   for (uint32_t e = threadIdx.x; e < n; e += kThreads) {
     const uint64_t key = item_key(cand, it.begin, s_pre, e);
@@ -1101,28 +1094,11 @@ __global__ __launch_bounds__(1024) void topk_plan(const int64_t* __restrict__ kk
                                                   uint32_t* __restrict__ bfill, const int64_t* __restrict__ kb2,
                                                   uint32_t* __restrict__ flag, uint32_t* __restrict__ status,
                                                   uint32_t* __restrict__ fse, const uint32_t* __restrict__ tkey,
-                                                  uint32_t* __restrict__ zcnt, int dbg, uint32_t* __restrict__ done,
-                                                  uint32_t* host, uint32_t seq, int32_t t0, uint32_t total) {
+                                                  uint32_t* __restrict__ zcnt, int dbg, int32_t t0) {
+  // (the verdict words in status are read by the kernels queued behind: the bucket kernels, the
+  // zero fill and the exact tail — no host round trip)
   topk_plan_tensor((int)(t0 + blockIdx.x), kk, fcount, fhist, bbase, fbucket, bstart, brec, bfill, kb2, flag, status,
                    fse, tkey, zcnt, dbg);
-  // The last block to finish publishes the call's verdict straight into mapped, coherent host
-  // memory (no copy packet in the stream, so the bucket kernels behind this one start at once):
-  // the data words, then the sequence number with release semantics at system scope; the host
-  // spins on it.  Each block's status atomics (thread 0's) complete before its arrival
-  // (vmcnt(0), not a fence: an agent-scope release writes back the whole L2); the last one
-  // reads status with atomic RMWs (performed where the other blocks' atomics were).
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    drain_vmem();
-    if (add_agent(done, 1u) == total - 1) {  // the call's last plan block, over every launch
-      __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t s0 = atomicOr(&status[0], 0u), s1 = atomicOr(&status[1], 0u), s2 = atomicOr(&status[2], 0u);
-      __hip_atomic_store(&host[0], s0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&host[1], s1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&host[2], s2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-  }
 }
 
 __device__ void topk_plan_tensor(int t, const int64_t* __restrict__ kk, const uint32_t* __restrict__ fcount,
@@ -1597,8 +1573,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
     const uint32_t* __restrict__ tkey, const uint32_t* __restrict__ bbase, BucketRec* __restrict__ brec,
     uint32_t* __restrict__ bfill, const int64_t* __restrict__ kb2, const int64_t* __restrict__ tbegin,
     float* __restrict__ r, uint64_t* __restrict__ bkeys, uint32_t* __restrict__ flag, uint32_t* __restrict__ zcnt,
-    uint32_t* __restrict__ status, const uint32_t* __restrict__ thi, uint32_t* __restrict__ done, uint32_t* host,
-    uint32_t seq, uint32_t total_arrivals, uint32_t sup0) {
+    uint32_t* __restrict__ status, const uint32_t* __restrict__ thi, uint32_t sup0) {
   __shared__ uint32_t s_b[kScatterSmallB];   // per bucket: this block's count, then its first slot
   __shared__ uint32_t s_bs[kScatterSmallB];  // per bucket: its first rank in the tensor
   __shared__ int16_t s_fb[kFineMax];         // per fine bin: its bucket (-1: below the k-th key's bin)
@@ -1687,7 +1662,7 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
   }
   __syncthreads();
   const bool skip = redo || s_over != 0u;  // block-uniform
-  if (v.first) {  // the tensor's records, flags and verdict bits; its arrival
+  if (v.first) {  // the tensor's records, flags and verdict bits
     const uint32_t nb = s_nb;
     for (uint32_t j = threadIdx.x; j < nbmax; j += 1024) {
       uint32_t st = 0, c = 0;
@@ -1705,17 +1680,6 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
       if (redo) atomicOr(&status[1], 1u);
       if (!redo && s_over) atomicOr(&status[2], 1u);
       if (zero_fill) atomicOr(&status[0], 1u);
-      // the arrival (as topk_plan): this thread's status atomics performed, then one agent-scope add;
-      // the last of the call's tensors publishes the verdict, the sequence number last (release)
-      drain_vmem();
-      if (add_agent(done, 1u) == total_arrivals - 1) {
-        __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t w0 = atomicOr(&status[0], 0u), w1 = atomicOr(&status[1], 0u), w2 = atomicOr(&status[2], 0u);
-        __hip_atomic_store(&host[0], w0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&host[1], w1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&host[2], w2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(&host[3], seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
     }
   }
   if (skip) return;
@@ -1783,9 +1747,13 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 // (tensor, sub) pairs of the plan-owned table).  A block counts the non-zeros before its sub
 // (the fused pass's per-sub candidate counts: in zero mode exactly the non-zeros), marks its
 // sub's non-zeros from their candidate keys in an LDS bitmap, and ranks its zeros with a block
-// scan; value = t' (the sign of the zero), residual := t' - t' (+0).  Launched only when the
-// plan's verdict reports a zero fill.
-__global__ __launch_bounds__(kSubThreads) void topk_zero_fill(const uint2* __restrict__ zmap,
+// scan; value = t' (the sign of the zero), residual := t' - t' (+0).  Always enqueued (round 6:
+// no host wait for the verdict): a grid of at most kZeroFillGrid blocks strides over the nblk
+// (tensor, sub) pairs and leaves at once unless the plan's verdict (status) reports a zero fill
+// and no fallback.
+constexpr uint32_t kZeroFillGrid = 1024;
+__global__ __launch_bounds__(kSubThreads) void topk_zero_fill(const uint2* __restrict__ zmap, uint32_t nblk,
+                                                           const uint32_t* __restrict__ status,
                                                            const uint32_t* __restrict__ zcnt,
                                                            const int64_t* __restrict__ kk,
                                                            const int64_t* __restrict__ koff,
@@ -1801,85 +1769,87 @@ __global__ __launch_bounds__(kSubThreads) void topk_zero_fill(const uint2* __res
   __shared__ uint32_t s_bm[kSubPer / 32];
   __shared__ uint32_t s_w[kSubWaves];
   __shared__ uint32_t s_sum[kSubWaves];
-  const uint2 zm = zmap[blockIdx.x];
-  const int t = (int)zm.x;
-  const uint32_t x = zm.y;
-  const uint32_t c = zcnt[t];
-  if (c == kNoZeroFill) return;  // block-uniform
-  const int64_t k = kk[t], n = tsize[t], base = tbegin[t];
-  const int64_t rel0 = (int64_t)x * kSubPer;
-  const uint32_t s0 = tfirst[t] * (uint32_t)kSubsPerItem;
-  // non-zeros before this sub
-  uint32_t nz = 0;
-  for (uint32_t j = threadIdx.x; j < x; j += kSubThreads) nz += sub_cnt[s0 + j];
+  if (!status[0] || status[1] || status[2]) return;  // grid-uniform: no zero fill, or a fallback verdict
+  for (uint32_t zb = blockIdx.x; zb < nblk; zb += gridDim.x) {
+    __syncthreads();  // the previous pair's LDS reads are done
+    const uint2 zm = zmap[zb];
+    const int t = (int)zm.x;
+    const uint32_t x = zm.y;
+    const uint32_t c = zcnt[t];
+    if (c == kNoZeroFill) continue;  // block-uniform
+    const int64_t k = kk[t], n = tsize[t], base = tbegin[t];
+    const int64_t rel0 = (int64_t)x * kSubPer;
+    const uint32_t s0 = tfirst[t] * (uint32_t)kSubsPerItem;
+    // non-zeros before this sub
+    uint32_t nz = 0;
+    for (uint32_t j = threadIdx.x; j < x; j += kSubThreads) nz += sub_cnt[s0 + j];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) nz += __shfl_xor(nz, o, 64);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) s_sum[wave] = nz;
-  if (threadIdx.x < kSubPer / 32) s_bm[threadIdx.x] = 0;
-  __syncthreads();
-  uint32_t nzb = 0;
+    for (int o = 32; o > 0; o >>= 1) nz += __shfl_xor(nz, o, 64);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) s_sum[wave] = nz;
+    if (threadIdx.x < kSubPer / 32) s_bm[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t nzb = 0;
 #pragma unroll
-  for (int w2 = 0; w2 < kSubWaves; ++w2) nzb += s_sum[w2];
-  const int64_t z = k - (int64_t)c;                 // zeros to select
-  const int64_t zr0 = rel0 - (int64_t)nzb;          // zeros before this sub
-  if (zr0 >= z) return;                             // block-uniform
-  const uint32_t g = s0 + x;
-  const int64_t b = items[g / kSubsPerItem].begin + (int64_t)(g % kSubsPerItem) * kSubPer;
-  const uint32_t cx = sub_cnt[g];
-  for (uint32_t e = threadIdx.x; e < cx; e += kSubThreads) {
-    const uint32_t rel = (uint32_t)(cand[b + e] >> 32) - (uint32_t)rel0;  // < kSubPer
-    atomicOr(&s_bm[rel >> 5], 1u << (rel & 31));
-  }
-  __syncthreads();
-  const uint32_t o = 4u * threadIdx.x;
-  const uint32_t bits = (s_bm[o >> 5] >> (o & 31)) & 0xFu;
-  uint32_t zmask = 0;
+    for (int w2 = 0; w2 < kSubWaves; ++w2) nzb += s_sum[w2];
+    const int64_t z = k - (int64_t)c;                 // zeros to select
+    const int64_t zr0 = rel0 - (int64_t)nzb;          // zeros before this sub
+    if (zr0 >= z) continue;                           // block-uniform
+    const uint32_t g = s0 + x;
+    const int64_t b = items[g / kSubsPerItem].begin + (int64_t)(g % kSubsPerItem) * kSubPer;
+    const uint32_t cx = sub_cnt[g];
+    for (uint32_t e = threadIdx.x; e < cx; e += kSubThreads) {
+      const uint32_t rel = (uint32_t)(cand[b + e] >> 32) - (uint32_t)rel0;  // < kSubPer
+      atomicOr(&s_bm[rel >> 5], 1u << (rel & 31));
+    }
+    __syncthreads();
+    const uint32_t o = 4u * threadIdx.x;
+    const uint32_t bits = (s_bm[o >> 5] >> (o & 31)) & 0xFu;
+    uint32_t zmask = 0;
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
-    if (rel0 + o + q < n && !((bits >> q) & 1u)) zmask |= 1u << q;
-  const uint32_t mine = (uint32_t)__popc(zmask);
-  uint32_t inc = mine;
+    for (int q = 0; q < 4; ++q)
+      if (rel0 + o + q < n && !((bits >> q) & 1u)) zmask |= 1u << q;
+    const uint32_t mine = (uint32_t)__popc(zmask);
+    uint32_t inc = mine;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t u = __shfl_up(inc, d, 64);
-    if (lane >= d) inc += u;
-  }
-  if (lane == 63) s_w[wave] = inc;
-  __syncthreads();
-  uint32_t pos = inc - mine;
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t u = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += u;
+    }
+    if (lane == 63) s_w[wave] = inc;
+    __syncthreads();
+    uint32_t pos = inc - mine;
 #pragma unroll
-  for (int w2 = 0; w2 < kSubWaves; ++w2)
-    if (w2 < wave) pos += s_w[w2];
-  const int64_t out0 = koff[t] + (int64_t)c;
+    for (int w2 = 0; w2 < kSubWaves; ++w2)
+      if (w2 < wave) pos += s_w[w2];
+    const int64_t out0 = koff[t] + (int64_t)c;
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    if (!((zmask >> q) & 1u)) continue;
-    const int64_t zr = zr0 + (int64_t)pos++;
-    if (zr >= z) break;
-    const int64_t idx = rel0 + o + q;
-    const float v = __fmul_rn(tp[base + idx], scale);  // +-0
-    values[out0 + zr] = v;
-    indices[out0 + zr] = idx;
-    if (r) r[base + idx] = __fsub_rn(v, v);
+    for (int q = 0; q < 4; ++q) {
+      if (!((zmask >> q) & 1u)) continue;
+      const int64_t zr = zr0 + (int64_t)pos++;
+      if (zr >= z) break;
+      const int64_t idx = rel0 + o + q;
+      const float v = __fmul_rn(tp[base + idx], scale);  // +-0
+      values[out0 + zr] = v;
+      indices[out0 + zr] = idx;
+      if (r) r[base + idx] = __fsub_rn(v, v);
+    }
   }
 }
 
-template <bool GLOBAL>
+// The exact path's gather: each tensor's first k sorted keys (|t'|bits << 32 | ~index).
 __global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict__ tp, float scale,
                                                         float* __restrict__ r, const uint64_t* __restrict__ sorted,
                                                         const int64_t* __restrict__ tbegin,
                                                         const int64_t* __restrict__ tsize,
-                                                        const int64_t* __restrict__ cstart,
                                                         const int64_t* __restrict__ kk, const int64_t* __restrict__ koff,
                                                         float* __restrict__ values, int64_t* __restrict__ indices) {
   const int t = blockIdx.y;
   const int64_t k = kk[t], base = tbegin[t], o = koff[t], n = tsize[t];
-  const int64_t s0 = GLOBAL ? cstart[t] : base;
   for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < k; j += (int64_t)gridDim.x * kThreads) {
-    const uint64_t key = sorted[s0 + j];
-    const uint32_t idx = GLOBAL ? (uint32_t)(key >> 39) : ~(uint32_t)key;
-    if (idx >= n || (GLOBAL && (int)((key >> 31) & 0xFFu) != t)) {  // never expected: a key of another tensor
+    const uint64_t key = sorted[base + j];
+    const uint32_t idx = ~(uint32_t)key;
+    if (idx >= n) {  // never expected
       values[o + j] = 0.0f;
       indices[o + j] = -1;
       continue;
@@ -1888,6 +1858,257 @@ __global__ __launch_bounds__(kThreads) void topk_gather(const float* __restrict_
     values[o + j] = v;
     indices[o + j] = (int64_t)idx;
     if (r) r[base + idx] = __fsub_rn(v, v);
+  }
+}
+
+// The tensor t with koff[t] <= j < koff[t + 1] among [0, nt): the largest t with koff[t] <= j
+// (a tensor with no values shares its koff with the next one, which is then the larger t).
+__device__ __forceinline__ int koff_tensor(const int64_t* koff, int nt, int64_t j) {
+  int lo = 0, hi = nt - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (koff[mid] <= j) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// ---- the exact tail (round 6): the sampled path's fallback, decided and run on the device
+//
+// Always enqueued after the bucket kernels and the zero fill, so omf_topk_encode never waits for
+// the plan's verdict on the host: a grid of one workgroup per CU (co-resident) reads the verdict
+// words and, unless they report a fallback (a redo: a sampled threshold too high for some tensor;
+// an over-full fine bin) or the call forces one, leaves at once.  On a fallback it runs the exact
+// path in phases separated by grid barriers (agent-scope arrivals on a monotone counter, bounded:
+// an expiry aborts every workgroup and sets the plan's error word, which omf_plan_check reports
+// as OMF_ETIMEOUT):
+//   restore    every candidate's residual back to t' (EF modes), per-item candidate counts
+//   scan       per-item offsets, per-tensor candidate starts / counts, redo flags (one block)
+//   redo       (flagged tensors) a 1024-bin histogram of |t'|, the k-th bin, a re-collection,
+//              and the scan again
+//   compact    the candidates as keys index << 39 | tensor << 31 | (2^31 - 1 - |t'|bits)
+//   sort       an LSD radix sort of the low 39 bits (5 stable passes of 8 bits: per-block digit
+//              counts, one block's scan of the digit-major count table, a stable scatter whose
+//              in-tile ranks come from wave ballots) — tensor ascending, |t'| descending, index
+//              ascending, the order the bucket sort gives
+//   gather     values / int64 indices of each tensor's first k keys, residual t' - t' there.
+// Sizes come from the device (the candidate count), so nothing is read back to the host.
+constexpr int kRadixDigits = 256;
+constexpr int kRadixPasses = (kSortBits + 7) / 8;  // 5
+constexpr uint32_t kTailWaitTicks = 20000000u;      // 200 ms of the 100 MHz wall clock: a guard only
+
+struct TailArgs {
+  const float* tp;      // t' (EF modes: the residual) or x (mode 0, times scale)
+  float scale;
+  float* rz;            // the residual (EF modes) or null
+  const Item* items;
+  int64_t n_items;
+  int32_t nt;
+  int32_t forced;
+  const int64_t *kk, *koff, *tbegin;
+  const uint32_t *tfirst, *tlast;
+  uint32_t *sub_cnt, *item_cnt, *item_off, *cnt, *flag, *hist, *bin;
+  int64_t* cstart;
+  uint64_t *cand, *packed;  // the candidates' runs; the packed keys (the sort ping-pongs between them)
+  uint32_t* gh;             // kRadixDigits x gridDim.x digit counts
+  uint32_t* status;         // [0..2] the plan's verdict; [4] arrivals, [5] exits, [6] abort, [7..8] the scan's
+  float* values;
+  int64_t* indices;
+  unsigned long long* stats;  // plan-owned: [0] fast path, [1] zero fills, [2] fallbacks, [3] redos
+  uint32_t* err;              // the plan's error word (bit 8: a tail barrier expired)
+};
+
+// Grid barrier of the tail: every workgroup's stores released at agent scope, one arrival on the
+// monotone counter status[4], a bounded poll for epoch * gridDim.x arrivals, then an acquire.
+// false: aborted (an expiry here or in another workgroup).
+__device__ bool tail_sync(const TailArgs& a, uint32_t& epoch) {
+  __shared__ uint32_t s_ok;
+  __syncthreads();
+  ++epoch;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    __hip_atomic_fetch_add(&a.status[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t target = epoch * gridDim.x;
+    const uint64_t t0 = wall_clock64();
+    uint32_t ok = 1, polls = 0;
+    while (__hip_atomic_load(&a.status[4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__hip_atomic_load(&a.status[6], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(8);
+      if (++polls > 4096u && wall_clock64() - t0 > kTailWaitTicks) {  // never expected
+        __hip_atomic_store(&a.status[6], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_or(a.err, 8u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    __threadfence();
+    s_ok = ok;
+  }
+  __syncthreads();
+  return s_ok != 0u;
+}
+
+__device__ __forceinline__ uint32_t ld_word(const uint32_t* p) {
+  return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One LSD pass over keys [0, n) of src (block b owns the tile-aligned range [b, b + 1) * chunk):
+// stable by digit (key >> sh) & 255 into dst.  Returns false when a barrier aborted.
+__device__ bool tail_radix_pass(const TailArgs& a, uint32_t& epoch, const uint64_t* __restrict__ src,
+                                uint64_t* __restrict__ dst, uint32_t n, int sh) {
+  __shared__ uint32_t s_h[kRadixDigits];
+  __shared__ uint32_t s_wc[kWaves * kRadixDigits];
+  __shared__ uint32_t s_part[kWaves];
+  const uint32_t G = gridDim.x, b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t dmask = (1u << min(8, kSortBits - sh)) - 1u;  // the last pass: bits 32-38 (bit 39 is the index's)
+  const uint64_t chunk = (((uint64_t)n + G - 1) / G + kThreads - 1) / kThreads * kThreads;
+  const uint32_t b0 = (uint32_t)min((uint64_t)n, b * chunk), b1 = (uint32_t)min((uint64_t)n, b0 + chunk);
+  s_h[tid] = 0;  // kThreads == kRadixDigits
+  __syncthreads();
+  for (uint32_t e = b0 + tid; e < b1; e += kThreads) atomicAdd(&s_h[(uint32_t)(src[e] >> sh) & dmask], 1u);
+  __syncthreads();
+  a.gh[(size_t)tid * G + b] = s_h[tid];
+  if (!tail_sync(a, epoch)) return false;
+  if (b == 0) {  // exclusive scan of the digit-major table: thread d owns digit d's G counts
+    uint32_t* row = a.gh + (size_t)tid * G;
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < G; ++q) sum += row[q];
+    uint32_t tot;
+    uint32_t run = block_scan_incl<kThreads>(sum, s_part, tot) - sum;
+    for (uint32_t q = 0; q < G; ++q) {
+      const uint32_t c = row[q];
+      row[q] = run;
+      run += c;
+    }
+  }
+  if (!tail_sync(a, epoch)) return false;
+  __shared__ uint32_t s_run[kRadixDigits];
+  s_run[tid] = a.gh[(size_t)tid * G + b];
+  const int lane = tid & 63, wave = tid >> 6;
+  const uint64_t lt = (1ull << lane) - 1ull;
+  for (uint32_t t0 = b0; t0 < b1; t0 += kThreads) {
+    const uint32_t e = t0 + tid;
+    const bool valid = e < b1;
+    const uint64_t key = valid ? src[e] : 0ull;
+    const uint32_t d = (uint32_t)(key >> sh) & dmask;
+    uint64_t m = __ballot(valid);  // the lanes of this wave with my digit
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const bool one = (d >> bit) & 1u;
+      const uint64_t mb = __ballot(one);
+      m &= one ? mb : ~mb;
+    }
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s_wc[w * kRadixDigits + tid] = 0;
+    __syncthreads();  // (also: s_run complete)
+    const uint32_t rank = (uint32_t)__popcll(m & lt);
+    if (valid && rank == 0) s_wc[wave * kRadixDigits + d] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = s_run[d] + rank;
+      for (int w = 0; w < wave; ++w) pos += s_wc[w * kRadixDigits + d];
+      dst[pos] = key;
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) add += s_wc[w * kRadixDigits + tid];
+    s_run[tid] += add;  // (read by other threads only after the next tile's first barrier)
+  }
+  return tail_sync(a, epoch);
+}
+
+__global__ __launch_bounds__(kThreads) void topk_exact_tail(TailArgs a) {
+  static_assert(kThreads == kRadixDigits, "one thread per radix digit");
+  const uint32_t* st = a.status;
+  const uint32_t zf = ld_word(&st[0]), redo = ld_word(&st[1]), over = ld_word(&st[2]);
+  const bool fb = a.forced || redo || over;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // the plan's counters (omf_topk_stats)
+    if (fb) {
+      atomicAdd(&a.stats[2], 1ull);
+      if (redo) atomicAdd(&a.stats[3], 1ull);
+    } else {
+      atomicAdd(&a.stats[0], 1ull);
+      if (zf) atomicAdd(&a.stats[1], 1ull);
+    }
+  }
+  if (!fb) return;  // the usual case: the bucket kernels wrote the selection
+  const uint32_t G = gridDim.x;
+  uint32_t epoch = 0;
+  bool ok = true;
+  // restore + item counts
+  for (int64_t i = blockIdx.x; i < a.n_items; i += G) {
+    __syncthreads();
+    restore_item(a.cand, a.items, a.sub_cnt, a.tbegin, a.rz, a.item_cnt, i);
+  }
+  ok = tail_sync(a, epoch);
+  if (ok && blockIdx.x == 0)
+    scan_check_block(a.nt, a.kk, a.tfirst, a.tlast, a.item_cnt, a.item_off, a.n_items, a.cstart, a.cnt, a.flag,
+                     &a.status[7]);
+  ok = ok && tail_sync(a, epoch);
+  if (ok && ld_word(&st[8])) {  // a sample set the threshold too high for some tensor: redo it exactly
+    for (int64_t i = blockIdx.x; i < a.n_items; i += G) {
+      __syncthreads();
+      prep_hist_item<0>(a.tp, nullptr, a.scale, a.items, a.flag, a.hist, i);
+    }
+    ok = tail_sync(a, epoch);
+    for (int t = blockIdx.x; ok && t < a.nt; t += G) {
+      __syncthreads();
+      select_bin_tensor(a.hist, a.kk, a.flag, a.bin, t);
+    }
+    ok = ok && tail_sync(a, epoch);
+    for (int64_t i = blockIdx.x; ok && i < a.n_items; i += G) {
+      __syncthreads();
+      collect_item<true>(a.tp, a.scale, a.items, a.tbegin, a.bin, a.flag, a.cnt, a.sub_cnt, a.item_cnt, a.cand, i);
+    }
+    ok = ok && tail_sync(a, epoch);
+    if (ok && blockIdx.x == 0)
+      scan_check_block(a.nt, a.kk, a.tfirst, a.tlast, a.item_cnt, a.item_off, a.n_items, a.cstart, a.cnt, a.flag,
+                       &a.status[7]);
+    ok = ok && tail_sync(a, epoch);
+  }
+  for (int64_t i = blockIdx.x; ok && i < a.n_items; i += G) {
+    __syncthreads();
+    compact_item(a.cand, a.items, a.sub_cnt, a.item_off, a.packed, i);
+  }
+  ok = ok && tail_sync(a, epoch);
+  const uint32_t n = ok ? ld_word(&st[7]) : 0u;
+  uint64_t* src = a.packed;
+  uint64_t* dst = a.cand;
+  for (int p = 0; ok && p < kRadixPasses; ++p) {
+    ok = tail_radix_pass(a, epoch, src, dst, n, 8 * p);
+    uint64_t* tmp = src;
+    src = dst;
+    dst = tmp;
+  }
+  if (ok) {  // gather: output j of tensor t is the t's sorted key cstart[t] + (j - koff[t])
+    const int64_t K = a.koff[a.nt];
+    for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < K; j += (int64_t)G * kThreads) {
+      const int t = koff_tensor(a.koff, a.nt, j);
+      const uint64_t key = src[a.cstart[t] + (j - a.koff[t])];
+      const uint32_t idx = (uint32_t)(key >> 39);
+      const int64_t base = a.tbegin[t];
+      if ((int)((key >> 31) & 0xFFu) != t) {  // never expected: a key of another tensor
+        a.values[j] = 0.0f;
+        a.indices[j] = -1;
+        continue;
+      }
+      const float v = __fmul_rn(a.tp[base + idx], a.scale);
+      a.values[j] = v;
+      a.indices[j] = (int64_t)idx;
+      if (a.rz) a.rz[base + idx] = __fsub_rn(v, v);
+    }
+  }
+  // exit: the last workgroup out resets the barrier words for the next call
+  __syncthreads();
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(&a.status[5], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1) {
+    __hip_atomic_store(&a.status[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.status[6], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&a.status[5], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -2002,18 +2223,6 @@ __global__ __launch_bounds__(kThreads) void topk_scatter(const float* __restrict
 // Indices are unique within a client, so the read-modify-write needs no atomics.  koff comes from
 // the plan's decode table (a ratio's k_t, or a received message's counts; k_t may be 0).
 constexpr int kArenaMaxTensors = 4096;
-
-// The tensor t with koff[t] <= j < koff[t + 1] among [0, nt): the largest t with koff[t] <= j
-// (a tensor with no values shares its koff with the next one, which is then the larger t).
-__device__ __forceinline__ int koff_tensor(const int64_t* koff, int nt, int64_t j) {
-  int lo = 0, hi = nt - 1;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (koff[mid] <= j) lo = mid;
-    else hi = mid - 1;
-  }
-  return lo;
-}
 
 __global__ __launch_bounds__(kThreads) void topk_scatter_arena(const float* __restrict__ values,
                                                                const int64_t* __restrict__ indices,
@@ -2303,66 +2512,40 @@ const std::vector<int64_t>& offsets(const omf_plan* p);
 void* topk_table(omf_plan* p, uint64_t key, size_t bytes, bool* fresh, uint64_t** host);
 void* topk_table_counts(omf_plan* p, const int64_t* counts, size_t bytes, bool* fresh, uint64_t** host);
 omf::TopkKnobs& topk_knobs(omf_plan* p);
+uint32_t* err_word(omf_plan* p);
 }  // namespace omf_plan_access
 
 namespace {
 
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// Per host thread and device: a 16-byte status buffer in mapped, coherent host memory that
-// topk_plan's last block writes (never freed: a few bytes per thread that calls the encoder).
+// Per host thread and device: the group pipeline's second stream and its events (made on first
+// use; experiment builds only use more than one group).
 struct HostSync {
-  uint32_t* pinned = nullptr;  // host view
-  uint32_t* dev = nullptr;     // device view of the same bytes
-  uint32_t seq = 0;
-  hipStream_t side = nullptr;  // the pipeline's second stream (made on first use)
+  hipStream_t side = nullptr;
   hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t fused[2] = {nullptr, nullptr};  // per stream: its latest group's streaming pass issued
 };
-
-// Wait for the verdict of call `seq` (launched at t0).  The verdict lands as soon as the plan kernel
-// ends (~90 % into the call; the bucket kernels are queued behind it, so the GPU stays busy while
-// the host reads it).  The host first sleeps for 60 % of the recent launch-to-verdict time — the
-// thread is descheduled instead of spinning a core for ~0.8 ms a call — then spins on the mapped
-// word (an event or a copy packet would add tens of us).  The time is the plan's (TopkStats).
-// If it has not come after 200 ms,
-// synchronise the stream (which reports a failed launch or fault) and look again.
-int wait_status(HostSync* h, uint32_t seq, hipStream_t st, std::chrono::steady_clock::time_point t0, TopkStats* ps) {
-  if (ps->verdict_us > 200.0) {
-    const auto nap = std::chrono::microseconds((int64_t)(0.6 * ps->verdict_us));
-    if (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq) std::this_thread::sleep_until(t0 + nap);
-  }
-  while (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq) {
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
-      OMF_HIP(hipStreamSynchronize(st));
-      if (__atomic_load_n(&h->pinned[3], __ATOMIC_ACQUIRE) != seq)
-        return fail(OMF_EHIP, "omf_topk_encode: the plan verdict never reached the host");
-      break;
-    }
-    __builtin_ia32_pause();
-  }
-  const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-  ps->verdict_us = (ps->verdict_us == 0.0 || us < ps->verdict_us) ? us : 0.9 * ps->verdict_us + 0.1 * us;
-  return OMF_OK;
-}
 HostSync* host_sync(int dev) {
   constexpr int kMaxDev = 64;
   thread_local HostSync hs[kMaxDev];
   if (dev < 0 || dev >= kMaxDev) return nullptr;
-  HostSync& h = hs[dev];
-  if (!h.pinned) {
-    void* p = nullptr;
-    if (hipHostMalloc(&p, 16, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
-    void* d = nullptr;
-    if (hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
-      (void)hipHostFree(p);
-      return nullptr;
-    }
-    std::memset(p, 0, 16);
-    h.pinned = static_cast<uint32_t*>(p);
-    h.dev = static_cast<uint32_t*>(d);
+  return &hs[dev];
+}
+
+// Workgroups of the exact tail: one per CU (all co-resident, which its grid barriers need), per
+// device.
+uint32_t tail_grid(int dev) {
+  static std::mutex mu;
+  static int cus[64] = {0};
+  std::lock_guard<std::mutex> lk(mu);
+  if (dev < 0 || dev >= 64) return 64u;
+  if (!cus[dev]) {
+    int n = 0;
+    if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 64;
+    cus[dev] = std::min(n, 1024);
   }
-  return &h;
+  return (uint32_t)cus[dev];
 }
 
 // The second stream and the fork / join events of the group pipeline (per device and thread).
@@ -2487,7 +2670,8 @@ size_t sort_tmp_bytes(const omf_plan* p) {
   size_t bytes = 0;
   uint64_t* dummy = nullptr;
   if (global_path(p)) {
-    (void)rocprim::radix_sort_keys(nullptr, bytes, dummy, dummy, (size_t)size, 0, 64, (hipStream_t)0, false);
+    (void)dummy;
+    bytes = 4 * (size_t)kRadixDigits * tail_grid(omf_plan_access::device(p));  // the exact tail's digit table
   } else {
     uint32_t* off = nullptr;
     (void)rocprim::segmented_radix_sort_keys_desc(nullptr, bytes, dummy, dummy, (unsigned int)size, (unsigned int)nt,
@@ -2604,6 +2788,18 @@ int64_t sample_max_runs(const TopkKnobs& kn) { return kn.sample_runs ? kn.sample
 float2 sure_margin(const TopkKnobs& kn) { return make_float2(kn.sure_z, kn.sure_c); }
 
 constexpr uint64_t kSetupTag = 0x5E7A9B1C00000000ull;
+constexpr uint64_t kStatsTag = 0x57A7500D0000000Full;
+
+// The plan's counters of the sampled path that the device decides (the exact tail updates them):
+// [0] fast path, [1] zero fills, [2] fallbacks, [3] redos.  A plan-owned table, zeroed on creation.
+unsigned long long* device_stats(omf_plan* p, hipStream_t st) {
+  bool fresh = false;
+  uint64_t* host = nullptr;
+  void* d = omf_plan_access::topk_table(p, kStatsTag, 64, &fresh, &host);
+  if (!d) return nullptr;
+  if (fresh && hipMemsetAsync(d, 0, 64, st) != hipSuccess) return nullptr;
+  return static_cast<unsigned long long*>(d);
+}
 
 int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uint32_t* status, SetupTable* out) {
   const std::vector<int64_t>& sizes = omf_plan_access::sizes(p);
@@ -2717,9 +2913,22 @@ int omf_plan_set_topk(omf_plan* plan, int32_t groups, int32_t force_fallback, in
 int omf_topk_stats(omf_plan* plan, int64_t* out6, int32_t reset) {
   if (!plan || !out6) return fail(OMF_EINVAL, "plan and out6 must be non-NULL");
   TopkStats& s = omf_plan_access::topk_knobs(plan).stats;
-  const int64_t v[6] = {s.calls, s.fast, s.zero_fill, s.fallback, s.redo, s.exact};
+  DeviceGuard g(omf_plan_access::device(plan));
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  OMF_HIP(hipDeviceSynchronize());  // the device keeps the path counters (the exact tail's)
+  bool fresh = false;
+  uint64_t* host = nullptr;
+  void* d = omf_plan_access::topk_table(plan, kStatsTag, 64, &fresh, &host);
+  if (!d) return fail(OMF_ENOMEM, "omf_topk_stats: counter table allocation failed");
+  unsigned long long dv[4] = {0, 0, 0, 0};
+  if (fresh) OMF_HIP(hipMemset(d, 0, 64));
+  else OMF_HIP(hipMemcpy(dv, d, sizeof dv, hipMemcpyDeviceToHost));
+  const int64_t v[6] = {s.calls, (int64_t)dv[0], (int64_t)dv[1], (int64_t)dv[2], (int64_t)dv[3], s.exact};
   std::memcpy(out6, v, sizeof v);
-  if (reset) s.calls = s.fast = s.zero_fill = s.fallback = s.redo = s.exact = 0;
+  if (reset) {
+    s.calls = s.exact = 0;
+    OMF_HIP(hipMemset(d, 0, sizeof dv));
+  }
   return OMF_OK;
 }
 
@@ -2799,9 +3008,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   const bool glob = global_path(plan);
   if (!glob) OMF_HIP(hipMemsetAsync(w, 0, L.zero_end, st));
   HostSync* hsync = host_sync(omf_plan_access::device(plan));
-  if (!hsync) return fail(OMF_EHIP, "omf_topk_encode: pinned status buffer");
-  const uint32_t seq = ++hsync->seq == 0 ? ++hsync->seq : hsync->seq;
-  const auto t_call = std::chrono::steady_clock::now();
+  if (!hsync) return fail(OMF_EHIP, "omf_topk_encode: device index out of range");
   // the per-(plan, ratio) constant tables: made by topk_setup on the first call at this ratio
   SetupTable tb;
   const TopkKnobs& kn = knobs(plan);
@@ -2812,6 +3019,8 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
   kk = tb.kk; koff = tb.koff; tfirst = tb.tfirst; tlast = tb.tlast; bbase = tb.bbase; kb2 = tb.kb2; sbase = tb.sbase;
   size_t tmp_bytes = L.tmp_bytes;
   if (glob) {
+    unsigned long long* dstats = device_stats(plan, st);
+    if (!dstats) return fail(OMF_ENOMEM, "omf_topk_encode: counter table allocation failed");
     const bool forced = kn.force_fallback != 0;
     const std::vector<Group> groups = make_groups(omf_plan_access::sizes(plan), ratio, max_runs,
                                                   topk_group_count(plan, kn));
@@ -2857,18 +3066,16 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       const dim3 supgrid(G.nsup), supblk(1024);
       hipLaunchKernelGGL(topk_fine_hist, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo, fmap,
                          tlo, fcount, fhist, bbase, bfill, G.sup0);
-      // the call's last plan block (over every group) publishes the verdict to mapped host
-      // memory; the bucket kernels are enqueued before the host waits for it (they do nothing
-      // when the verdict is a fallback), so the GPU does not idle while the host reads it
+      // the plan writes the verdict words (status); the bucket kernels behind it do nothing on a
+      // fallback verdict, which the exact tail then handles
       const bool small = G.nb_max <= kScatterSmallB && kn.scatter_small;
       if (!forced && small && kn.planned_scatter)  // the plan inside the scatter launch
         hipLaunchKernelGGL(topk_scatter_planned, supgrid, supblk, 0, s, cand, items, sub_cnt, (const uint4*)tb.supinfo,
                            fmap, tlo, fcount, fhist, kk, tkey, bbase, brec, bfill, kb2, d_begins, rz, sorted, flag, zcnt,
-                           status, thi, tb.done, hsync->dev, seq, (uint32_t)nt, G.sup0);
+                           status, thi, G.sup0);
       else
         hipLaunchKernelGGL(topk_plan, dim3((unsigned)(G.t1 - G.t0)), sblk, 0, s, kk, fcount, fhist, bbase, fbucket,
-                           bstart, brec, bfill, kb2, flag, status, fse, tkey, zcnt, dbg, tb.done, hsync->dev, seq, G.t0,
-                           (uint32_t)nt);
+                           bstart, brec, bfill, kb2, flag, status, fse, tkey, zcnt, dbg, G.t0);
       if (!forced) {
         if (!(small && kn.planned_scatter)) {  // (the planned scatter has run above)
           if (small)
@@ -2889,62 +3096,58 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       OMF_HIP(hipEventRecord(hsync->join, hsync->side));
       OMF_HIP(hipStreamWaitEvent(st, hsync->join, 0));
     }
-    if (int rc = wait_status(hsync, seq, st, t_call, &stats)) return rc;
-    uint32_t host_status[4];
-    std::memcpy(host_status, hsync->pinned, 16);
-    if (kn.dbg & 4)
-      fprintf(stderr, "omf_topk: zero fill %u redo %u overflow %u\n", host_status[0], host_status[1], host_status[2]);
     ++stats.calls;
-    if (!host_status[1] && !host_status[2] && !forced) {
-      ++stats.fast;
-      if (host_status[0]) {  // zero mode: complete the short tensors with their lowest-index zeros
-        ++stats.zero_fill;
-        hipLaunchKernelGGL(topk_zero_fill, dim3((unsigned)tb.nzb), dim3(kSubThreads), 0, st, (const uint2*)tb.zmap, zcnt, kk, koff,
-                           d_begins, d_sizes, tfirst, items, sub_cnt, cand, tp, scale, rz, values, indices);
-        OMF_HIP(hipGetLastError());
-      }
-      return OMF_OK;
-    }
-    ++stats.fallback;
-    if (host_status[1]) ++stats.redo;
-    // fallback (a redo, a fine bin over kBucketHalf keys, or forced): device-wide radix sort
-    if (rz) hipLaunchKernelGGL(topk_restore, grid, blk, 0, st, cand, items, sub_cnt, d_begins, rz);
-    hipLaunchKernelGGL(topk_item_counts, dim3((unsigned)((n_items + kThreads - 1) / kThreads)), blk, 0, st, sub_cnt,
-                       (int64_t)n_items, item_cnt);
-    auto scan_and_check = [&]() -> int {
-      hipLaunchKernelGGL(topk_scan_check, dim3(1), dim3(1024), 0, st, nt, kk, tfirst, tlast, item_cnt, item_off,
-                         n_items, cstart, cnt, flag, status);
-      OMF_HIP(hipGetLastError());
-      // the sort needs the candidate count on the host (and the redo decision)
-      OMF_HIP(hipMemcpyAsync(host_status, status, 8, hipMemcpyDeviceToHost, st));
-      OMF_HIP(hipStreamSynchronize(st));
-      return OMF_OK;
-    };
-    if (int rc = scan_and_check()) return rc;
-    if (host_status[1]) {  // a sample set the threshold too high for some tensor: redo it exactly
-      hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, tp, nullptr, scale, items, flag, hist);
-      hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, flag, bin);
-      hipLaunchKernelGGL((topk_collect<true>), grid, blk, 0, st, tp, scale, items, d_begins, bin, flag, cnt, sub_cnt,
-                         item_cnt, cand);
-      if (int rc = scan_and_check()) return rc;
-    }
-    const uint64_t total = host_status[0];
-    hipLaunchKernelGGL(topk_compact, grid, blk, 0, st, cand, items, sub_cnt, item_off, sorted);
-    // sort the packed keys back into `cand` (the per-item regions are no longer needed):
-    // candidates are in index order within each tensor, so a stable sort of the tensor and
-    // magnitude bits alone yields (tensor, |t'| descending, index ascending)
-    OMF_HIP(rocprim::radix_sort_keys(w + L.tmp, tmp_bytes, sorted, cand, (size_t)total, 0, kSortBits, st, false));
+    // zero mode: the short tensors completed with their lowest-index zeros (leaves at once unless
+    // the verdict reports a zero fill and no fallback)
+    if (tb.nzb > 0 && !forced)
+      hipLaunchKernelGGL(topk_zero_fill, dim3(std::min<uint32_t>((uint32_t)tb.nzb, kZeroFillGrid)), dim3(kSubThreads), 0,
+                         st, (const uint2*)tb.zmap, (uint32_t)tb.nzb, status, zcnt, kk, koff, d_begins, d_sizes, tfirst,
+                         items, sub_cnt, cand, tp, scale, rz, values, indices);
+    // the fallback (a redo, a fine bin over what a bucket holds, or forced), decided and run on the
+    // device: leaves at once on a fast-path verdict
+    TailArgs ta;
+    ta.tp = tp;
+    ta.scale = scale;
+    ta.rz = rz;
+    ta.items = items;
+    ta.n_items = n_items;
+    ta.nt = nt;
+    ta.forced = forced ? 1 : 0;
+    ta.kk = kk;
+    ta.koff = koff;
+    ta.tbegin = d_begins;
+    ta.tfirst = tfirst;
+    ta.tlast = tlast;
+    ta.sub_cnt = sub_cnt;
+    ta.item_cnt = item_cnt;
+    ta.item_off = item_off;
+    ta.cnt = cnt;
+    ta.flag = flag;
+    ta.hist = hist;
+    ta.bin = bin;
+    ta.cstart = cstart;
+    ta.cand = cand;
+    ta.packed = sorted;
+    ta.gh = reinterpret_cast<uint32_t*>(w + L.tmp);
+    ta.status = status;
+    ta.values = values;
+    ta.indices = indices;
+    ta.stats = dstats;
+    ta.err = omf_plan_access::err_word(plan);
+    hipLaunchKernelGGL(topk_exact_tail, dim3(tail_grid(omf_plan_access::device(plan))), dim3(kThreads), 0, st, ta);
+    OMF_HIP(hipGetLastError());
+    (void)tmp_bytes;
+    return OMF_OK;
   } else {
     ++stats.exact;
     if (residual_mode == 0)
-      hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
+      hipLaunchKernelGGL((topk_prep_hist<0>), grid, blk, 0, st, x, residual, alpha, items, hist);
     else if (residual_mode == 1)
-      hipLaunchKernelGGL((topk_prep_hist<1>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
+      hipLaunchKernelGGL((topk_prep_hist<1>), grid, blk, 0, st, x, residual, alpha, items, hist);
     else
-      hipLaunchKernelGGL((topk_prep_hist<2>), grid, blk, 0, st, x, residual, alpha, items, nullptr, hist);
-    hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, nullptr, bin);
-    hipLaunchKernelGGL((topk_collect<false>), grid, blk, 0, st, tp, scale, items, d_begins, bin, nullptr, cnt, sub_cnt,
-                       item_cnt, cand);
+      hipLaunchKernelGGL((topk_prep_hist<2>), grid, blk, 0, st, x, residual, alpha, items, hist);
+    hipLaunchKernelGGL(topk_select_bin, dim3((unsigned)nt), blk, 0, st, hist, kk, bin);
+    hipLaunchKernelGGL(topk_collect, grid, blk, 0, st, tp, scale, items, d_begins, bin, cnt, cand);
     hipLaunchKernelGGL(topk_segments, dim3(((unsigned)nt + kThreads - 1) / kThreads), blk, 0, st, nt, d_begins, cnt,
                        seg_b, seg_e);
     OMF_HIP(hipGetLastError());
@@ -2952,14 +3155,9 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
                                                     (unsigned int)omf_plan_access::arena_end(plan), (unsigned int)nt,
                                                     seg_b, seg_e, 0, 64, st, false));
   }
-  const uint64_t* sorted_keys = glob ? cand : sorted;
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((kmax + kThreads - 1) / kThreads, 1024));
-  if (glob)
-    hipLaunchKernelGGL((topk_gather<true>), dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted_keys, d_begins,
-                       d_sizes, cstart, kk, koff, values, indices);
-  else
-    hipLaunchKernelGGL((topk_gather<false>), dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted_keys, d_begins,
-                       d_sizes, cstart, kk, koff, values, indices);
+  hipLaunchKernelGGL(topk_gather, dim3(gx, (unsigned)nt), blk, 0, st, tp, scale, rz, sorted, d_begins, d_sizes, kk,
+                     koff, values, indices);
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }
@@ -3064,8 +3262,6 @@ int omf_topk_torch_order(omf_plan* plan, const float* x, float* residual, int32_
   uint32_t* cnt = reinterpret_cast<uint32_t*>(w + L.cnt);  // the encode's scratch, free once it is done
   uint32_t* flags = reinterpret_cast<uint32_t*>(w + L.flag);
   SetupTable tb;
-  HostSync* hsync = host_sync(dev);
-  if (!hsync) return fail(OMF_EHIP, "omf_topk_torch_order: pinned status buffer");
   if (int r = setup_table(plan, ratio, sample_max_runs(knobs(plan)), st, reinterpret_cast<uint32_t*>(w + L.status), &tb))
     return r;
   int64_t n_items = 0;

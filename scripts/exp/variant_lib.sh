@@ -1,6 +1,6 @@
 #!/bin/bash
 # Variant library for A/B runs: recompile one source with extra defines and link it with the
-# in-tree objects.  scripts/exp/variant_lib.sh <out.so> <source> -DNAME=VALUE ...
+# in-tree objects.  scripts/exp/variant_lib.sh <out.so> <source[,source...]> -DNAME=VALUE ...
 # Load it with OMF_CODEC_LIB_EXPERIMENT=<out.so> (omnifed_amd/_lib.py).
 set -e
 cd "$(dirname "$0")/../.."
@@ -9,9 +9,10 @@ python3 -m omnifed_amd.build > /dev/null
 flags=$(python3 -c "from omnifed_amd.build import FLAGS; print(' '.join(FLAGS))")
 objs=()
 for o in omnifed_amd/_obj/*.o; do
-  if [ "$(basename $o)" = "$src.o" ]; then
-    /opt/rocm/bin/hipcc $flags -I include "$@" -c omnifed_amd/csrc/$src -o /tmp/variant_$src.o
-    objs+=(/tmp/variant_$src.o)
+  b=$(basename $o .o)
+  if [[ ",$src," == *",$b,"* ]]; then
+    /opt/rocm/bin/hipcc $flags -I include "$@" -c omnifed_amd/csrc/$b -o /tmp/variant_$b.o
+    objs+=(/tmp/variant_$b.o)
   else
     objs+=($o)
   fi
