@@ -270,7 +270,7 @@ constexpr int kSRunsPerBlock = OMF_SRUNS_PER_BLOCK;
 // samples to trust, or fewer non-zero samples than the target: an exact-zero-heavy tensor such
 // as the PS's average of sparse Top-K updates).  Exact zeros are never candidates: when a tensor
 // has fewer than k non-zeros, its selection is completed by its lowest-index zeros (topk_plan
-// and topk_zero_fill), the order the exact path's stable sort gives ties.
+// and the zero fill, zero_fill_chunk), the order the exact path's stable sort gives ties.
 // Also clears the tensor's redo histogram and its fine bins.
 __device__ void sample_threshold_tensor(int t, int64_t n, const uint32_t* h, uint32_t zeros, float2 sure_zc,
                                         const int64_t* __restrict__ kk,
@@ -1076,7 +1076,7 @@ __global__ __launch_bounds__(1024) void topk_fine_hist(const uint64_t* __restric
 // (se_i = keys in higher bins), a bucket starts at its smallest se.  A tensor with fewer than
 // k candidates is flagged for the exact redo — unless its threshold was every non-zero (zero
 // mode, tkey == 1): then every candidate is selected (ranks [0, c)) and the rest of its
-// selection is its k - c lowest-index exact zeros, written by topk_zero_fill; zcnt[t] = c for
+// selection is its k - c lowest-index exact zeros, written by zero_fill_chunk; zcnt[t] = c for
 // such a tensor, 0xffffffff otherwise.  Flags the call for the fallback sort when a kept fine
 // bin holds more than kBucketHalf keys.  status[0] |= zero fill, [1] |= redo, [2] |= overflow.
 constexpr uint32_t kNoZeroFill = 0xffffffffu;
@@ -1742,98 +1742,78 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(8))) void 
 // Fast path, zero mode (topk_plan_tensor): a tensor with c < k non-zero t' selects all of them
 // (ranks [0, c), written by the bucket sort) and then its k - c lowest-index exact zeros, at
 // ranks [c, k) in index order — the (|t'| descending, index ascending) order.  Since the tensor
-// has only c non-zeros, its first k elements hold at least k - c zeros, so only the sub-chunks
-// (1 Ki elements) below index k are visited: one 256-thread block per such sub-chunk (zmap =
-// (tensor, sub) pairs of the plan-owned table).  A block counts the non-zeros before its sub
-// (the fused pass's per-sub candidate counts: in zero mode exactly the non-zeros), marks its
-// sub's non-zeros from their candidate keys in an LDS bitmap, and ranks its zeros with a block
-// scan; value = t' (the sign of the zero), residual := t' - t' (+0).  Always enqueued (round 6:
-// no host wait for the verdict): a grid of at most kZeroFillGrid blocks strides over the nblk
-// (tensor, sub) pairs and leaves at once unless the plan's verdict (status) reports a zero fill
-// and no fallback.
-constexpr uint32_t kZeroFillGrid = 1024;
-__global__ __launch_bounds__(kSubThreads) void topk_zero_fill(const uint2* __restrict__ zmap, uint32_t nblk,
-                                                           const uint32_t* __restrict__ status,
-                                                           const uint32_t* __restrict__ zcnt,
-                                                           const int64_t* __restrict__ kk,
-                                                           const int64_t* __restrict__ koff,
-                                                           const int64_t* __restrict__ tbegin,
-                                                           const int64_t* __restrict__ tsize,
-                                                           const uint32_t* __restrict__ tfirst,
-                                                           const Item* __restrict__ items,
-                                                           const uint32_t* __restrict__ sub_cnt,
-                                                           const uint64_t* __restrict__ cand,
-                                                           const float* __restrict__ tp, float scale,
-                                                           float* __restrict__ r, float* __restrict__ values,
-                                                           int64_t* __restrict__ indices) {
-  __shared__ uint32_t s_bm[kSubPer / 32];
-  __shared__ uint32_t s_w[kSubWaves];
-  __shared__ uint32_t s_sum[kSubWaves];
-  if (!status[0] || status[1] || status[2]) return;  // grid-uniform: no zero fill, or a fallback verdict
-  for (uint32_t zb = blockIdx.x; zb < nblk; zb += gridDim.x) {
-    __syncthreads();  // the previous pair's LDS reads are done
-    const uint2 zm = zmap[zb];
-    const int t = (int)zm.x;
-    const uint32_t x = zm.y;
-    const uint32_t c = zcnt[t];
-    if (c == kNoZeroFill) continue;  // block-uniform
-    const int64_t k = kk[t], n = tsize[t], base = tbegin[t];
-    const int64_t rel0 = (int64_t)x * kSubPer;
-    const uint32_t s0 = tfirst[t] * (uint32_t)kSubsPerItem;
-    // non-zeros before this sub
-    uint32_t nz = 0;
-    for (uint32_t j = threadIdx.x; j < x; j += kSubThreads) nz += sub_cnt[s0 + j];
+// has only c non-zeros, its first k elements hold at least k - c zeros, so only the 1 Ki-element
+// chunks below index k are visited (zmap = (tensor, chunk) pairs of the plan-owned table).  A
+// workgroup (kThreads, 4 elements per thread) counts the non-zeros before its chunk (the fused
+// pass's per-sub-chunk candidate counts: in zero mode exactly the non-zeros), marks the chunk's
+// non-zeros from the candidate keys of its two sub-chunks in an LDS bitmap, and ranks its zeros
+// with a block scan; value = t' (the sign of the zero), residual := t' - t' (+0).  Run by the exact
+// tail's workgroups when the verdict reports a zero fill and no fallback (round 6; rounds 4-5 ran
+// it as a launch of its own, queued by the host after it had read the verdict).
+constexpr int kZChunk = 2 * kSubPer;  // elements per zero-fill chunk (kThreads x 4)
+static_assert(kZChunk == 4 * kThreads, "one float4 of a zero-fill chunk per thread");
+__device__ void zero_fill_chunk(uint2 zm, const uint32_t* __restrict__ zcnt, const int64_t* __restrict__ kk,
+                                const int64_t* __restrict__ koff, const int64_t* __restrict__ tbegin,
+                                const int64_t* __restrict__ tsize, const uint32_t* __restrict__ tfirst,
+                                const Item* __restrict__ items, const uint32_t* __restrict__ sub_cnt,
+                                const uint64_t* __restrict__ cand, const float* __restrict__ tp, float scale,
+                                float* __restrict__ r, float* __restrict__ values, int64_t* __restrict__ indices) {
+  __shared__ uint32_t s_bm[kZChunk / 32];
+  __shared__ uint32_t s_w[kWaves];
+  __shared__ uint32_t s_sum[kWaves];
+  const int t = (int)zm.x;
+  const uint32_t x = zm.y;  // chunk: sub-chunks 2x and 2x + 1 of the tensor
+  const uint32_t c = zcnt[t];
+  if (c == kNoZeroFill) return;  // block-uniform
+  const int64_t k = kk[t], n = tsize[t], base = tbegin[t];
+  const int64_t rel0 = (int64_t)x * kZChunk;
+  const uint32_t s0 = tfirst[t] * (uint32_t)kSubsPerItem;
+  // non-zeros before this chunk
+  uint32_t nz = 0;
+  for (uint32_t j = threadIdx.x; j < 2 * x; j += kThreads) nz += sub_cnt[s0 + j];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) nz += __shfl_xor(nz, o, 64);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) s_sum[wave] = nz;
-    if (threadIdx.x < kSubPer / 32) s_bm[threadIdx.x] = 0;
-    __syncthreads();
-    uint32_t nzb = 0;
+  for (int o = 32; o > 0; o >>= 1) nz += __shfl_xor(nz, o, 64);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) s_sum[wave] = nz;
+  if (threadIdx.x < kZChunk / 32) s_bm[threadIdx.x] = 0;
+  __syncthreads();
+  uint32_t nzb = 0;
 #pragma unroll
-    for (int w2 = 0; w2 < kSubWaves; ++w2) nzb += s_sum[w2];
-    const int64_t z = k - (int64_t)c;                 // zeros to select
-    const int64_t zr0 = rel0 - (int64_t)nzb;          // zeros before this sub
-    if (zr0 >= z) continue;                           // block-uniform
-    const uint32_t g = s0 + x;
+  for (int w2 = 0; w2 < kWaves; ++w2) nzb += s_sum[w2];
+  const int64_t z = k - (int64_t)c;         // zeros to select
+  const int64_t zr0 = rel0 - (int64_t)nzb;  // zeros before this chunk
+  if (zr0 >= z) return;                     // block-uniform
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {  // (every item has kSubsPerItem sub-chunk counts, 0 past the tensor)
+    const uint32_t g = s0 + 2 * x + (uint32_t)h;
     const int64_t b = items[g / kSubsPerItem].begin + (int64_t)(g % kSubsPerItem) * kSubPer;
     const uint32_t cx = sub_cnt[g];
-    for (uint32_t e = threadIdx.x; e < cx; e += kSubThreads) {
-      const uint32_t rel = (uint32_t)(cand[b + e] >> 32) - (uint32_t)rel0;  // < kSubPer
+    for (uint32_t e = threadIdx.x; e < cx; e += kThreads) {
+      const uint32_t rel = (uint32_t)(cand[b + e] >> 32) - (uint32_t)rel0;  // < kZChunk
       atomicOr(&s_bm[rel >> 5], 1u << (rel & 31));
     }
-    __syncthreads();
-    const uint32_t o = 4u * threadIdx.x;
-    const uint32_t bits = (s_bm[o >> 5] >> (o & 31)) & 0xFu;
-    uint32_t zmask = 0;
+  }
+  __syncthreads();
+  const uint32_t o = 4u * threadIdx.x;
+  const uint32_t bits = (s_bm[o >> 5] >> (o & 31)) & 0xFu;
+  uint32_t zmask = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q)
-      if (rel0 + o + q < n && !((bits >> q) & 1u)) zmask |= 1u << q;
-    const uint32_t mine = (uint32_t)__popc(zmask);
-    uint32_t inc = mine;
+  for (int q = 0; q < 4; ++q)
+    if (rel0 + o + q < n && !((bits >> q) & 1u)) zmask |= 1u << q;
+  const uint32_t mine = (uint32_t)__popc(zmask);
+  uint32_t tot;
+  uint32_t pos = block_scan_incl<kThreads>(mine, s_w, tot) - mine;
+  const int64_t out0 = koff[t] + (int64_t)c;
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const uint32_t u = __shfl_up(inc, d, 64);
-      if (lane >= d) inc += u;
-    }
-    if (lane == 63) s_w[wave] = inc;
-    __syncthreads();
-    uint32_t pos = inc - mine;
-#pragma unroll
-    for (int w2 = 0; w2 < kSubWaves; ++w2)
-      if (w2 < wave) pos += s_w[w2];
-    const int64_t out0 = koff[t] + (int64_t)c;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (!((zmask >> q) & 1u)) continue;
-      const int64_t zr = zr0 + (int64_t)pos++;
-      if (zr >= z) break;
-      const int64_t idx = rel0 + o + q;
-      const float v = __fmul_rn(tp[base + idx], scale);  // +-0
-      values[out0 + zr] = v;
-      indices[out0 + zr] = idx;
-      if (r) r[base + idx] = __fsub_rn(v, v);
-    }
+  for (int q = 0; q < 4; ++q) {
+    if (!((zmask >> q) & 1u)) continue;
+    const int64_t zr = zr0 + (int64_t)pos++;
+    if (zr >= z) break;
+    const int64_t idx = rel0 + o + q;
+    const float v = __fmul_rn(tp[base + idx], scale);  // +-0
+    values[out0 + zr] = v;
+    indices[out0 + zr] = idx;
+    if (r) r[base + idx] = __fsub_rn(v, v);
   }
 }
 
@@ -1875,10 +1855,10 @@ __device__ __forceinline__ int koff_tensor(const int64_t* koff, int nt, int64_t 
 
 // ---- the exact tail (round 6): the sampled path's fallback, decided and run on the device
 //
-// Always enqueued after the bucket kernels and the zero fill, so omf_topk_encode never waits for
-// the plan's verdict on the host: a grid of one workgroup per CU (co-resident) reads the verdict
-// words and, unless they report a fallback (a redo: a sampled threshold too high for some tensor;
-// an over-full fine bin) or the call forces one, leaves at once.  On a fallback it runs the exact
+// Always enqueued after the bucket kernels, so omf_topk_encode never waits for the plan's verdict
+// on the host: a grid of one workgroup per CU (co-resident) reads the verdict words and, unless
+// they report a fallback (a redo: a sampled threshold too high for some tensor; an over-full fine
+// bin) or the call forces one, runs the zero fill if the verdict reports one and leaves.  On a fallback it runs the exact
 // path in phases separated by grid barriers (agent-scope arrivals on a monotone counter, bounded:
 // an expiry aborts every workgroup and sets the plan's error word, which omf_plan_check reports
 // as OMF_ETIMEOUT):
@@ -1916,6 +1896,10 @@ struct TailArgs {
   int64_t* indices;
   unsigned long long* stats;  // plan-owned: [0] fast path, [1] zero fills, [2] fallbacks, [3] redos
   uint32_t* err;              // the plan's error word (bit 8: a tail barrier expired)
+  const uint2* zmap;          // the zero fill's (tensor, 1 Ki-element chunk) pairs
+  uint32_t nzc;
+  const uint32_t* zcnt;
+  const int64_t* tsize;
 };
 
 // Grid barrier of the tail: every workgroup's stores released at agent scope, one arrival on the
@@ -2035,7 +2019,15 @@ __global__ __launch_bounds__(kThreads) void topk_exact_tail(TailArgs a) {
       if (zf) atomicAdd(&a.stats[1], 1ull);
     }
   }
-  if (!fb) return;  // the usual case: the bucket kernels wrote the selection
+  if (!fb) {  // the usual case: the bucket kernels wrote the selection
+    if (zf)     // zero mode: complete the short tensors with their lowest-index zeros
+      for (uint32_t c = blockIdx.x; c < a.nzc; c += gridDim.x) {
+        __syncthreads();  // (the previous chunk's LDS reads are done)
+        zero_fill_chunk(a.zmap[c], a.zcnt, a.kk, a.koff, a.tbegin, a.tsize, a.tfirst, a.items, a.sub_cnt, a.cand,
+                        a.tp, a.scale, a.rz, a.values, a.indices);
+      }
+    return;
+  }
   const uint32_t G = gridDim.x;
   uint32_t epoch = 0;
   bool ok = true;
@@ -2772,7 +2764,7 @@ struct SetupTable {
   int64_t *kk, *koff, *kb2;
   uint32_t *tfirst, *tlast, *bbase, *sbase, *smap, *gh, *gz, *done, *arrive;
   uint32_t* supinfo;  // per super-item {tensor, first item, items, first super-item of its tensor}
-  uint32_t* zmap;     // per zero-fill block {tensor, sub-chunk}: the sub-chunks below index k_t
+  uint32_t* zmap;     // per zero-fill chunk {tensor, 1 Ki-element chunk}: the chunks below index k_t
   int32_t nsb, nzb;
 };
 
@@ -2826,10 +2818,10 @@ int setup_table(omf_plan* p, double ratio, int64_t max_runs, hipStream_t st, uin
     }
     item0 += ni;
   }
-  std::vector<uint32_t> zmap;  // topk_zero_fill's blocks
+  std::vector<uint32_t> zmap;  // the zero fill's chunks (zero_fill_chunk)
   for (int32_t t = 0; t < nt; ++t) {
     const int64_t k = std::min(omf_topk_k(sizes[t], ratio), sizes[t]);
-    for (int64_t x = 0; x * kSubPer < k; ++x) {
+    for (int64_t x = 0; x * kZChunk < k; ++x) {
       zmap.push_back((uint32_t)t);
       zmap.push_back((uint32_t)x);
     }
@@ -3097,14 +3089,8 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
       OMF_HIP(hipStreamWaitEvent(st, hsync->join, 0));
     }
     ++stats.calls;
-    // zero mode: the short tensors completed with their lowest-index zeros (leaves at once unless
-    // the verdict reports a zero fill and no fallback)
-    if (tb.nzb > 0 && !forced)
-      hipLaunchKernelGGL(topk_zero_fill, dim3(std::min<uint32_t>((uint32_t)tb.nzb, kZeroFillGrid)), dim3(kSubThreads), 0,
-                         st, (const uint2*)tb.zmap, (uint32_t)tb.nzb, status, zcnt, kk, koff, d_begins, d_sizes, tfirst,
-                         items, sub_cnt, cand, tp, scale, rz, values, indices);
-    // the fallback (a redo, a fine bin over what a bucket holds, or forced), decided and run on the
-    // device: leaves at once on a fast-path verdict
+    // the zero fill and the fallback (a redo, a fine bin over what a bucket holds, or forced),
+    // decided and run on the device: leaves at once on a plain fast-path verdict
     TailArgs ta;
     ta.tp = tp;
     ta.scale = scale;
@@ -3134,6 +3120,10 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     ta.indices = indices;
     ta.stats = dstats;
     ta.err = omf_plan_access::err_word(plan);
+    ta.zmap = (const uint2*)tb.zmap;
+    ta.nzc = (uint32_t)tb.nzb;
+    ta.zcnt = zcnt;
+    ta.tsize = d_sizes;
     hipLaunchKernelGGL(topk_exact_tail, dim3(tail_grid(omf_plan_access::device(plan))), dim3(kThreads), 0, st, ta);
     OMF_HIP(hipGetLastError());
     (void)tmp_bytes;

@@ -6,7 +6,7 @@ the average of the clients' zero-filled Top-K decodes (``global_grpc_server.py:1
 213-234``): at most C·k non-zeros per tensor.  With fewer than ~1.4 k non-zeros the sampled
 threshold used to land in the zero bin and every element became a candidate (the radix-sort
 fallback, ~25 ms on Llama-400M).  Zero mode takes every non-zero as a candidate and completes a
-tensor with fewer than k of them by its lowest-index zeros (``topk_zero_fill``).  These tests
+tensor with fewer than k of them by its lowest-index zeros (the exact tail's ``zero_fill_chunk``).  These tests
 check that the fast path is taken (the plan's verdict counters) and that its bytes — values,
 indices, error-feedback residual — equal the device-wide radix-sort fallback's, which the other
 Top-K tests pin to ``torch.topk`` and the reference's goldens; and, on small cases, the oracle.
