@@ -28,10 +28,12 @@ def load(d, counter):
     return per
 
 
-# one encode call's launches: the planned scatter (the default since round 5), or plan + scatter
-TOPK_ENCODE_SETS = (("topk_sample", "topk_fused", "topk_fine_hist", "topk_scatter_planned", "topk_bucket_sort"),
+# one encode call's launches: the planned scatter (the default since round 5), or plan + scatter;
+# since round 6 the exact tail (zero fill, fallback) ends every call
+TOPK_ENCODE_SETS = (("topk_sample", "topk_fused", "topk_fine_hist", "topk_scatter_planned", "topk_bucket_sort",
+                     "topk_exact_tail"),
                     ("topk_sample", "topk_fused", "topk_fine_hist", "topk_plan", "topk_bucket_scatter",
-                     "topk_bucket_sort"))
+                     "topk_bucket_sort", "topk_exact_tail"))
 TOPK_ENCODE = tuple(sorted(set(TOPK_ENCODE_SETS[0] + TOPK_ENCODE_SETS[1])))
 TOPK_DECODE = ("topk_dec_place", "topk_dec_tiles", "topk_dec_overflow")
 
