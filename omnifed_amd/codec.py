@@ -504,9 +504,11 @@ class Plan:
 
         ``alpha``: the client weighting (t' = residual + fl32(alpha * x)), fused in.
         ``tie_order``: "index" — the device selection alone, (|t'| descending, index ascending),
-        asynchronous on the stream; "torch" — then ``omf_topk_torch_order``: where magnitudes tie,
-        which of them are selected and their order are torch's CPU ``topk`` (the reference's bytes;
-        synchronises the stream).  Without ties the two are the same bytes."""
+        asynchronous on the stream (the fallback too: ``omf_plan_check`` reports an exact-tail
+        barrier expiry, never expected); "torch" — then ``omf_topk_torch_order``: where magnitudes
+        tie, which of them are selected and their order are torch's CPU ``topk`` (the reference's
+        bytes; synchronises the stream, then checks the plan).  Without ties the two are the same
+        bytes."""
         if tie_order not in ("index", "torch"):
             raise ValueError(f"tie_order must be 'index' or 'torch', not {tie_order!r}")
         dev = self.device
@@ -544,6 +546,8 @@ class Plan:
                                              ctypes.c_void_p(st), ctypes.byref(nre)),
                       "omf_topk_torch_order")
                 self.topk_reordered = int(nre.value)
+        if tie_order == "torch":  # (the stream is synchronised already) an exact-tail barrier expiry raises
+            self.check(st)
         return values, indices, ks
 
 

@@ -482,6 +482,8 @@ def _encode_topk_updates(updates, compressor: TopKCompression, weight) -> list:
             t = i - nt
             layers[t] = topk_layer_from_bytes(names[t], tuple(updates[names[t]].shape), vals[t], payload)
             vals[t] = None
+    if compressor.tie_order != "torch":  # (torch order checked the plan already) an exact-tail expiry raises
+        plan.check()
     return layers
 
 
