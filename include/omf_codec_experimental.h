@@ -66,7 +66,9 @@ int omf_plan_spec_stats(omf_plan* plan, void* stream, int64_t* out4);
 /* Test / experiment hook of the plan's Top-K encoder (never needed in production; an experiment
  * build also reads them from the OMF_TOPK_* environment, once, at the plan's first Top-K call).  Every
  * setting changes only how the exact selection is found, never what it is: groups (>= 1) = the
- * two-stream group pipeline, force_fallback (0 / 1) = always the device-wide radix sort,
+ * two-stream group pipeline, force_fallback (0 / 1) = always the exact tail's device-wide radix sort
+ * (2: the same, with one tail workgroup skipping its first barrier arrival — the test of the bound's
+ * expiry: the call's selection is invalid and omf_plan_check reports OMF_ETIMEOUT),
  * sample_runs (0 = default, or 64..2^20) = sampled runs per tensor, sure_z / sure_c = the sure
  * bin's margin.  A negative argument keeps the current setting. */
 int omf_plan_set_topk(omf_plan* plan, int32_t groups, int32_t force_fallback, int64_t sample_runs, float sure_z,

@@ -169,8 +169,10 @@ class Plan:
 
     def set_topk(self, groups: int = -1, fallback: int = -1, sample_runs: int = -1, sure=None) -> None:
         """Test / experiment hook of the Top-K encoder (omf_plan_set_topk): the group pipeline,
-        the forced radix-sort fallback, the sample size (0 = default), the sure margin (z, c).
-        None of them changes the selection; -1 / None keeps a setting."""
+        the forced fallback (1: the exact tail's radix sort; 2: the same with a forced barrier
+        expiry, the test of its bound), the sample size (0 = default), the sure margin (z, c).
+        None of them changes the selection (fallback 2 invalidates it and makes ``check`` raise);
+        -1 / None keeps a setting."""
         z, c = (-1.0, -1.0) if sure is None else (float(sure[0]), float(sure[1]))
         with self._lock:
             check(lib().omf_plan_set_topk(self._h, int(groups), int(fallback), int(sample_runs), z, c),

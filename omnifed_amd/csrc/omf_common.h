@@ -32,7 +32,7 @@ struct TopkKnobs {
   bool init = false;
   int32_t groups = 1;          // two-stream group pipeline (off: measured slower)
   int32_t dbg = 0;             // OMF_TOPK_DBG diagnostics
-  int32_t force_fallback = 0;  // always take the device-wide radix-sort path (tests of that path)
+  int32_t force_fallback = 0;  // 1: always the exact tail's radix sort; 2: and a barrier expiry (tests)
   int64_t sample_runs = 0;     // sampled runs per tensor at most (0: the default, 2 Ki)
   float sure_z = 1.5f, sure_c = 2.0f;  // the "sure" bin's margin below the expected rank-k count
   bool scatter_small = true;   // the bucket scatter's LDS-staged bucket table (OMF_TOPK_SCATTER_SMALL=0 off)

@@ -1885,6 +1885,7 @@ struct TailArgs {
   int64_t n_items;
   int32_t nt;
   int32_t forced;
+  int32_t skip_arrival;  // test hook (omf_plan_set_topk force_fallback 2): the last workgroup skips barrier 1
   const int64_t *kk, *koff, *tbegin;
   const uint32_t *tfirst, *tlast;
   uint32_t *sub_cnt, *item_cnt, *item_off, *cnt, *flag, *hist, *bin;
@@ -1911,7 +1912,8 @@ __device__ bool tail_sync(const TailArgs& a, uint32_t& epoch) {
   ++epoch;
   if (threadIdx.x == 0) {
     __threadfence();
-    __hip_atomic_fetch_add(&a.status[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!(a.skip_arrival && epoch == 1 && blockIdx.x == gridDim.x - 1))
+      __hip_atomic_fetch_add(&a.status[4], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t target = epoch * gridDim.x;
     const uint64_t t0 = wall_clock64();
     uint32_t ok = 1, polls = 0;
@@ -2895,7 +2897,8 @@ int omf_plan_set_topk(omf_plan* plan, int32_t groups, int32_t force_fallback, in
   (void)knobs(plan);  // the environment's values first, so a negative argument keeps them
   TopkKnobs& k = omf_plan_access::topk_knobs(plan);
   if (groups >= 1) k.groups = groups;
-  if (force_fallback >= 0) k.force_fallback = force_fallback != 0;
+  if (force_fallback > 2) return fail(OMF_EINVAL, "omf_plan_set_topk: force_fallback must be 0, 1 or 2");
+  if (force_fallback >= 0) k.force_fallback = force_fallback;
   if (sample_runs >= 0) k.sample_runs = sample_runs;
   if (sure_z >= 0.f) k.sure_z = sure_z;
   if (sure_c >= 0.f) k.sure_c = sure_c;
@@ -3099,6 +3102,7 @@ int omf_topk_encode(omf_plan* plan, const float* x, float* residual, int32_t res
     ta.n_items = n_items;
     ta.nt = nt;
     ta.forced = forced ? 1 : 0;
+    ta.skip_arrival = kn.force_fallback == 2 ? 1 : 0;
     ta.kk = kk;
     ta.koff = koff;
     ta.tbegin = d_begins;

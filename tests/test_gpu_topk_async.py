@@ -184,3 +184,40 @@ def test_encode_graph_capture_replays_same_bytes(gpu):
         assert torch.equal(si, i), j
         assert sv.cpu().numpy().tobytes() == v.cpu().numpy().tobytes(), j
         assert sres.cpu().numpy().tobytes() == r.cpu().numpy().tobytes(), j
+
+
+def test_exact_tail_barrier_expiry_is_reported_and_recovers(gpu):
+    """The tail's grid barrier is bounded: with one workgroup withholding its first arrival (test
+    hook, force_fallback 2) every workgroup gives up after the bound (~0.2 s), the plan's error word
+    makes ``check`` raise, and the barrier words are reset — the next call's bytes are right."""
+    from omnifed_amd._lib import CodecError
+
+    sizes = [1 << 20, 70000, 3 << 20]
+    plan = codec.Plan(sizes, device=gpu)
+    x = _arena(plan, gpu, 40)
+    r0 = _arena(plan, gpu, 41, 0.1)
+    want_res = r0.clone()
+    wv, wi, _ = plan.topk_encode(x, 0.01, residual=want_res, residual_mode=1)
+    torch.cuda.synchronize()
+    plan.set_topk(fallback=2)
+    try:
+        res = r0.clone()
+        plan.topk_encode(x, 0.01, residual=res, residual_mode=1)
+        torch.cuda.synchronize()
+    finally:
+        plan.set_topk(fallback=0)
+    with pytest.raises(CodecError, match="exact tail"):
+        plan.check()
+    assert plan.check()  # reported once
+    for fb in (1, 0):  # the tail runs again, whole, then the fast path
+        plan.set_topk(fallback=fb)
+        try:
+            res = r0.clone()
+            v, i, _ = plan.topk_encode(x, 0.01, residual=res, residual_mode=1)
+            torch.cuda.synchronize()
+        finally:
+            plan.set_topk(fallback=0)
+        msg = _same("indices", i.cpu(), wi.cpu()) + _same("values", v.cpu(), wv.cpu()) + \
+            _same("residual", res.cpu(), want_res.cpu())
+        assert not msg, (fb, msg)
+        assert plan.check()
