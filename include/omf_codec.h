@@ -63,7 +63,7 @@ extern "C" {
 typedef struct omf_plan omf_plan;
 
 /* ABI version (major*100 + minor). */
-#define OMF_ABI_VERSION 111
+#define OMF_ABI_VERSION 112
 int omf_abi_version(void);
 
 /* Last error message of the calling thread ("" if none). */
@@ -372,6 +372,16 @@ int omf_topk_decode_counts(omf_plan* plan, const int64_t* counts, const float* v
  * when every index is in range.  Asynchronous on `stream`.
  */
 int omf_topk_check_indices(omf_plan* plan, const int64_t* counts, int64_t* indices, int32_t* bad, void* stream);
+/*
+ * Repeated indices of the same received message (after omf_topk_check_indices has wrapped them):
+ * flags[t] (DEVICE int32[ntensors], written) = 1 when an in-range index of tensor t appears more
+ * than once.  The reference decodes a layer as dense[indices] = values, where numpy keeps the LAST
+ * value of a repeated index (global_grpc_compression.py:140-160); the scatter decodes do not, so the
+ * Python layer decodes a flagged layer by itself with that rule.  Never true for a selection an
+ * encoder produced.  Uses a plan-owned bitmap of arena_end bits (made on first use).  Asynchronous.
+ */
+int omf_topk_check_duplicates(omf_plan* plan, const int64_t* counts, const int64_t* indices, int32_t* flags,
+                              void* stream);
 
 #ifdef __cplusplus
 }

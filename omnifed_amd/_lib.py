@@ -81,6 +81,7 @@ SIGNATURES = {
     "omf_topk_decode_counts": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64), _c_p, _c_p, _c_p, _c_i32, _c_p, _c_size,
                                               _c_p]),
     "omf_topk_check_indices": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64), _c_p, _c_p, _c_p]),
+    "omf_topk_check_duplicates": (ctypes.c_int, [_c_p, ctypes.POINTER(_c_i64), _c_p, _c_p, _c_p]),
 }
 
 _lock = threading.Lock()
@@ -91,7 +92,7 @@ class CodecError(RuntimeError):
     pass
 
 
-ABI_VERSION = 111  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
+ABI_VERSION = 112  # include/omf_codec.h OMF_ABI_VERSION; a library of another version is refused
 
 
 def lib() -> ctypes.CDLL:

@@ -633,6 +633,20 @@ class Plan:
                   "omf_topk_check_indices")
         return bad
 
+    def topk_check_duplicates(self, counts: Sequence[int], indices: torch.Tensor,
+                              stream: Optional[int] = None) -> torch.Tensor:
+        """omf_topk_check_duplicates: a device int32 per tensor, 1 where an (in-range) index of the
+        message repeats (run after ``topk_check_indices``).  Asynchronous."""
+        arr, ktot, _ = self._counts(counts)
+        dev = self.device
+        _need(indices, "indices", torch.int64, dev, ktot, 8)
+        flags = torch.empty(self.nt, dtype=torch.int32, device=dev)
+        st = stream if stream is not None else _stream(dev)
+        with self._lock:
+            check(lib().omf_topk_check_duplicates(self._h, arr, _ptr(indices), _ptr(flags), ctypes.c_void_p(st)),
+                  "omf_topk_check_duplicates")
+        return flags
+
     def topk_decode_counts(self, counts: Sequence[int], values: torch.Tensor, indices: torch.Tensor,
                            y: Optional[torch.Tensor] = None, mode: int = 0, stream: Optional[int] = None) -> torch.Tensor:
         """Decode one received message's Top-K selection (per-tensor sizes ``counts``, packed in plan

@@ -2259,6 +2259,34 @@ __global__ __launch_bounds__(kThreads) void topk_check_idx(int64_t* __restrict__
   if ((threadIdx.x & 63) == 0 && lowest != 0x7fffffff) atomicMin(bad, lowest);
 }
 
+// Repeated indices of a received selection (omf_topk_check_duplicates): the reference decodes a
+// layer as dense[indices] = values (numpy: the last value of a repeated index wins), which a
+// scatter does not reproduce.  MARK sets each (in-range, wrapped) index's bit of an arena bitmap
+// (plan-owned, all zero between calls) and flags the tensor whose bit was already set; the clear
+// pass resets the bits it touched, so the bitmap is zero again for the next call.
+template <bool MARK>
+__global__ __launch_bounds__(kThreads) void topk_dup_bits(const int64_t* __restrict__ indices,
+                                                          const int64_t* __restrict__ sizes,
+                                                          const int64_t* __restrict__ tbegin,
+                                                          const int64_t* __restrict__ koff_g, int nt, int64_t ktot,
+                                                          uint32_t* __restrict__ bits, int32_t* __restrict__ flags) {
+  __shared__ int64_t koff[kArenaMaxTensors + 1];
+  for (int t = threadIdx.x; t <= nt; t += kThreads) koff[t] = koff_g[t];
+  __syncthreads();
+  for (int64_t j = (int64_t)blockIdx.x * kThreads + threadIdx.x; j < ktot; j += (int64_t)gridDim.x * kThreads) {
+    const int t = koff_tensor(koff, nt, j);
+    const int64_t i = indices[j];
+    if (i < 0 || i >= sizes[t]) continue;  // out of range: omf_topk_check_indices reports it
+    const uint64_t pos = (uint64_t)(tbegin[t] + i);
+    const uint32_t b = 1u << (pos & 31);
+    if (MARK) {
+      if (atomicOr(&bits[pos >> 5], b) & b) flags[t] = 1;
+    } else {
+      atomicAnd(&bits[pos >> 5], ~b);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- tiled zero-fill decode (mode 0)
 // y := 0 over the whole arena, then y[begin_t + idx] = v for one client's selection, as ONE
 // streaming write of the arena: the scattered 4-byte stores of a fill-then-scatter decode reach
@@ -3571,6 +3599,38 @@ int omf_topk_check_indices(omf_plan* plan, const int64_t* counts, int64_t* indic
   const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ktot + 4 * kThreads - 1) / (4 * kThreads), 2048));
   hipLaunchKernelGGL(topk_check_idx, dim3(gx), dim3(kThreads), 0, st, indices, omf_plan_access::d_sizes(plan),
                      (const int64_t*)tb.koff, (int)nt, ktot, bad);
+  OMF_HIP(hipGetLastError());
+  return OMF_OK;
+}
+
+int omf_topk_check_duplicates(omf_plan* plan, const int64_t* counts, const int64_t* indices, int32_t* flags,
+                              void* stream) {
+  if (!plan) return fail(OMF_EINVAL, "plan is NULL");
+  if (!flags) return fail(OMF_EINVAL, "omf_topk_check_duplicates: flags is NULL");
+  int64_t ktot = 0;
+  if (int r = check_counts(plan, counts, &ktot)) return r;
+  if (ktot && !indices) return fail(OMF_EINVAL, "omf_topk_check_duplicates: indices is NULL");
+  const int32_t nt = omf_plan_access::ntensors(plan);
+  if (nt > kArenaMaxTensors) return fail(OMF_EINVAL, "omf_topk_check_duplicates: too many tensors");
+  DeviceGuard g(omf_plan_access::device(plan));
+  if (!g.ok) return fail(OMF_EHIP, "hipSetDevice failed");
+  hipStream_t st = (hipStream_t)stream;
+  OMF_HIP(hipMemsetAsync(flags, 0, 4 * (size_t)nt, st));
+  if (ktot == 0) return OMF_OK;
+  DecTables tb;
+  if (int r = dec_tables(plan, counts, ktot, nullptr, &tb)) return r;
+  constexpr uint64_t kDupTag = 0xD0B1E5B17A9E0000ull;
+  const size_t words = (size_t)((omf_plan_access::arena_end(plan) + 31) / 32);
+  bool fresh = false;
+  uint64_t* host = nullptr;
+  uint32_t* bits = static_cast<uint32_t*>(omf_plan_access::topk_table(plan, kDupTag, 4 * words, &fresh, &host));
+  if (!bits) return fail(OMF_ENOMEM, "omf_topk_check_duplicates: bitmap allocation failed");
+  if (fresh) OMF_HIP(hipMemsetAsync(bits, 0, 4 * words, st));
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((ktot + kThreads - 1) / kThreads, 2048));
+  hipLaunchKernelGGL(topk_dup_bits<true>, dim3(gx), dim3(kThreads), 0, st, indices, omf_plan_access::d_sizes(plan),
+                     omf_plan_access::d_begins(plan), (const int64_t*)tb.koff, (int)nt, ktot, bits, flags);
+  hipLaunchKernelGGL(topk_dup_bits<false>, dim3(gx), dim3(kThreads), 0, st, indices, omf_plan_access::d_sizes(plan),
+                     omf_plan_access::d_begins(plan), (const int64_t*)tb.koff, (int)nt, ktot, bits, flags);
   OMF_HIP(hipGetLastError());
   return OMF_OK;
 }

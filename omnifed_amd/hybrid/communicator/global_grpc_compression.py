@@ -268,8 +268,11 @@ def _last_wins(v: torch.Tensor, ix: torch.Tensor, n: int):
     return v[keep], ix[keep]
 
 
-def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, device=None) -> torch.Tensor:
-    """global_grpc_compression.py:140-160: overlay on ``base_tensor`` or zero-filled dense."""
+def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, device=None,
+                       last_wins: bool = False) -> torch.Tensor:
+    """global_grpc_compression.py:140-160: overlay on ``base_tensor`` or zero-filled dense.
+    ``last_wins``: the layer repeats an index (omf_topk_check_duplicates): numpy's rule, the last
+    value per index (always applied when there are more values than elements)."""
     if not layer.values_data or not layer.indices_data:
         raise ValueError(f"Compressed layer {layer.layer_name!r} missing values/indices")
     values = np.frombuffer(layer.values_data, dtype=np.float32)
@@ -286,7 +289,7 @@ def _decode_topk_layer(layer, *, base_tensor: Optional[torch.Tensor] = None, dev
     dev = _gpu_for(out_dev)
     v = torch.from_numpy(values.copy()).to(dev)
     ix = torch.from_numpy(np.array(indices, dtype=np.int64, copy=True)).to(dev)
-    if ix.numel() > numel:
+    if last_wins or ix.numel() > numel:
         v, ix = _last_wins(v, ix, numel)
     if base_tensor is not None:
         # the reference overlays a numpy copy of the base, so the result has the base's dtype
@@ -739,14 +742,21 @@ def check_topk_indices(plan, counts, indices, names) -> None:
 
 def _decode_topk_batch(topk, dev: torch.device):
     """Decode a message's Top-K layers (zero-filled, no base) in one call: returns the decoded
-    fp32 arena and the plan (layer t at ``[plan.offsets[t], + plan.sizes[t])``)."""
+    fp32 arena and the plan (layer t at ``[plan.offsets[t], + plan.sizes[t])``).  A layer that
+    repeats an index is decoded again by itself with numpy's last-value rule (never for a
+    selection an encoder produced)."""
     plan = codec.Plan.get([_layer_numel(L) for L, *_ in topk], device=dev)
     counts, values, indices = stage_topk([(v, i) for _L, v, i, _k in topk], dev, "topk_decode")
     bad = plan.topk_check_indices(counts, indices)
+    dup = plan.topk_check_duplicates(counts, indices)
     y = plan.topk_decode_counts(counts, values, indices, mode=0)  # out-of-range indices are skipped
-    b = int(bad.item())  # synchronises: the staging is free again
+    flags = torch.cat([bad, dup]).cpu()  # synchronises: the staging is free again
+    b = int(flags[0])
     if b < plan.nt:
         raise IndexError(f"Compressed layer {topk[b][0].layer_name!r}: index out of bounds for size {plan.sizes[b]}")
+    for t in flags[1:].nonzero().flatten().tolist():
+        o, n = plan.offsets[t], plan.sizes[t]
+        y[o:o + n] = _decode_topk_layer(topk[t][0], device=dev, last_wins=True).reshape(-1)
     return y, plan
 
 
@@ -837,6 +847,7 @@ def _overlay_topk_into(topk, targets) -> set:
     plan = codec.Plan.get([_layer_numel(L) for L, *_ in mine], device=dev)
     counts, values, indices = stage_topk([(v, i) for _L, v, i, _k in mine], dev, "topk_overlay")
     check_topk_indices(plan, counts, indices, names)
+    dup = plan.topk_check_duplicates(counts, indices)
     flats = [targets[n].detach().reshape(-1) for n in names]
     from ..compression.core import shared_arena
 
@@ -848,6 +859,13 @@ def _overlay_topk_into(topk, targets) -> set:
         for f, k in zip(flats, counts):
             codec.topk_decode(values[K:K + k], indices[K:K + k], f.numel(), y=f, mode=1)
             K += k
+    rep = dup.nonzero().flatten().tolist()  # (synchronises) layers that repeat an index: the last value wins
+    koff = [0]
+    for k in counts:
+        koff.append(koff[-1] + int(k))
+    for t in rep:
+        v, ix = _last_wins(values[koff[t]:koff[t + 1]], indices[koff[t]:koff[t + 1]], plan.sizes[t])
+        codec.topk_decode(v.contiguous(), ix.contiguous(), flats[t].numel(), y=flats[t], mode=1)
     return {id(L) for L, *_ in mine}
 
 

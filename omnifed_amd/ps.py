@@ -203,6 +203,15 @@ class DeviceAggregator:
                 pairs[i] = (v, ix)
             counts, values, indices = stage_topk(pairs, self.device, "ps_topk")
             check_topk_indices(self.plan, counts, indices, self.names)  # synchronises
+            dup = self.plan.topk_check_duplicates(counts, indices).cpu()
+            rep = [L for L in topk if dup[self.index[L.layer_name]]]
+            if rep:  # a layer repeating an index (never an encoder's): alone, numpy's last value per index
+                odd_args += [(L.layer_name, _decode_topk_layer(L, device=self.device, last_wins=True).reshape(-1))
+                             for L in rep]
+                for L in rep:
+                    pairs[self.index[L.layer_name]] = (b"", b"")
+                counts, values, indices = stage_topk(pairs, self.device, "ps_topk")
+                check_topk_indices(self.plan, counts, indices, self.names)
             t_args = (counts, values, indices)
         dense_args = []
         for L in dense:
