@@ -20,12 +20,16 @@
 //                       every |t'| at or above the threshold as index << 32 | bits(t') to the
 //                       512-element sub-chunk's own range (one block scan, no atomics).
 //   3. topk_fine_hist   exact fine-bin histogram of the candidates (LDS per super-item).
-//   4. topk_plan        per tensor: the fine bins above rank k -> buckets of <= 4096 keys with
-//                       known first ranks; the last block publishes the verdict to host memory.
-//   5. topk_bucket_scatter / topk_bucket_sort: keys into buckets, an LDS sort per bucket ->
-//                       values / int64 indices (torch's partial-sort order), residual fix-ups.
-//   6. fallback (a verdict flag, rare): exact redo of flagged tensors, one rocPRIM radix sort
-//                       of (index << 39 | tensor << 31 | 2^31-1 - |t'|bits), a gather.
+//   4. topk_scatter_planned (topk_plan + topk_bucket_scatter for large plans): per tensor, the fine
+//                       bins above rank k -> buckets of <= 4096 keys with known first ranks, the
+//                       verdict words (zero fill / redo / overflow) in the workspace; keys into buckets.
+//   5. topk_bucket_sort an LDS sort per bucket -> values / int64 indices ((|t'| desc, index asc)),
+//                       residual fix-ups.
+//   6. topk_exact_tail  always enqueued (no host wait: the call is stream-asynchronous): reads the
+//                       verdict; the zero fill when it reports one; on a fallback (rare) the exact
+//                       path behind grid barriers — redo of flagged tensors, an LSD radix sort of
+//                       (index << 39 | tensor << 31 | 2^31-1 - |t'|bits) sized by the device's own
+//                       candidate count, a gather.
 // Larger plans take the exact path (histogram of every t', collection, a segmented
 // descending sort of (|t'|bits << 32 | ~index) per tensor).
 // Decode is a scatter (mode 0 zero-fill, 1 overlay, 2 scatter-add); the arena zero-fill decode

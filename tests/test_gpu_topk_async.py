@@ -221,3 +221,53 @@ def test_exact_tail_barrier_expiry_is_reported_and_recovers(gpu):
             _same("residual", res.cpu(), want_res.cpu())
         assert not msg, (fb, msg)
         assert plan.check()
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_exact_tail_randomized_against_fast_path(gpu, seed):
+    """Random plans (1-40 tensors of 1 to 300 k elements), ratios from 0.1 % to 25 %, Gaussian,
+    tie-heavy (quantised), zero-heavy and inf-salted inputs, every residual mode and a random
+    weighting: the forced exact tail, the default path and torch.topk's magnitudes agree."""
+    g = torch.Generator().manual_seed(1000 + seed)
+    nt = int(torch.randint(1, 41, (1,), generator=g))
+    ratio = [0.001, 0.01, 0.05, 0.25][seed % 4]
+    sizes = [int(v) for v in torch.randint(1, 300_000, (nt,), generator=g)]
+    sizes = [max(n, int(1 / ratio) + 1) for n in sizes]  # k >= 1 always; keep k <= n
+    plan = codec.Plan(sizes, device=gpu)
+    kind = seed % 3
+    x = torch.randn(plan.arena_end, generator=g)
+    if kind == 1:
+        x = torch.round(x * 8) / 8  # ties everywhere
+    elif kind == 2:
+        x[torch.rand(plan.arena_end, generator=g) < 0.995] = 0.0  # fewer non-zeros than k
+    if seed % 5 == 0:
+        x[torch.randint(0, plan.arena_end, (7,), generator=g)] = float("inf")
+    mode = seed % 3
+    alpha = float(torch.rand(1, generator=g)) * 3 + 0.5
+    r0 = (torch.randn(plan.arena_end, generator=g) * 0.1).to(gpu)
+    x = x.to(gpu)
+    outs = []
+    for fb in (0, 1):
+        res = r0.clone() if mode else None
+        plan.set_topk(fallback=fb)
+        try:
+            v, i, ks = plan.topk_encode(x, ratio, residual=res, residual_mode=mode, alpha=alpha)
+            torch.cuda.synchronize()
+        finally:
+            plan.set_topk(fallback=0)
+        outs.append((v.cpu(), i.cpu(), None if res is None else res.cpu()))
+    (va, ia, ra), (vb, ib, rb) = outs
+    msg = _same("indices", ia, ib) + _same("values", va, vb)
+    if mode:
+        msg += _same("residual", ra, rb)
+    assert not msg, msg
+    assert plan.check()
+    xh = x.cpu()
+    rh = r0.cpu() if mode == 1 else torch.zeros_like(xh)
+    K = 0
+    for t, (o, n) in enumerate(zip(plan.offsets, sizes)):
+        k = ks[t]
+        tp = rh[o:o + n] + xh[o:o + n] * alpha if mode == 1 else xh[o:o + n] * alpha
+        want, _ = torch.topk(tp.abs(), k, sorted=True)
+        assert torch.equal(va[K:K + k].abs(), want), (seed, t)
+        K += k
