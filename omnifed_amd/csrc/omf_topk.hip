@@ -3218,11 +3218,20 @@ int reorder_tensor(hipStream_t s, const float* src, float* residual, bool ef, fl
     if (e != hipSuccess) *msg = std::string(what) + ": " + hipGetErrorString(e);
     return e == hipSuccess;
   };
+#ifdef OMF_EXP_TIE_TS  // experiment builds: phase times of the large tensors' rewrites
+  const auto ts0 = std::chrono::steady_clock::now();
+  auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::milli>(b - a).count();
+  };
+#endif
   if (!hip(hipMemcpyAsync(tp.data(), src + off, 4 * (size_t)n, hipMemcpyDeviceToHost, s), "t' to host") ||
       !hip(hipMemcpyAsync(v.data(), values, 4 * (size_t)k, hipMemcpyDeviceToHost, s), "values to host") ||
       !hip(hipMemcpyAsync(ix.data(), indices, 8 * (size_t)k, hipMemcpyDeviceToHost, s), "indices to host") ||
       !hip(hipStreamSynchronize(s), "copy to host"))
     return OMF_EHIP;
+#ifdef OMF_EXP_TIE_TS
+  const auto ts1 = std::chrono::steady_clock::now();
+#endif
   if (ef) {
     for (int64_t j = 0; j < k; ++j)
       if (ix[j] >= 0 && ix[j] < n) tp[ix[j]] = v[j];
@@ -3233,12 +3242,42 @@ int reorder_tensor(hipStream_t s, const float* src, float* residual, bool ef, fl
     *msg = omf_last_error();
     return rc;
   }
+#ifdef OMF_EXP_TIE_TS
+  const auto ts2 = std::chrono::steady_clock::now();
+  struct Report {
+    int64_t n;
+    std::chrono::steady_clock::time_point a, b, c;
+    ~Report() {
+      if (n >= (1 << 24))
+        fprintf(stderr, "TIE_TS n=%lld fetch=%.1f select=%.1f writeback=%.1f ms\n", (long long)n,
+                std::chrono::duration<double, std::milli>(b - a).count(),
+                std::chrono::duration<double, std::milli>(c - b).count(),
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c).count());
+    }
+  } report{n, ts0, ts1, ts2};
+  (void)ms;
+#endif
   if (sel == ix) return OMF_OK;
   *changed = true;
   for (int64_t j = 0; j < k; ++j) nv[j] = tp[sel[j]];
   bool same_set = true;
   if (ef) {
-    std::vector<int64_t> a(ix), b(sel);
+    // Both selections are exact top-k multisets of the magnitude keys (every NaN one key), so they
+    // can differ only among the elements whose key is the smallest selected one, T: compare those
+    // index sets (a handful; sorting both whole selections took 30-40 ms on a 32 Mi tensor).
+    auto key = [](float f) {
+      uint32_t u;
+      std::memcpy(&u, &f, 4);
+      u &= 0x7fffffffu;
+      return u > 0x7f800000u ? 0x7fc00000u : u;
+    };
+    uint32_t T = 0xffffffffu;
+    for (int64_t j = 0; j < k; ++j) T = std::min(T, key(v[j]));
+    std::vector<int64_t> a, b;
+    for (int64_t j = 0; j < k; ++j) {
+      if (key(v[j]) == T) a.push_back(ix[j]);
+      if (key(nv[j]) == T) b.push_back(sel[j]);
+    }
     std::sort(a.begin(), a.end());
     std::sort(b.begin(), b.end());
     same_set = a == b;

@@ -24,6 +24,10 @@
 //   - the introselect regime calls std::nth_element on the n pairs with the same comparison.
 // tests/test_topk_order_host.py pins both against torch.topk on tie-heavy inputs (CPU).
 #include <algorithm>
+#ifdef OMF_EXP_TIE_TS
+#include <chrono>
+#include <cstdio>
+#endif
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
@@ -126,16 +130,34 @@ int torch_topk_select(const float* t, int64_t n, int64_t k, int64_t* out) {
     }
     uint32_t* kp = K.data();
     uint32_t* ip = I.data();
+#ifdef OMF_EXP_TIE_TS
+    const auto T0 = std::chrono::steady_clock::now();
+    int64_t nrep = 0;
+#endif
     for (int64_t i = k; i < n; ++i) {
       const uint32_t key = mag_key_host(t[i]);
-      if (key > kp[0]) replace_top(kp, ip, k, key, (uint32_t)i);  // before(pair i, top): it replaces the top
+      if (key > kp[0]) {  // before(pair i, top): it replaces the top
+#ifdef OMF_EXP_TIE_TS
+        ++nrep;
+#endif
+        replace_top(kp, ip, k, key, (uint32_t)i);
+      }
     }
+#ifdef OMF_EXP_TIE_TS
+    const auto T1 = std::chrono::steady_clock::now();
+#endif
     for (int64_t last = k - 1; last > 0; --last) {  // the heap sort: __pop_heap(h, h + last, h + last)
       const uint32_t kv = kp[last], iv = ip[last];
       kp[last] = kp[0];
       ip[last] = ip[0];
       replace_top(kp, ip, last, kv, iv);
     }
+#ifdef OMF_EXP_TIE_TS
+    if (n >= (1 << 24))
+      fprintf(stderr, "TIE_HEAP n=%lld k=%lld replacements=%lld select=%.1f sort=%.1f ms\n", (long long)n, (long long)k,
+              (long long)nrep, std::chrono::duration<double, std::milli>(T1 - T0).count(),
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - T1).count());
+#endif
     for (int64_t j = 0; j < k; ++j) out[j] = (int64_t)ip[j];
     return OMF_OK;
   }
