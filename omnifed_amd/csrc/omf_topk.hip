@@ -44,6 +44,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -3200,12 +3201,64 @@ namespace {
 // back, or fl32(alpha * x)), torch's CPU selection recomputed on the host, and the tensor's values /
 // indices (and, when the selected set changed, its residual) written back.  Returns OMF_OK or an
 // error with *msg set (the worker's thread-local error string is not the caller's).
+#ifdef OMF_EXP_TIE_TS
+std::atomic<int64_t> g_tie_us[3];  // summed over the call's tensors: fetch, select, write-back
+#endif
+// Host buffers for t', kept from one omf_topk_torch_order call to the next (a fresh 128 MB array per
+// 32 Mi-element tensor cost its zero fill and page faults on every call).  A tensor takes the smallest
+// kept buffer that holds it, else a new one; at most kTieKeepBytes stay kept (a released buffer beyond
+// that is freed).  Never zero-filled: the copy writes every element.
+constexpr size_t kTieKeepBytes = (size_t)768 << 20;
+struct TieBuf {
+  std::unique_ptr<float[]> p;
+  size_t cap = 0;
+};
+std::mutex g_tie_mu;
+std::vector<TieBuf> g_tie_pool;
+size_t g_tie_kept = 0;
+TieBuf tie_acquire(size_t n) {
+  TieBuf b;
+  {
+    std::lock_guard<std::mutex> lk(g_tie_mu);
+    int best = -1;  // the smallest kept buffer of >= n floats
+    for (int i = 0; i < (int)g_tie_pool.size(); ++i)
+      if (g_tie_pool[i].cap >= n && (best < 0 || g_tie_pool[i].cap < g_tie_pool[best].cap)) best = i;
+    if (best >= 0) {
+      b = std::move(g_tie_pool[best]);
+      g_tie_pool.erase(g_tie_pool.begin() + best);
+      g_tie_kept -= 4 * b.cap;
+    }
+  }
+  if (!b.p) {  // none kept holds it: a new one (the kept ones stay for smaller tensors)
+    b.p.reset(new (std::nothrow) float[std::max<size_t>(n, 1)]);
+    b.cap = b.p ? std::max<size_t>(n, 1) : 0;
+  }
+  return b;
+}
+void tie_release(TieBuf&& b) {
+  if (!b.p) return;
+  std::lock_guard<std::mutex> lk(g_tie_mu);
+  if (g_tie_kept + 4 * b.cap > kTieKeepBytes) return;  // freed
+  g_tie_kept += 4 * b.cap;
+  g_tie_pool.push_back(std::move(b));
+}
+struct TieLease {
+  TieBuf b;
+  explicit TieLease(size_t n) : b(tie_acquire(n)) {}
+  ~TieLease() { tie_release(std::move(b)); }
+  float* data() { return b.p.get(); }
+  float& operator[](size_t i) { return b.p[i]; }
+};
 int reorder_tensor(hipStream_t s, const float* src, float* residual, bool ef, float alpha, int64_t off, int64_t n,
                    int64_t k, float* values, int64_t* indices, bool* changed, std::string* msg) {
-  std::vector<float> tp, v, nv;
+#ifdef OMF_EXP_TIE_TS  // experiment builds: phase times of the rewrites (allocation counted as fetch)
+  const auto ts0 = std::chrono::steady_clock::now();
+#endif
+  TieLease tp((size_t)n);
+  std::vector<float> v, nv;
   std::vector<int64_t> ix, sel;
   try {
-    tp.resize((size_t)n);
+    if (!tp.data()) throw std::bad_alloc();
     v.resize((size_t)k);
     nv.resize((size_t)k);
     ix.resize((size_t)k);
@@ -3218,12 +3271,6 @@ int reorder_tensor(hipStream_t s, const float* src, float* residual, bool ef, fl
     if (e != hipSuccess) *msg = std::string(what) + ": " + hipGetErrorString(e);
     return e == hipSuccess;
   };
-#ifdef OMF_EXP_TIE_TS  // experiment builds: phase times of the large tensors' rewrites
-  const auto ts0 = std::chrono::steady_clock::now();
-  auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
-    return std::chrono::duration<double, std::milli>(b - a).count();
-  };
-#endif
   if (!hip(hipMemcpyAsync(tp.data(), src + off, 4 * (size_t)n, hipMemcpyDeviceToHost, s), "t' to host") ||
       !hip(hipMemcpyAsync(v.data(), values, 4 * (size_t)k, hipMemcpyDeviceToHost, s), "values to host") ||
       !hip(hipMemcpyAsync(ix.data(), indices, 8 * (size_t)k, hipMemcpyDeviceToHost, s), "indices to host") ||
@@ -3248,6 +3295,10 @@ int reorder_tensor(hipStream_t s, const float* src, float* residual, bool ef, fl
     int64_t n;
     std::chrono::steady_clock::time_point a, b, c;
     ~Report() {
+      const auto d = std::chrono::steady_clock::now();
+      g_tie_us[0] += std::chrono::duration_cast<std::chrono::microseconds>(b - a).count();
+      g_tie_us[1] += std::chrono::duration_cast<std::chrono::microseconds>(c - b).count();
+      g_tie_us[2] += std::chrono::duration_cast<std::chrono::microseconds>(d - c).count();
       if (n >= (1 << 24))
         fprintf(stderr, "TIE_TS n=%lld fetch=%.1f select=%.1f writeback=%.1f ms\n", (long long)n,
                 std::chrono::duration<double, std::milli>(b - a).count(),
@@ -3255,7 +3306,6 @@ int reorder_tensor(hipStream_t s, const float* src, float* residual, bool ef, fl
                 std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c).count());
     }
   } report{n, ts0, ts1, ts2};
-  (void)ms;
 #endif
   if (sel == ix) return OMF_OK;
   *changed = true;
@@ -3383,10 +3433,19 @@ int omf_topk_torch_order(omf_plan* plan, const float* x, float* residual, int32_
     }
     (void)hipStreamDestroy(s);
   };
+#ifdef OMF_EXP_TIE_TS
+  for (auto& g : g_tie_us) g = 0;
+  const auto tw0 = std::chrono::steady_clock::now();
+#endif
   std::vector<std::thread> pool;
   for (int i = 1; i < nw; ++i) pool.emplace_back(work);
   work();
   for (std::thread& th : pool) th.join();
+#ifdef OMF_EXP_TIE_TS
+  fprintf(stderr, "TIE_CALL tensors=%zu workers=%d wall=%.1f ms  sums: fetch=%.1f select=%.1f writeback=%.1f ms\n",
+          todo.size(), nw, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count(),
+          g_tie_us[0] / 1e3, g_tie_us[1] / 1e3, g_tie_us[2] / 1e3);
+#endif
   if (err) return fail(err, err_msg);
   if (n_reordered) *n_reordered = changed_count.load();
   return OMF_OK;
