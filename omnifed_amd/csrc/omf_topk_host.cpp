@@ -23,6 +23,8 @@
 //     built; keys and indices live in two arrays, the walk reading keys only;
 //   - the introselect regime calls std::nth_element on the n pairs with the same comparison.
 // tests/test_topk_order_host.py pins both against torch.topk on tie-heavy inputs (CPU).
+#include <immintrin.h>
+
 #include <algorithm>
 #ifdef OMF_EXP_TIE_TS
 #include <chrono>
@@ -106,6 +108,43 @@ inline void replace_top(uint32_t* __restrict K, uint32_t* __restrict I, int64_t 
   I[hole] = iv;
 }
 
+// The heap select's pass over t[k, n): every element whose key beats the heap's top replaces the top,
+// in index order.  The top only grows, so an element whose key does not beat the top as it was at the
+// start of its group of 8 cannot beat it later: the AVX2 pass compares 8 keys at once against that top
+// and visits, in order, only the lanes that beat it (each re-checked against the current top) — the
+// same replacements in the same order as the scalar loop, about a third of the groups visited at k = 1 %.
+inline void heap_pass_scalar(const float* t, int64_t k, int64_t n, uint32_t* kp, uint32_t* ip, int64_t len) {
+  for (int64_t i = k; i < n; ++i) {
+    const uint32_t key = mag_key_host(t[i]);
+    if (key > kp[0]) replace_top(kp, ip, len, key, (uint32_t)i);  // before(pair i, top): it replaces the top
+  }
+}
+__attribute__((target("avx2"))) void heap_pass_avx2(const float* t, int64_t k, int64_t n, uint32_t* kp, uint32_t* ip,
+                                                    int64_t len) {
+  const __m256i abs_mask = _mm256_set1_epi32(0x7fffffff), inf = _mm256_set1_epi32(0x7f800000),
+                nan_key = _mm256_set1_epi32(0x7fc00000);
+  int64_t i = k;
+  for (; i < n && (i & 7); ++i) {  // to an 8-element boundary of t (aligned loads below when t is)
+    const uint32_t key = mag_key_host(t[i]);
+    if (key > kp[0]) replace_top(kp, ip, len, key, (uint32_t)i);
+  }
+  for (; i + 8 <= n; i += 8) {
+    const __m256i u = _mm256_and_si256(_mm256_loadu_si256(reinterpret_cast<const __m256i*>(t + i)), abs_mask);
+    const __m256i key = _mm256_blendv_epi8(u, nan_key, _mm256_cmpgt_epi32(u, inf));  // keys < 2^31: signed compare
+    uint32_t m = (uint32_t)_mm256_movemask_ps(_mm256_castsi256_ps(_mm256_cmpgt_epi32(key, _mm256_set1_epi32((int)kp[0]))));
+    while (m) {
+      const int j = __builtin_ctz(m);
+      m &= m - 1;
+      const uint32_t kv = mag_key_host(t[i + j]);
+      if (kv > kp[0]) replace_top(kp, ip, len, kv, (uint32_t)(i + j));
+    }
+  }
+  for (; i < n; ++i) {
+    const uint32_t key = mag_key_host(t[i]);
+    if (key > kp[0]) replace_top(kp, ip, len, key, (uint32_t)i);
+  }
+}
+
 }  // namespace
 
 // torch.topk(|t|, k, sorted=False).indices of t[0, n) on the CPU, into out[0, k).  1 <= k <= n < 2^32.
@@ -132,17 +171,13 @@ int torch_topk_select(const float* t, int64_t n, int64_t k, int64_t* out) {
     uint32_t* ip = I.data();
 #ifdef OMF_EXP_TIE_TS
     const auto T0 = std::chrono::steady_clock::now();
-    int64_t nrep = 0;
+    const int64_t nrep = -1;  // (not counted since the AVX2 pass)
 #endif
-    for (int64_t i = k; i < n; ++i) {
-      const uint32_t key = mag_key_host(t[i]);
-      if (key > kp[0]) {  // before(pair i, top): it replaces the top
-#ifdef OMF_EXP_TIE_TS
-        ++nrep;
-#endif
-        replace_top(kp, ip, k, key, (uint32_t)i);
-      }
-    }
+    static const bool avx2 = __builtin_cpu_supports("avx2");
+    if (avx2)
+      heap_pass_avx2(t, k, n, kp, ip, k);
+    else
+      heap_pass_scalar(t, k, n, kp, ip, k);
 #ifdef OMF_EXP_TIE_TS
     const auto T1 = std::chrono::steady_clock::now();
 #endif
