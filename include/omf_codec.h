@@ -24,10 +24,11 @@
  *  - Return value: 0 (OMF_OK) or a negative OMF_E* code; the message for the
  *    calling thread is in omf_last_error().  No C++ exception crosses the ABI.
  *  - Reentrant: no global mutable state.  A plan is driven by one host thread at
- *    a time; its stateful launches (encode, norms, fused PS step) may go to any
- *    stream: a launch on a different stream than the plan's previous one is
- *    ordered after everything enqueued so far on that previous stream (an event
- *    recorded there at the switch, hipStreamWaitEvent), never run concurrently.
+ *    a time; its stateful launches (QSGD encode, norms, fused PS step, Top-K
+ *    duplicate check) may go to any stream: a launch on a different stream than
+ *    the plan's previous one is ordered after everything enqueued so far on
+ *    that previous stream (an event recorded there at the switch,
+ *    hipStreamWaitEvent), never run concurrently.
  *    The previous stream must therefore still exist when the plan moves to
  *    another stream (PyTorch's pooled streams always do): before destroying the
  *    stream of a plan's last stateful launch, call omf_plan_check on it (which
@@ -378,7 +379,9 @@ int omf_topk_check_indices(omf_plan* plan, const int64_t* counts, int64_t* indic
  * than once.  The reference decodes a layer as dense[indices] = values, where numpy keeps the LAST
  * value of a repeated index (global_grpc_compression.py:140-160); the scatter decodes do not, so the
  * Python layer decodes a flagged layer by itself with that rule.  Never true for a selection an
- * encoder produced.  Uses a plan-owned bitmap of arena_end bits (made on first use).  Asynchronous.
+ * encoder produced.  Uses a plan-owned bitmap of arena_end bits (made on first use), so it is one
+ * of the plan's stateful launches: ordered after the previous one when the stream changes.
+ * Asynchronous.
  */
 int omf_topk_check_duplicates(omf_plan* plan, const int64_t* counts, const int64_t* indices, int32_t* flags,
                               void* stream);

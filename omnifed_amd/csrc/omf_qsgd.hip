@@ -1984,6 +1984,9 @@ const std::vector<int64_t>& offsets(const omf_plan* p) { return p->offsets; }
 omf::TopkKnobs& topk_knobs(omf_plan* p) { return p->topk_knobs; }
 // The plan's device error word (omf_plan_check reports and clears it).
 uint32_t* err_word(omf_plan* p) { return reinterpret_cast<uint32_t*>(p->d_sync + 4); }
+// Stream ordering of a stateful launch outside this file (plan_enter / plan_leave).
+int order_enter(omf_plan* p, hipStream_t st) { return plan_enter(p, st); }
+int order_leave(omf_plan* p, hipStream_t st) { return plan_leave(p, st); }
 }  // namespace omf_plan_access
 
 static size_t round16(size_t b) { return (b + 15) & ~(size_t)15; }

@@ -2540,6 +2540,8 @@ void* topk_table(omf_plan* p, uint64_t key, size_t bytes, bool* fresh, uint64_t*
 void* topk_table_counts(omf_plan* p, const int64_t* counts, size_t bytes, bool* fresh, uint64_t** host);
 omf::TopkKnobs& topk_knobs(omf_plan* p);
 uint32_t* err_word(omf_plan* p);
+int order_enter(omf_plan* p, hipStream_t st);
+int order_leave(omf_plan* p, hipStream_t st);
 }  // namespace omf_plan_access
 
 namespace {
@@ -3721,6 +3723,9 @@ int omf_topk_check_duplicates(omf_plan* plan, const int64_t* counts, const int64
   if (ktot == 0) return OMF_OK;
   DecTables tb;
   if (int r = dec_tables(plan, counts, ktot, nullptr, &tb)) return r;
+  // the bitmap is the plan's: a call on another stream than the plan's previous stateful launch
+  // is ordered after it (include/omf_codec.h), so two checks never mark and clear it at once
+  if (int r = omf_plan_access::order_enter(plan, st)) return r;
   constexpr uint64_t kDupTag = 0xD0B1E5B17A9E0000ull;
   const size_t words = (size_t)((omf_plan_access::arena_end(plan) + 31) / 32);
   bool fresh = false;
@@ -3734,7 +3739,7 @@ int omf_topk_check_duplicates(omf_plan* plan, const int64_t* counts, const int64
   hipLaunchKernelGGL(topk_dup_bits<false>, dim3(gx), dim3(kThreads), 0, st, indices, omf_plan_access::d_sizes(plan),
                      omf_plan_access::d_begins(plan), (const int64_t*)tb.koff, (int)nt, ktot, bits, flags);
   OMF_HIP(hipGetLastError());
-  return OMF_OK;
+  return omf_plan_access::order_leave(plan, st);
 }
 
 int omf_topk_decode(const float* values, const int64_t* indices, int64_t k, float* y, int64_t n, int32_t mode,

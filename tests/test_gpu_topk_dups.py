@@ -86,3 +86,45 @@ def test_ps_accumulate_last_value_wins(gpu):
         want = (np.zeros_like(d) + d) + d  # acc += dense per client, fp32
         o = agg.plan.offsets[t]
         assert acc[o:o + d.size].tobytes() == want.tobytes(), n
+
+
+def test_check_duplicates_ordered_across_streams(gpu):
+    """The duplicate check marks and clears a plan-owned bitmap, so it is one of the plan's stateful
+    launches (include/omf_codec.h): a call on another stream waits for the plan's previous one.
+    Stream A queues ~200 ms of spin before its check; stream B's check, issued right after, must
+    complete after A's (not beside it), and both report the same flags."""
+    import time
+    from omnifed_amd import codec
+
+    shapes, msgs, _ = _layers()
+    names = list(shapes)
+    sizes = [int(np.prod(shapes[n])) for n in names]
+    plan = codec.Plan.get(sizes, device=gpu)
+    counts = [msgs[n][1].size for n in names]
+    idx = np.concatenate([np.where(msgs[n][1] < 0, msgs[n][1] + s, msgs[n][1]) for n, s in zip(names, sizes)])
+    indices = torch.from_numpy(idx.astype(np.int64)).to(gpu)
+    want = [1, 0, 1]
+    assert plan.topk_check_duplicates(counts, indices).cpu().tolist() == want  # bitmap made
+    # spin calibration (torch's sleep kernel: cycles per ms)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    torch.cuda._sleep(10_000_000)
+    b.record()
+    torch.cuda.synchronize()
+    cycles_per_ms = 10_000_000 / max(a.elapsed_time(b), 1e-3)
+    sa, sb = torch.cuda.Stream(gpu), torch.cuda.Stream(gpu)
+    with torch.cuda.stream(sa):
+        torch.cuda._sleep(int(200 * cycles_per_ms))
+        fa = plan.topk_check_duplicates(counts, indices, stream=sa.cuda_stream)
+    fb = plan.topk_check_duplicates(counts, indices, stream=sb.cuda_stream)
+    t0 = time.perf_counter()
+    sb.synchronize()
+    wait_ms = (time.perf_counter() - t0) * 1e3
+    a_done = sa.query()
+    torch.cuda.synchronize()
+    assert wait_ms > 100.0 and a_done, (wait_ms, a_done)
+    assert fa.cpu().tolist() == want and fb.cpu().tolist() == want
+    # and back on A with nothing pending: no wait, same flags
+    fc = plan.topk_check_duplicates(counts, indices, stream=sa.cuda_stream)
+    sa.synchronize()
+    assert fc.cpu().tolist() == want
