@@ -120,9 +120,11 @@ def test_check_duplicates_ordered_across_streams(gpu):
     t0 = time.perf_counter()
     sb.synchronize()
     wait_ms = (time.perf_counter() - t0) * 1e3
-    a_done = sa.query()
+    t1 = time.perf_counter()
+    sa.synchronize()  # A's spin and check ended before B's check did: nothing left to wait for
+    rest_ms = (time.perf_counter() - t1) * 1e3
     torch.cuda.synchronize()
-    assert wait_ms > 100.0 and a_done, (wait_ms, a_done)
+    assert wait_ms > 100.0 and rest_ms < 50.0, (wait_ms, rest_ms)
     assert fa.cpu().tolist() == want and fb.cpu().tolist() == want
     # and back on A with nothing pending: no wait, same flags
     fc = plan.topk_check_duplicates(counts, indices, stream=sa.cuda_stream)
